@@ -1,0 +1,259 @@
+"""Generate golden vectors by running the upstream reference (imported read-only).
+
+Run in the build container only (needs /root/reference):
+    python tests/golden/make_golden.py
+Writes small ``.npz`` fixtures next to this file.  Each fixture holds inputs,
+(small) weights or the seed that regenerates them, and the reference's outputs:
+forward output, loss, every gradient, parameters after one AdamW step.  The
+reference's own repo has no tests or fixtures, so these vectors,
+produced by the reference code itself, pin the oracle.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, HERE)
+
+from ref_harness import load_reference  # noqa: E402
+from multimodalreactiongeneration_amd import configs as C  # noqa: E402
+from multimodalreactiongeneration_amd.synthetic import (  # noqa: E402
+    make_batch, make_simple_batch, clone_batch, fill_params_randomstate)
+
+torch.set_num_threads(8)
+R = load_reference()
+
+
+def _np(t):
+    return t.detach().cpu().numpy().astype(np.float32)
+
+
+def pack_batch(out, batch, prefix="in"):
+    for i, (x, n) in enumerate(batch):
+        out[f"{prefix}/{i}/x"] = _np(x)
+        out[f"{prefix}/{i}/len"] = n.numpy().astype(np.int64)
+
+
+def run_train_step(model, batch, out, save_params=True, full_grads=True):
+    """forward output, loss, grads, params after one AdamW step (training_step + optimizer)."""
+    model.train()
+    if save_params:
+        for k, v in model.state_dict().items():
+            out[f"param/{k}"] = _np(v)
+    res = model.training_step(batch)
+    loss = res["loss"]
+    loss.backward()
+    out["loss"] = np.float32(loss.item())
+    for k, p in model.named_parameters():
+        g = p.grad if p.grad is not None else torch.zeros_like(p)
+        if full_grads:
+            out[f"grad/{k}"] = _np(g)
+        else:
+            out[f"gradsum/{k}"] = np.array([g.double().sum().item(),
+                                            (g.double() ** 2).sum().item()], dtype=np.float64)
+    opt = model.configure_optimizers()["optimizer"]
+    opt.step()
+    for k, p in model.named_parameters():
+        if full_grads:
+            out[f"after/{k}"] = _np(p)
+    return out
+
+
+def metaformer_case(name, hidden, nb, enc, bn, B, T, lead, ratio, lengths=None, seed=0,
+                    full_width=False):
+    model_cfg, optim, metrics = C.lstmformer_config(hidden=hidden, num_block=nb,
+                                                    encoder_num_layer=enc, bottleneck=bn,
+                                                    ratio=ratio, lr=1e-3)
+    torch.manual_seed(seed)
+    m = R.Metaformer(model_cfg, optim, metrics)
+    if full_width:
+        fill_params_randomstate(m, seed)
+    batch = make_batch(B=B, T=T, lead=lead, ratio=ratio, seed=1234 + seed, lengths=lengths)
+    out = {"meta/config": json.dumps(dict(model=model_cfg, optim=optim, metrics=metrics))}
+    pack_batch(out, batch)
+    # forward output on the training-step view (self motion padding zeroed, lstmformer.py:365-366)
+    with torch.no_grad():
+        b2 = clone_batch(batch)
+        mask = (b2[2][0] != -100).int()
+        b2[2] = (b2[2][0] * mask, b2[2][1])
+        y, _ = m.forward(*b2[:-1])
+        out["y"] = _np(y)
+        m.eval()
+        y_eval, _ = m.forward(*clone_batch(batch)[:-1])   # eval: raw padding flows (mask AND-rule live)
+        out["y_eval"] = _np(y_eval)
+        m.train()
+    run_train_step(m, clone_batch(batch), out, save_params=not full_width,
+                   full_grads=not full_width)
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    print("wrote", name, "loss", out["loss"])
+
+
+def lstm_with_sample_case(name, hidden, sh, B, T, lead, ratio, scheduled=False, epoch=30,
+                          seed=0, lengths=None):
+    model_cfg, optim, metrics = C.lstm_with_sampling_config(
+        hidden=hidden, sampler_hidden=sh, bottleneck=16, ratio=ratio, lr=1e-3,
+        use_scheduled_sampling=scheduled, max_epochs=60)
+    torch.manual_seed(seed)
+    m = R.LSTMwithSample(model_cfg, optim, metrics)
+    m.current_epoch = epoch
+    batch = make_batch(B=B, T=T, lead=lead, ratio=ratio, seed=1234 + seed, lengths=lengths)
+    out = {"meta/config": json.dumps(dict(model=model_cfg, optim=optim, metrics=metrics)),
+           "meta/epoch": np.int64(epoch)}
+    pack_batch(out, batch)
+    if scheduled:
+        # record the global-RNG sampling mask the reference draws (lstm_with_sample.py:389)
+        rec = {}
+        orig = torch.rand
+
+        def _rand(*a, **k):
+            r = orig(*a, **k)
+            rec.setdefault("mask_rand", r.clone())
+            return r
+        torch.manual_seed(7)
+        torch.rand = _rand
+        try:
+            run_train_step(m, clone_batch(batch), out)
+        finally:
+            torch.rand = orig
+        out["sampling_mask"] = (rec["mask_rand"] < epoch / 60).numpy()
+    else:
+        with torch.no_grad():
+            y, _, _ = m.forward(*clone_batch(batch)[:-1])
+            out["y"] = _np(y)
+        run_train_step(m, clone_batch(batch), out)
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    print("wrote", name, "loss", out["loss"])
+
+
+def simple_lstm_case(name, hidden, lstm, B, T, seed=0):
+    cfg, optim, metrics = C.simple_lstm_config(hidden=hidden, lstm=lstm, bottleneck=8,
+                                               att_heads=4, att_layers=2, enc_layers=2,
+                                               dec_layers=2, mapping=8, lr=1e-3)
+    torch.manual_seed(seed)
+    m = R.SimpleLSTM(cfg, optim, metrics)
+    a, mo, t = make_simple_batch(B=B, T=T, seed=1234 + seed)
+    out = {"meta/config": json.dumps(dict(model=cfg, optim=optim, metrics=metrics)),
+           "in/audio": _np(a), "in/motion": _np(mo), "in/target": _np(t)}
+    with torch.no_grad():
+        out["y"] = _np(m.forward(a, mo))
+    run_train_step(m, (a, mo, t), out)
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    print("wrote", name, "loss", out["loss"])
+
+
+def mask_cases():
+    out = {}
+    rs = np.random.RandomState(5)
+    for i, (tq, tk, heads) in enumerate([(5, 5, 2), (5, 10, 2), (10, 5, 1), (4, 12, 3), (6, 6, 1)]):
+        a = torch.from_numpy(rs.standard_normal((2, tq, 3)).astype(np.float32))
+        b = torch.from_numpy(rs.standard_normal((2, tk, 3)).astype(np.float32))
+        a[1, tq - 2:] = -100
+        b[1, tk - 3:] = -100
+        if i == 4:
+            a[0, 0] = -100      # padded query row at the front
+            b[0, 0] = -100
+        msk = R.gen_attention_mask(a, b, heads, -100)
+        out[f"case{i}/main"] = _np(a)
+        out[f"case{i}/other"] = _np(b)
+        out[f"case{i}/heads"] = np.int64(heads)
+        out[f"case{i}/mask"] = msk.numpy()
+    np.savez_compressed(os.path.join(HERE, "attention_masks.npz"), **out)
+    print("wrote attention_masks")
+
+
+def op_cases():
+    """nn.LSTM / nn.MultiheadAttention exactly as the reference instantiates them."""
+    from torch import nn
+    out = {}
+    torch.manual_seed(3)
+    # uni-directional single layer with h0/c0 (LSTMMixer: mixer_block.py:237-252)
+    lstm = nn.LSTM(24, 32, num_layers=1, batch_first=True)
+    x = torch.randn(3, 7, 24, requires_grad=True)
+    h0 = torch.randn(1, 3, 32, requires_grad=True)
+    c0 = torch.randn(1, 3, 32, requires_grad=True)
+    y, (hT, cT) = lstm(x, (h0, c0))
+    dy = torch.randn_like(y)
+    dhT = torch.randn_like(hT)
+    dcT = torch.randn_like(cT)
+    (y * dy).sum().add((hT * dhT).sum()).add((cT * dcT).sum()).backward()
+    for k, v in lstm.state_dict().items():
+        out[f"lstm1/param/{k}"] = _np(v)
+    for k, p in lstm.named_parameters():
+        out[f"lstm1/grad/{k}"] = _np(p.grad)
+    for nm, t in dict(x=x, h0=h0, c0=c0, y=y, hT=hT, cT=cT, dy=dy, dhT=dhT, dcT=dcT).items():
+        out[f"lstm1/{nm}"] = _np(t)
+    for nm, t in dict(dx=x.grad, dh0=h0.grad, dc0=c0.grad).items():
+        out[f"lstm1/{nm}"] = _np(t)
+    # bi-directional 2-layer (LSTMModule, lstm_block.py:21-28)
+    lstm = nn.LSTM(16, 12, num_layers=2, batch_first=True, bidirectional=True)
+    x = torch.randn(2, 6, 16, requires_grad=True)
+    y, (hT, cT) = lstm(x)
+    dy = torch.randn_like(y)
+    (y * dy).sum().backward()
+    for k, v in lstm.state_dict().items():
+        out[f"lstm2/param/{k}"] = _np(v)
+    for k, p in lstm.named_parameters():
+        out[f"lstm2/grad/{k}"] = _np(p.grad)
+    for nm, t in dict(x=x, y=y, hT=hT, cT=cT, dy=dy, dx=x.grad).items():
+        out[f"lstm2/{nm}"] = _np(t)
+    # cross-attention with the reference's 3-D block-causal + padding mask (for_sequential.py:27-51)
+    for case, (tq, tk, heads, E) in enumerate([(6, 12, 4, 32), (8, 8, 2, 16), (10, 5, 4, 32)]):
+        mha = nn.MultiheadAttention(E, heads, batch_first=True, kdim=E, vdim=E)
+        with torch.no_grad():
+            mha.in_proj_bias.normal_()
+            mha.out_proj.bias.normal_()
+        q = torch.randn(2, tq, E, requires_grad=True)
+        kv = torch.randn(2, tk, E, requires_grad=True)
+        mq, mk = q.detach().clone(), kv.detach().clone()
+        mq[1, tq - 2:] = -100
+        mk[1, tk - 3:] = -100
+        mask = R.gen_attention_mask(mq, mk, heads, -100).view(-1, tq, tk)
+        o, _ = mha(q, kv, kv, None, False, mask, False, False)
+        do = torch.randn_like(o)
+        (o * do).sum().backward()
+        p = f"mha{case}/"
+        for k, v in mha.state_dict().items():
+            out[p + f"param/{k}"] = _np(v)
+        for k, prm in mha.named_parameters():
+            out[p + f"grad/{k}"] = _np(prm.grad)
+        for nm, t in dict(q=q, kv=kv, o=o, do=do, dq=q.grad, dkv=kv.grad).items():
+            out[p + nm] = _np(t)
+        out[p + "mask"] = mask.numpy()
+        out[p + "heads"] = np.int64(heads)
+    np.savez_compressed(os.path.join(HERE, "ops.npz"), **out)
+    print("wrote ops")
+
+
+def state_dict_keys():
+    res = {}
+    mc, o, me = C.lstmformer_config()
+    res["Metaformer"] = {k: list(v.shape) for k, v in R.Metaformer(mc, o, me).state_dict().items()}
+    mc, o, me = C.lstmformer_config(ratio=8)
+    res["Metaformer_r8"] = {k: list(v.shape) for k, v in R.Metaformer(mc, o, me).state_dict().items()}
+    mc, o, me = C.lstm_with_sampling_config()
+    res["LSTMwithSample"] = {k: list(v.shape) for k, v in R.LSTMwithSample(mc, o, me).state_dict().items()}
+    mc, o, me = C.simple_lstm_config()
+    res["SimpleLSTM"] = {k: list(v.shape) for k, v in R.SimpleLSTM(mc, o, me).state_dict().items()}
+    with open(os.path.join(HERE, "state_dict_keys.json"), "w") as f:
+        json.dump(res, f, indent=0)
+    print("wrote state_dict_keys", {k: len(v) for k, v in res.items()})
+
+
+if __name__ == "__main__":
+    mask_cases()
+    op_cases()
+    state_dict_keys()
+    metaformer_case("metaformer_small_r1", 32, 2, 2, 16, B=2, T=10, lead=3, ratio=1)
+    metaformer_case("metaformer_small_r2_pad", 32, 2, 2, 16, B=3, T=8, lead=2, ratio=2,
+                    lengths=[8, 6, 5], seed=1)
+    metaformer_case("metaformer_full_r1", 256, 5, 5, 64, B=2, T=8, lead=0, ratio=1,
+                    seed=2, full_width=True)
+    lstm_with_sample_case("lstm_with_sample_tf", 32, 16, B=2, T=9, lead=2, ratio=2)
+    lstm_with_sample_case("lstm_with_sample_ss", 32, 16, B=2, T=7, lead=3, ratio=2,
+                          scheduled=True, seed=1)
+    simple_lstm_case("simple_lstm_small", 32, 16, B=3, T=9)
