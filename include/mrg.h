@@ -1,0 +1,144 @@
+/*
+ * mrg.h — C-ABI of libmrg.so, the MI355X (gfx950) kernels of the mr_gen
+ * training path.  Plain pointers, sizes and hipStream_t only; no torch types.
+ *
+ * The reference (TUT-SLP-lab/MultimodalReactionGeneration) has no FFI of its
+ * own: its GPU work is stock PyTorch ops.  Each entry point below replaces the
+ * torch op the reference calls at the cited line; the Python drop-in layer
+ * (multimodalreactiongeneration_amd/functional.py) binds them with ctypes.
+ *
+ * Conventions
+ *   - every function returns 0 on success; on failure a non-zero code and a
+ *     message via mrg_last_error() (thread-local);
+ *   - the caller owns every buffer, including workspaces sized by the
+ *     *_bytes() helpers; nothing here allocates device memory or synchronises,
+ *     so calls are legal inside hipGraph capture;
+ *   - all tensors are fp32, row-major; strides are in elements;
+ *   - RowMap operands (lda/lda_hi/a_rdiv): row r lives at
+ *       (r / rdiv) * ld_hi + (r % rdiv) * ld   (rdiv <= 0: r * ld)
+ *     which lets one call walk a [B, T, F] tensor with a time shift or a
+ *     [:, lead:] slice without a copy.
+ */
+#ifndef MRG_H_
+#define MRG_H_
+
+#include <stddef.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+const char* mrg_last_error(void);
+int mrg_version(void);
+int mrg_device_cu_count(int device, int* out);
+
+/* ---------------------------------------------------------------- GEMM
+ * C = epi(alpha * op(A) op(B) + beta * C + bias[n]); epi 0 none, 1 relu,
+ * 2 multiply by (aux[m, n] > 0) (relu backward).  split-K > 1 writes fp32
+ * slabs to `workspace` and reduces them in a fixed order (deterministic).
+ * Replaces nn.Linear / addmm (mixer_block.py:63-74, multi_modal_metaformer.py:
+ * 433-435,474,504, lstm_with_sample.py:92-130) and the x W_ih^T / weight-grad
+ * GEMMs inside cuDNN's LSTM (mixer_block.py:237-252).                      */
+size_t mrg_gemm_workspace_bytes(int M, int N, int splits);
+int mrg_gemm_f32(int M, int N, int K, float alpha,
+                 const float* A, int transA, long lda, long lda_hi, int a_rdiv,
+                 const float* B, int transB, long ldb, long ldb_hi, int b_rdiv,
+                 float beta, float* C, long ldc, const float* bias, int epilogue,
+                 const float* aux, long ldaux, float* workspace, int splits,
+                 hipStream_t stream);
+
+/* out[n] = beta*out[n] + sum_rows X(row, n); out2 (nullable) receives the same
+ * sum (b_ih and b_hh share one gradient).  Bias gradients of every Linear.  */
+size_t mrg_colsum_workspace_bytes(int rows, int N);
+int mrg_colsum_f32(int rows, int N, const float* X, long ld, long ld_hi, int rdiv,
+                   float beta, float* out, float* out2, float* workspace, hipStream_t stream);
+
+/* ---------------------------------------------------------------- LSTM
+ * Persistent recurrence of torch.nn.LSTM (gate order i, f, g, o) given the
+ * input projection gx = x W_ih^T + b_ih.  Replaces the cuDNN RNN behind
+ * LSTMMixer.forward (mixer_block.py:248-252), LSTMModule.forward
+ * (lstm_block.py:38-46) and LSTMSampler.forward (lstm_sampler.py:26-34).
+ * `nprob` (1..4) independent same-shape recurrences share one launch
+ * (e.g. the audio and partner encoders of block 0).  Arrays are indexed by
+ * problem.  xbuf[i] must be zeroed before every call
+ * (mrg_lstm_fwd_xbuf_bytes / mrg_lstm_bwd_xbuf_bytes); *err is OR-ed with 1
+ * if a hand-off spin times out.  H in {16, 32, 64, 128, 256}.            */
+int mrg_lstm_supported_hidden(int H);
+size_t mrg_lstm_fwd_xbuf_bytes(int B, int H);
+size_t mrg_lstm_bwd_xbuf_bytes(int B, int H);
+int mrg_lstm_fwd(int nprob, int B, int T, int H,
+                 const float* const* gx, const long* gx_bs, const long* gx_ts,
+                 const float* const* w_hh, const float* const* b_hh,
+                 const float* const* h0, const float* const* c0,
+                 float* const* y, const long* y_bs, const long* y_ts,
+                 float* const* gates, float* const* cs, float* const* hT, float* const* cT,
+                 const int* reverse, void* const* xbuf, int* err, int cus, int force_bs,
+                 hipStream_t stream);
+/* Backward: dG[B, T, 4H] = d(pre-activation gates); dh0 / dc0 optional. */
+int mrg_lstm_bwd(int nprob, int B, int T, int H,
+                 const float* const* w_hh, const float* const* gates, const float* const* cs,
+                 const float* const* c0, const float* const* dy, const long* dy_bs,
+                 const long* dy_ts, const float* const* dhT, const float* const* dcT,
+                 float* const* dG, float* const* dh0, float* const* dc0, const int* reverse,
+                 void* const* xbuf, int* err, int cus, int force_bs, hipStream_t stream);
+
+/* ---------------------------------------------------------------- attention
+ * Scaled-dot-product core of nn.MultiheadAttention as the reference calls it
+ * (MHAforSequentail.forward, for_sequential.py:42-51;
+ * MultiModalAttentionBlockSequential.forward, multi_modal_att.py:22-31) with
+ * the gen_attention_mask rules (multi_modal_metaformer.py:32-79) evaluated
+ * from indices: causal != 0 selects the block-causal rectangular mask;
+ * qpad/kpad (uint8 [B,Tq]/[B,Tk], nullable) give the padding AND rule.
+ * Element (b, t, head, d) lives at base + b*bs + t*ts + head*D + d.
+ * lse: [B, heads, Tq] log-sum-exp saved for the backward.  D in {8,16,32,64}. */
+int mrg_attention_fwd(int B, int heads, int Tq, int Tk, int D,
+                      const float* q, long q_bs, long q_ts, const float* k, long k_bs, long k_ts,
+                      const float* v, long v_bs, long v_ts, float* o, long o_bs, long o_ts,
+                      float* lse, const unsigned char* qpad, const unsigned char* kpad,
+                      int causal, float scale, hipStream_t stream);
+size_t mrg_attention_bwd_workspace_bytes(int B, int heads, int Tq);
+int mrg_attention_bwd(int B, int heads, int Tq, int Tk, int D,
+                      const float* q, long q_bs, long q_ts, const float* k, long k_bs, long k_ts,
+                      const float* v, long v_bs, long v_ts, const float* o, long o_bs, long o_ts,
+                      const float* lse, const unsigned char* qpad, const unsigned char* kpad,
+                      int causal, float scale, const float* dout, long do_bs, long do_ts,
+                      float* dq, long dq_bs, long dq_ts, float* dk, long dk_bs, long dk_ts,
+                      float* dv, long dv_bs, long dv_ts, float* workspace, hipStream_t stream);
+
+/* ---------------------------------------------------------------- LayerNorm
+ * y = LayerNorm(a + b) (ResidualConnection.forward, residual_connection.py:
+ * 20-37), rows x E, E in {64, 128, 256, 512}; mean/rstd saved per row.     */
+int mrg_residual_layernorm_fwd(int rows, int E, const float* a, const float* b,
+                               const float* gamma, const float* beta, float eps, float* y,
+                               float* mean, float* rstd, hipStream_t stream);
+size_t mrg_residual_layernorm_bwd_workspace_bytes(int rows, int E);
+int mrg_residual_layernorm_bwd(int rows, int E, const float* dy, const float* a, const float* b,
+                               const float* gamma, const float* mean, const float* rstd,
+                               float* dx, float* dgamma, float* dbeta, int accumulate,
+                               float* workspace, hipStream_t stream);
+
+/* ---------------------------------------------------------------- loss
+ * Masked regression loss of training_step (lstmformer.py:372-380,
+ * lossfun :313-325): mask = target != -100, feature scaler from
+ * delta_start; type 0 huber, 1 mse, 2 l1, 3 smoothl1; mean reduction.
+ * y is viewed [B, T, F] with batch stride y_bstride (y[:, lead:] slices). */
+size_t mrg_loss_workspace_bytes(int B, int T, int F);
+int mrg_masked_loss_fwd(int B, int T, int F, const float* y, long y_bstride, const float* target,
+                        int type, float delta, float beta, int mask_padding, int delta_start,
+                        float dscale, float* loss_out, float* workspace, hipStream_t stream);
+int mrg_masked_loss_bwd(int B, int T, int F, const float* y, long y_bstride, const float* target,
+                        int type, float delta, float beta, int mask_padding, int delta_start,
+                        float dscale, const float* grad_out, float* dy, hipStream_t stream);
+
+/* ---------------------------------------------------------------- AdamW
+ * torch.optim.AdamW step over flat buffers (configure_optimizers,
+ * lstmformer.py:327-333).  step_lr = device float[2] {steps done, lr}.     */
+int mrg_adamw_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, long n,
+                   float* step_lr, float weight_decay, float beta1, float beta2, float eps,
+                   hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MRG_H_ */

@@ -1,0 +1,328 @@
+// Row-parallel HBM-bound kernels: fused residual-add + LayerNorm (fwd/bwd),
+// masked regression loss (Huber / MSE / L1 / SmoothL1, fwd/bwd) and the fused
+// multi-tensor AdamW step.  One 64-lane wave owns one row; row reductions are
+// wave shuffles (no LDS); parameter-gradient column sums go through per-block
+// fp32 partials reduced in a fixed order (deterministic).
+#include "mrg_common.h"
+
+namespace mrg {
+
+// ------------------------------------------------------------- residual + LayerNorm
+// y = LN(a + b) * gamma + beta (ResidualConnection, residual_connection.py:20-37)
+template <int EPL>  // elements per lane: E = 64 * EPL
+__global__ __launch_bounds__(256) void resln_fwd_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                        const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                        float* __restrict__ y, float* __restrict__ mean_out,
+                                                        float* __restrict__ rstd_out, int rows, float eps) {
+  constexpr int E = 64 * EPL;
+  int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* pa = a + (long)row * E;
+  const float* pb = b + (long)row * E;
+  float x[EPL];
+  float s = 0.0f;
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) {
+    int c = i * 64 + lane;
+    x[i] = pa[c] + pb[c];
+    s += x[i];
+  }
+  float mean = wave_sum(s) * (1.0f / E);
+  float v = 0.0f;
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) {
+    float d = x[i] - mean;
+    v += d * d;
+  }
+  float var = wave_sum(v) * (1.0f / E);
+  float rstd = rsqrtf(var + eps);
+  float* py = y + (long)row * E;
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) {
+    int c = i * 64 + lane;
+    py[c] = (x[i] - mean) * rstd * gamma[c] + beta[c];
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * gamma
+// per-block partial column sums of dy*xhat and dy -> part[blk][2][E]
+template <int EPL>
+__global__ __launch_bounds__(256) void resln_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ a,
+                                                        const float* __restrict__ b, const float* __restrict__ gamma,
+                                                        const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+                                                        float* __restrict__ dx, float* __restrict__ part,
+                                                        int rows, int rows_per_block) {
+  constexpr int E = 64 * EPL;
+  __shared__ float red[4][2][E];
+  int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float dg[EPL], db[EPL];
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) { dg[i] = 0.0f; db[i] = 0.0f; }
+  int r0 = blockIdx.x * rows_per_block;
+  int r1 = min(rows, r0 + rows_per_block);
+  for (int row = r0 + wave; row < r1; row += 4) {
+    const float* pa = a + (long)row * E;
+    const float* pb = b + (long)row * E;
+    const float* pdy = dy + (long)row * E;
+    float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[EPL], g[EPL];
+    float s1 = 0.0f, s2 = 0.0f;
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) {
+      int c = i * 64 + lane;
+      float d = pdy[c];
+      xh[i] = (pa[c] + pb[c] - mean) * rstd;
+      g[i] = d * gamma[c];
+      s1 += g[i];
+      s2 += g[i] * xh[i];
+      dg[i] += d * xh[i];
+      db[i] += d;
+    }
+    float m1 = wave_sum(s1) * (1.0f / E);
+    float m2 = wave_sum(s2) * (1.0f / E);
+    float* pdx = dx + (long)row * E;
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) pdx[i * 64 + lane] = rstd * (g[i] - m1 - xh[i] * m2);
+  }
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) {
+    red[wave][0][i * 64 + lane] = dg[i];
+    red[wave][1][i * 64 + lane] = db[i];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 2 * E; c += 256) {
+    int k = c / E, e = c % E;
+    float s = red[0][k][e] + red[1][k][e] + red[2][k][e] + red[3][k][e];
+    part[((long)blockIdx.x * 2 + k) * E + e] = s;
+  }
+}
+
+__global__ void resln_param_reduce_kernel(const float* part, int nblk, int E, float* dgamma,
+                                          float* dbeta, int accumulate) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= 2 * E) return;
+  int k = c / E, e = c % E;
+  float s = 0.0f;
+  for (int i = 0; i < nblk; ++i) s += part[((long)i * 2 + k) * E + e];
+  float* out = k == 0 ? dgamma : dbeta;
+  out[e] = accumulate ? out[e] + s : s;
+}
+
+// ------------------------------------------------------------------ loss
+// Masked regression loss over y viewed as [B, T, F] (batch stride ys, time stride F),
+// target contiguous [B, T, F]; lossfun() of lstmformer.py:313-325 with the
+// padding mask and delta scaler of training_step (lstmformer.py:372-380).
+struct LossArgs {
+  const float* y;
+  long ys;
+  const float* t;
+  int B, T, F;
+  int type;  // 0 huber, 1 mse, 2 l1, 3 smoothl1
+  float delta, beta;
+  int mask_padding;
+  int delta_start;
+  float dscale;  // sqrt(delta_loss_scale) for features >= delta_start
+};
+
+__device__ __forceinline__ void loss_elem(const LossArgs& a, long i, float& l, float& g) {
+  int f = i % a.F;
+  long bt = i / a.F;
+  int b = bt / a.T, tt = bt % a.T;
+  float y = a.y[(long)b * a.ys + (long)tt * a.F + f];
+  float t = a.t[i];
+  float m = (a.mask_padding && t == -100.0f) ? 0.0f : 1.0f;
+  float s = f >= a.delta_start ? a.dscale : 1.0f;
+  float d = (y * m) * s - (t * m) * s;
+  float z = fabsf(d);
+  switch (a.type) {
+    case 0:
+      l = z < a.delta ? 0.5f * d * d : a.delta * (z - 0.5f * a.delta);
+      g = d <= -a.delta ? -a.delta : (d >= a.delta ? a.delta : d);
+      break;
+    case 1:
+      l = d * d;
+      g = 2.0f * d;
+      break;
+    case 2:
+      l = z;
+      g = d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f);
+      break;
+    default:
+      l = z < a.beta ? 0.5f * d * d / a.beta : z - 0.5f * a.beta;
+      g = z < a.beta ? d / a.beta : (d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f));
+      break;
+  }
+  g *= s * m;
+}
+
+__global__ __launch_bounds__(256) void loss_fwd_partial_kernel(LossArgs a, float* part) {
+  long n = (long)a.B * a.T * a.F;
+  float acc = 0.0f;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    float l, g;
+    loss_elem(a, i, l, g);
+    acc += l;
+  }
+  __shared__ float red[4];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ void loss_fwd_final_kernel(const float* part, int nblk, float inv_n, float* out) {
+  float acc = 0.0f;
+  for (int i = threadIdx.x; i < nblk; i += 64) acc += part[i];
+  acc = wave_sum(acc);
+  if (threadIdx.x == 0) out[0] = acc * inv_n;
+}
+
+// dy (same strided layout as y) = grad_out * dloss/dy / N
+__global__ __launch_bounds__(256) void loss_bwd_kernel(LossArgs a, const float* grad_out, float inv_n,
+                                                       float* dy) {
+  long n = (long)a.B * a.T * a.F;
+  float go = grad_out[0] * inv_n;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    float l, g;
+    loss_elem(a, i, l, g);
+    int f = i % a.F;
+    long bt = i / a.F;
+    int b = bt / a.T, tt = bt % a.T;
+    dy[(long)b * a.ys + (long)tt * a.F + f] = g * go;
+  }
+}
+
+// ------------------------------------------------------------------ AdamW
+// torch.optim.AdamW (lstmformer.py:327-333), one launch over the flat buffers.
+// step / lr live on the device so a captured graph replays correct bias corrections.
+__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v, long n,
+                                                    const float* __restrict__ step_lr, float wd, float b1,
+                                                    float b2, float eps) {
+  float t = step_lr[0] + 1.0f;
+  float lr = step_lr[1];
+  float bc1 = 1.0f - powf(b1, t);
+  float bc2s = sqrtf(1.0f - powf(b2, t));
+  float step_size = lr / bc1;
+  float decay = 1.0f - lr * wd;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    float gi = g[i];
+    float pi = p[i] * decay;
+    float mi = m[i] + (1.0f - b1) * (gi - m[i]);
+    float vi = v[i] * b2 + (1.0f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    p[i] = pi - step_size * mi / (sqrtf(vi) / bc2s + eps);
+  }
+}
+
+__global__ void adamw_step_inc_kernel(float* step_lr) { step_lr[0] += 1.0f; }
+
+}  // namespace mrg
+
+using namespace mrg;
+
+MRG_API int mrg_residual_layernorm_fwd(int rows, int E, const float* a, const float* b,
+                                       const float* gamma, const float* beta, float eps, float* y,
+                                       float* mean, float* rstd, hipStream_t stream) {
+  if (rows == 0) return 0;
+  dim3 grid((rows + 3) / 4);
+  switch (E) {
+    case 64: resln_fwd_kernel<1><<<grid, 256, 0, stream>>>(a, b, gamma, beta, y, mean, rstd, rows, eps); break;
+    case 128: resln_fwd_kernel<2><<<grid, 256, 0, stream>>>(a, b, gamma, beta, y, mean, rstd, rows, eps); break;
+    case 256: resln_fwd_kernel<4><<<grid, 256, 0, stream>>>(a, b, gamma, beta, y, mean, rstd, rows, eps); break;
+    case 512: resln_fwd_kernel<8><<<grid, 256, 0, stream>>>(a, b, gamma, beta, y, mean, rstd, rows, eps); break;
+    default: set_error("mrg_residual_layernorm_fwd: unsupported E=%d", E); return 2;
+  }
+  return check_launch("resln_fwd_kernel");
+}
+
+MRG_API size_t mrg_residual_layernorm_bwd_workspace_bytes(int rows, int E) {
+  int nblk = (rows + 127) / 128;
+  return (size_t)nblk * 2 * E * sizeof(float);
+}
+
+MRG_API int mrg_residual_layernorm_bwd(int rows, int E, const float* dy, const float* a,
+                                       const float* b, const float* gamma, const float* mean,
+                                       const float* rstd, float* dx, float* dgamma, float* dbeta,
+                                       int accumulate, float* workspace, hipStream_t stream) {
+  if (rows == 0) return 0;
+  const int rpb = 128;
+  int nblk = (rows + rpb - 1) / rpb;
+  switch (E) {
+    case 64: resln_bwd_kernel<1><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, rpb); break;
+    case 128: resln_bwd_kernel<2><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, rpb); break;
+    case 256: resln_bwd_kernel<4><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, rpb); break;
+    case 512: resln_bwd_kernel<8><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, rpb); break;
+    default: set_error("mrg_residual_layernorm_bwd: unsupported E=%d", E); return 2;
+  }
+  if (check_launch("resln_bwd_kernel")) return 1;
+  resln_param_reduce_kernel<<<(2 * E + 255) / 256, 256, 0, stream>>>(workspace, nblk, E, dgamma, dbeta,
+                                                                     accumulate);
+  return check_launch("resln_param_reduce_kernel");
+}
+
+static LossArgs make_loss_args(int B, int T, int F, const float* y, long y_bstride, const float* t,
+                               int type, float delta, float beta, int mask_padding, int delta_start,
+                               float dscale) {
+  LossArgs a;
+  a.y = y; a.ys = y_bstride; a.t = t; a.B = B; a.T = T; a.F = F; a.type = type;
+  a.delta = delta; a.beta = beta; a.mask_padding = mask_padding; a.delta_start = delta_start;
+  a.dscale = dscale;
+  return a;
+}
+
+static int loss_blocks(long n) {
+  long b = (n + 255) / 256;
+  return (int)(b < 1024 ? (b < 1 ? 1 : b) : 1024);
+}
+
+MRG_API size_t mrg_loss_workspace_bytes(int B, int T, int F) {
+  return (size_t)loss_blocks((long)B * T * F) * sizeof(float);
+}
+
+MRG_API int mrg_masked_loss_fwd(int B, int T, int F, const float* y, long y_bstride, const float* target,
+                                int type, float delta, float beta, int mask_padding, int delta_start,
+                                float dscale, float* loss_out, float* workspace, hipStream_t stream) {
+  MRG_REQUIRE(type >= 0 && type <= 3, "mrg_masked_loss_fwd: bad loss type %d", type);
+  long n = (long)B * T * F;
+  if (n == 0) return 0;
+  LossArgs a = make_loss_args(B, T, F, y, y_bstride, target, type, delta, beta, mask_padding,
+                              delta_start, dscale);
+  int nb = loss_blocks(n);
+  loss_fwd_partial_kernel<<<nb, 256, 0, stream>>>(a, workspace);
+  if (check_launch("loss_fwd_partial_kernel")) return 1;
+  loss_fwd_final_kernel<<<1, 64, 0, stream>>>(workspace, nb, 1.0f / (float)n, loss_out);
+  return check_launch("loss_fwd_final_kernel");
+}
+
+MRG_API int mrg_masked_loss_bwd(int B, int T, int F, const float* y, long y_bstride, const float* target,
+                                int type, float delta, float beta, int mask_padding, int delta_start,
+                                float dscale, const float* grad_out, float* dy, hipStream_t stream) {
+  long n = (long)B * T * F;
+  if (n == 0) return 0;
+  LossArgs a = make_loss_args(B, T, F, y, y_bstride, target, type, delta, beta, mask_padding,
+                              delta_start, dscale);
+  loss_bwd_kernel<<<loss_blocks(n), 256, 0, stream>>>(a, grad_out, 1.0f / (float)n, dy);
+  return check_launch("loss_bwd_kernel");
+}
+
+// step_lr: device float[2] = {completed steps, lr}; incremented after the update.
+MRG_API int mrg_adamw_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, long n,
+                           float* step_lr, float weight_decay, float beta1, float beta2, float eps,
+                           hipStream_t stream) {
+  if (n > 0) {
+    long nb = (n + 255) / 256;
+    int grid = (int)(nb < 4096 ? nb : 4096);
+    adamw_kernel<<<grid, 256, 0, stream>>>(params, grads, exp_avg, exp_avg_sq, n, step_lr, weight_decay,
+                                           beta1, beta2, eps);
+    if (check_launch("adamw_kernel")) return 1;
+  }
+  adamw_step_inc_kernel<<<1, 1, 0, stream>>>(step_lr);
+  return check_launch("adamw_step_inc_kernel");
+}

@@ -1,0 +1,591 @@
+"""Autograd functions of the MI355X path; every FLOP runs in libmrg.so (include/mrg.h).
+
+torch is used for device memory (caching allocator), the current HIP stream
+and the autograd graph only.  Parameter gradients are written straight into
+``param.grad`` by the fused backward GEMMs (beta = 1 accumulation; the
+functions return ``None`` for parameters), so a step needs no per-parameter
+gradient copies and a flat gradient buffer (optim.FusedAdamW, ddp.GradReducer)
+sees them in place.
+
+Reference ops replaced (file:line in /root/reference):
+  linear / FFN        nn.Linear + ReLU            mixer_block.py:37-87, lstm_block.py:88-96
+  lstm                nn.LSTM (cuDNN RNN)         mixer_block.py:237-252, lstm_block.py:21-46,
+                                                  lstm_sampler.py:16-34
+  mha                 nn.MultiheadAttention       for_sequential.py:27-51, multi_modal_att.py:12-31
+  residual_layernorm  ResidualConnection          residual_connection.py:20-37
+  masked_loss         training_step / lossfun     lstmformer.py:313-325,372-380
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import List, Optional, Sequence
+
+import torch
+from torch.autograd import Function
+
+from . import _lib
+
+F32 = 4
+_ERR = {}
+
+
+def _ptr(t: Optional[torch.Tensor], elem_offset: int = 0):
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr() + elem_offset * t.element_size())
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _ws(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(max(1, (int(nbytes) + 3) // 4), dtype=torch.float32, device=device)
+
+
+def _err_flag(device) -> torch.Tensor:
+    key = torch.device(device).index or 0
+    if key not in _ERR:
+        _ERR[key] = torch.zeros(1, dtype=torch.int32, device=device)
+    return _ERR[key]
+
+
+def check_errors(device=None):
+    """Synchronise and raise if a persistent kernel reported a hand-off timeout."""
+    for k, t in _ERR.items():
+        if device is not None and (torch.device(device).index or 0) != k:
+            continue
+        if int(t.item()) != 0:
+            t.zero_()
+            raise RuntimeError("libmrg: LSTM recurrence hand-off timed out (grid not co-resident?)")
+
+
+def _gbuf(p: torch.Tensor) -> Optional[torch.Tensor]:
+    """The tensor a parameter's gradient accumulates into (created zero-filled on first use)."""
+    if p is None or not p.requires_grad:
+        return None
+    if p.grad is None:
+        p.grad = torch.zeros_like(p)
+    return p.grad
+
+
+def gemm(M, N, K, A, transA, lda, B, transB, ldb, C, ldc, *, alpha=1.0, beta=0.0, bias=None,
+         epi=0, aux=None, ldaux=0, a_hi=0, a_div=0, b_hi=0, b_div=0, splits=1, device=None):
+    """C = epi(alpha op(A) op(B) + beta C + bias); A/B/C/bias/aux are ctypes pointers."""
+    if M == 0 or N == 0:
+        return
+    lib = _lib.load()
+    ws = None
+    if splits > 1:
+        ws = _ws(lib.mrg_gemm_workspace_bytes(M, N, splits), device)
+    rc = lib.mrg_gemm_f32(M, N, K, alpha, A, transA, lda, a_hi, a_div, B, transB, ldb, b_hi, b_div,
+                          beta, C, ldc, bias, epi, aux, ldaux, _ptr(ws), splits, _stream())
+    _lib.check(rc, "gemm")
+
+
+def wgrad_splits(M, N, K):
+    """split-K factor for weight-gradient GEMMs (small M x N output, long B*T reduction)."""
+    tiles = ((M + 63) // 64) * ((N + 63) // 64)
+    s = max(1, 512 // max(1, tiles))
+    return int(max(1, min(s, K // 256, 64)))
+
+
+def colsum(rows, N, X, ld, out, *, out2=None, beta=1.0, ld_hi=0, rdiv=0, device=None):
+    if N == 0:
+        return
+    lib = _lib.load()
+    ws = _ws(lib.mrg_colsum_workspace_bytes(rows, N), device)
+    _lib.check(lib.mrg_colsum_f32(rows, N, X, ld, ld_hi, rdiv, beta, out, out2, _ptr(ws), _stream()),
+               "colsum")
+
+
+def _wgrad(dY, ldy, X, ldx, rows, Nout, Nin, gw, device, *, dy_hi=0, dy_div=0, x_hi=0, x_div=0):
+    """gw[Nout, Nin] += sum_rows dY[row, :]^T X[row, :]."""
+    gemm(Nout, Nin, rows, dY, 1, ldy, X, 0, ldx, _ptr(gw), Nin, beta=1.0, a_hi=dy_hi, a_div=dy_div,
+         b_hi=x_hi, b_div=x_div, splits=wgrad_splits(Nout, Nin, rows), device=device)
+
+
+# ------------------------------------------------------------------ Linear
+class _LinearFn(Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        _lib.require_device(x)
+        In, N = w.shape[1], w.shape[0]
+        x2 = x.reshape(-1, In).contiguous()
+        M = x2.shape[0]
+        y = torch.empty(M, N, device=x.device, dtype=torch.float32)
+        gemm(M, N, In, _ptr(x2), 0, In, _ptr(w), 1, In, _ptr(y), N, bias=_ptr(b), device=x.device)
+        ctx.save_for_backward(x2, w, b)
+        ctx.xshape = x.shape
+        return y.view(*x.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, b = ctx.saved_tensors
+        N, In = w.shape
+        dy2 = dy.reshape(-1, N).contiguous()
+        M = dy2.shape[0]
+        dev = dy.device
+        gw = _gbuf(w)
+        if gw is not None:
+            _wgrad(_ptr(dy2), N, _ptr(x2), In, M, N, In, gw, dev)
+        gb = _gbuf(b)
+        if gb is not None:
+            colsum(M, N, _ptr(dy2), N, _ptr(gb), device=dev)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(M, In, device=dev, dtype=torch.float32)
+            gemm(M, In, N, _ptr(dy2), 0, N, _ptr(w), 0, In, _ptr(dx), In, device=dev)
+            dx = dx.view(ctx.xshape)
+        return dx, None, None
+
+
+def linear(x, weight, bias=None):
+    return _LinearFn.apply(x, weight, bias)
+
+
+# ------------------------------------------------------------------ FFN (Linear -> ReLU -> Linear)
+class _FFNFn(Function):
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        _lib.require_device(x)
+        In, Hb, N = w1.shape[1], w1.shape[0], w2.shape[0]
+        x2 = x.reshape(-1, In).contiguous()
+        M = x2.shape[0]
+        dev = x.device
+        h = torch.empty(M, Hb, device=dev, dtype=torch.float32)
+        gemm(M, Hb, In, _ptr(x2), 0, In, _ptr(w1), 1, In, _ptr(h), Hb, bias=_ptr(b1), epi=1, device=dev)
+        z = torch.empty(M, N, device=dev, dtype=torch.float32)
+        gemm(M, N, Hb, _ptr(h), 0, Hb, _ptr(w2), 1, Hb, _ptr(z), N, bias=_ptr(b2), device=dev)
+        ctx.save_for_backward(x2, h, w1, b1, w2, b2)
+        ctx.xshape = x.shape
+        return z.view(*x.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dz):
+        x2, h, w1, b1, w2, b2 = ctx.saved_tensors
+        Hb, In = w1.shape
+        N = w2.shape[0]
+        dz2 = dz.reshape(-1, N).contiguous()
+        M = dz2.shape[0]
+        dev = dz.device
+        # d(pre-activation) = (dz W2) * (h > 0): relu backward fused into the GEMM epilogue
+        dh = torch.empty(M, Hb, device=dev, dtype=torch.float32)
+        gemm(M, Hb, N, _ptr(dz2), 0, N, _ptr(w2), 0, Hb, _ptr(dh), Hb, epi=2, aux=_ptr(h), ldaux=Hb,
+             device=dev)
+        g = _gbuf(w2)
+        if g is not None:
+            _wgrad(_ptr(dz2), N, _ptr(h), Hb, M, N, Hb, g, dev)
+        g = _gbuf(b2)
+        if g is not None:
+            colsum(M, N, _ptr(dz2), N, _ptr(g), device=dev)
+        g = _gbuf(w1)
+        if g is not None:
+            _wgrad(_ptr(dh), Hb, _ptr(x2), In, M, Hb, In, g, dev)
+        g = _gbuf(b1)
+        if g is not None:
+            colsum(M, Hb, _ptr(dh), Hb, _ptr(g), device=dev)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(M, In, device=dev, dtype=torch.float32)
+            gemm(M, In, Hb, _ptr(dh), 0, Hb, _ptr(w1), 0, In, _ptr(dx), In, device=dev)
+            dx = dx.view(ctx.xshape)
+        return dx, None, None, None, None
+
+
+def ffn(x, w1, b1, w2, b2):
+    return _FFNFn.apply(x, w1, b1, w2, b2)
+
+
+# ------------------------------------------------------------------ residual + LayerNorm
+class _ResLNFn(Function):
+    @staticmethod
+    def forward(ctx, a, b, gamma, beta, eps):
+        _lib.require_device(a)
+        E = a.shape[-1]
+        a2 = a.reshape(-1, E).contiguous()
+        b2 = b.reshape(-1, E).contiguous()
+        rows = a2.shape[0]
+        dev = a.device
+        y = torch.empty_like(a2)
+        mean = torch.empty(rows, device=dev, dtype=torch.float32)
+        rstd = torch.empty(rows, device=dev, dtype=torch.float32)
+        _lib.check(_lib.load().mrg_residual_layernorm_fwd(rows, E, _ptr(a2), _ptr(b2), _ptr(gamma),
+                                                          _ptr(beta), eps, _ptr(y), _ptr(mean),
+                                                          _ptr(rstd), _stream()), "layernorm fwd")
+        ctx.save_for_backward(a2, b2, gamma, beta, mean, rstd)
+        ctx.shape = a.shape
+        return y.view(a.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        a2, b2, gamma, beta, mean, rstd = ctx.saved_tensors
+        rows, E = a2.shape
+        dev = dy.device
+        dy2 = dy.reshape(-1, E).contiguous()
+        dx = torch.empty_like(a2)
+        lib = _lib.load()
+        ws = _ws(lib.mrg_residual_layernorm_bwd_workspace_bytes(rows, E), dev)
+        gg, gb = _gbuf(gamma), _gbuf(beta)
+        scratch = None
+        if gg is None or gb is None:
+            scratch = torch.empty(2, E, device=dev, dtype=torch.float32)
+        _lib.check(lib.mrg_residual_layernorm_bwd(
+            rows, E, _ptr(dy2), _ptr(a2), _ptr(b2), _ptr(gamma), _ptr(mean), _ptr(rstd), _ptr(dx),
+            _ptr(gg if gg is not None else scratch[0]), _ptr(gb if gb is not None else scratch[1]),
+            1, _ptr(ws), _stream()), "layernorm bwd")
+        dx = dx.view(ctx.shape)
+        return dx, dx, None, None, None
+
+
+def residual_layernorm(y, x, gamma, beta, eps=1e-5):
+    """LayerNorm(y + x) — ResidualConnection with use_layer_norm (residual_connection.py:29-31)."""
+    return _ResLNFn.apply(y, x, gamma, beta, eps)
+
+
+# ------------------------------------------------------------------ LSTM
+class _LSTMFn(Function):
+    """``nprob`` same-shape single-layer LSTM directions in one persistent launch.
+
+    tensors = [x, w_ih, w_hh, b_ih, b_hh, h0, c0] * nprob (h0/c0 may be None).
+    concat: all problems share x and write one [B, T, nprob*H] output
+    (bidirectional layer: forward then reverse, like nn.LSTM).
+    Outputs: (y...) then (hT_i, cT_i) per problem.
+    """
+
+    @staticmethod
+    def forward(ctx, spec, *tensors):
+        nprob, concat, reverse, force_bs = spec
+        probs = [tensors[7 * i:7 * i + 7] for i in range(nprob)]
+        x0 = probs[0][0]
+        _lib.require_device(x0)
+        dev = x0.device
+        B, T, In = x0.shape
+        H = probs[0][2].shape[1]
+        lib = _lib.load()
+        if not lib.mrg_lstm_supported_hidden(H):
+            raise RuntimeError(f"LSTM hidden size {H} not supported by libmrg (16/32/64/128/256)")
+        xs = [p[0].contiguous() for p in probs]
+        gxs, ys, y_ptrs, y_bs, y_ts = [], [], [], [], []
+        if concat:
+            ycat = torch.empty(B, T, nprob * H, device=dev, dtype=torch.float32)
+        for i, p in enumerate(probs):
+            x, w_ih, b_ih = xs[i], p[1], p[3]
+            In_i = x.shape[2]
+            gx = torch.empty(B, T, 4 * H, device=dev, dtype=torch.float32)
+            gemm(B * T, 4 * H, In_i, _ptr(x), 0, In_i, _ptr(w_ih), 1, In_i, _ptr(gx), 4 * H,
+                 bias=_ptr(b_ih), device=dev)
+            gxs.append(gx)
+            if concat:
+                y_ptrs.append(_ptr(ycat, i * H))
+                y_bs.append(T * nprob * H)
+                y_ts.append(nprob * H)
+            else:
+                y = torch.empty(B, T, H, device=dev, dtype=torch.float32)
+                ys.append(y)
+                y_ptrs.append(_ptr(y))
+                y_bs.append(T * H)
+                y_ts.append(H)
+        gates = [torch.empty(B, T, 4 * H, device=dev, dtype=torch.float32) for _ in range(nprob)]
+        cs = [torch.empty(B, T, H, device=dev, dtype=torch.float32) for _ in range(nprob)]
+        hT = [torch.empty(B, H, device=dev, dtype=torch.float32) for _ in range(nprob)]
+        cT = [torch.empty(B, H, device=dev, dtype=torch.float32) for _ in range(nprob)]
+        xb_elems = lib.mrg_lstm_fwd_xbuf_bytes(B, H) // 8
+        xbuf = torch.zeros(nprob, xb_elems, dtype=torch.int64, device=dev)
+        h0 = [None if p[5] is None else p[5].contiguous() for p in probs]
+        c0 = [None if p[6] is None else p[6].contiguous() for p in probs]
+
+        def arr(ctype, vals):
+            return (ctype * nprob)(*vals)
+        VP = ctypes.c_void_p
+        rc = lib.mrg_lstm_fwd(
+            nprob, B, T, H,
+            arr(VP, [_ptr(g) for g in gxs]), arr(ctypes.c_long, [T * 4 * H] * nprob),
+            arr(ctypes.c_long, [4 * H] * nprob),
+            arr(VP, [_ptr(p[2]) for p in probs]), arr(VP, [_ptr(p[4]) for p in probs]),
+            arr(VP, [_ptr(h) for h in h0]), arr(VP, [_ptr(c) for c in c0]),
+            arr(VP, y_ptrs), arr(ctypes.c_long, y_bs), arr(ctypes.c_long, y_ts),
+            arr(VP, [_ptr(g) for g in gates]), arr(VP, [_ptr(c) for c in cs]),
+            arr(VP, [_ptr(h) for h in hT]), arr(VP, [_ptr(c) for c in cT]),
+            arr(ctypes.c_int, [int(r) for r in reverse]),
+            arr(VP, [_ptr(xbuf[i]) for i in range(nprob)]), _ptr(_err_flag(dev)),
+            _lib.cu_count(dev.index or 0), force_bs, _stream())
+        _lib.check(rc, "lstm fwd")
+        ctx.spec = (nprob, concat, tuple(reverse), force_bs, B, T, H)
+        ctx.has_h0 = [h is not None for h in h0]
+        ctx.has_c0 = [c is not None for c in c0]
+        ctx.y_layout = (y_bs, y_ts)
+        yout = [ycat] if concat else ys
+        save = []
+        for i, p in enumerate(probs):
+            save += [xs[i], p[1], p[2], p[3], p[4], gates[i], cs[i], h0[i], c0[i]]
+        save += yout
+        ctx.save_for_backward(*save)
+        ctx.shared_x = [any(probs[i][0] is probs[k][0] for k in range(i)) for i in range(nprob)]
+        outs = list(yout)
+        for i in range(nprob):
+            outs += [hT[i], cT[i]]
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        nprob, concat, reverse, force_bs, B, T, H = ctx.spec
+        saved = ctx.saved_tensors
+        per = [saved[9 * i:9 * i + 9] for i in range(nprob)]
+        yout = saved[9 * nprob:]
+        dev = yout[0].device
+        lib = _lib.load()
+        ny = 1 if concat else nprob
+        gy = list(grads[:ny])
+        gstate = grads[ny:]
+        y_bs, y_ts = ctx.y_layout
+        dy_ptr, dy_bs, dy_ts = [], [], []
+        for i in range(nprob):
+            g = gy[0] if concat else gy[i]
+            if g is None:
+                dy_ptr.append(None)
+                dy_bs.append(0)
+                dy_ts.append(0)
+            else:
+                g = g.contiguous()
+                if concat:
+                    gy[0] = g
+                    dy_ptr.append(_ptr(g, i * H))
+                else:
+                    gy[i] = g
+                    dy_ptr.append(_ptr(g))
+                dy_bs.append(y_bs[i])
+                dy_ts.append(y_ts[i])
+        dhT = [None if gstate[2 * i] is None else gstate[2 * i].contiguous() for i in range(nprob)]
+        dcT = [None if gstate[2 * i + 1] is None else gstate[2 * i + 1].contiguous() for i in range(nprob)]
+        dG = [torch.empty(B, T, 4 * H, device=dev, dtype=torch.float32) for _ in range(nprob)]
+        need = ctx.needs_input_grad  # index 0 is spec
+        dh0 = [torch.empty(B, H, device=dev, dtype=torch.float32)
+               if ctx.has_h0[i] and need[1 + 7 * i + 5] else None for i in range(nprob)]
+        dc0 = [torch.empty(B, H, device=dev, dtype=torch.float32)
+               if ctx.has_c0[i] and need[1 + 7 * i + 6] else None for i in range(nprob)]
+        xb_elems = lib.mrg_lstm_bwd_xbuf_bytes(B, H) // 8
+        xbuf = torch.zeros(nprob, xb_elems, dtype=torch.int64, device=dev)
+
+        def arr(ctype, vals):
+            return (ctype * nprob)(*vals)
+        VP = ctypes.c_void_p
+        rc = lib.mrg_lstm_bwd(
+            nprob, B, T, H,
+            arr(VP, [_ptr(p[2]) for p in per]), arr(VP, [_ptr(p[5]) for p in per]),
+            arr(VP, [_ptr(p[6]) for p in per]), arr(VP, [_ptr(p[8]) for p in per]),
+            arr(VP, dy_ptr), arr(ctypes.c_long, dy_bs), arr(ctypes.c_long, dy_ts),
+            arr(VP, [_ptr(t) for t in dhT]), arr(VP, [_ptr(t) for t in dcT]),
+            arr(VP, [_ptr(t) for t in dG]), arr(VP, [_ptr(t) for t in dh0]),
+            arr(VP, [_ptr(t) for t in dc0]), arr(ctypes.c_int, [int(r) for r in reverse]),
+            arr(VP, [_ptr(xbuf[i]) for i in range(nprob)]), _ptr(_err_flag(dev)),
+            _lib.cu_count(dev.index or 0), force_bs, _stream())
+        _lib.check(rc, "lstm bwd")
+
+        out = [None]
+        dx_first = None
+        for i in range(nprob):
+            x, w_ih, w_hh, b_ih, b_hh, _g, _c, h0, _c0 = per[i]
+            In = x.shape[2]
+            g = dG[i]
+            rows = B * T
+            gw = _gbuf(w_hh)
+            if gw is not None and T > 1:
+                # sum_t dG_t^T h_{t-1}: forward dir pairs (dG[t], y[t-1]); reverse (dG[t], y[t+1])
+                yb = yout[0] if concat else yout[i]
+                yoff = i * H if concat else 0
+                a_off = 0 if reverse[i] else 4 * H
+                b_off = yoff + (y_ts[i] if reverse[i] else 0)
+                _wgrad(_ptr(g, a_off), 4 * H, _ptr(yb, b_off), y_ts[i], B * (T - 1), 4 * H, H, gw, dev,
+                       dy_hi=T * 4 * H, dy_div=T - 1, x_hi=y_bs[i], x_div=T - 1)
+            if gw is not None and h0 is not None:
+                t0 = T - 1 if reverse[i] else 0
+                gemm(4 * H, H, B, _ptr(g, t0 * 4 * H), 1, T * 4 * H, _ptr(h0), 0, H, _ptr(gw), H,
+                     beta=1.0, device=dev)
+            gw = _gbuf(w_ih)
+            if gw is not None:
+                _wgrad(_ptr(g), 4 * H, _ptr(x), In, rows, 4 * H, In, gw, dev)
+            gbi, gbh = _gbuf(b_ih), _gbuf(b_hh)
+            if gbi is not None or gbh is not None:
+                first = gbi if gbi is not None else gbh
+                second = gbh if gbi is not None else None
+                colsum(rows, 4 * H, _ptr(g), 4 * H, _ptr(first), out2=_ptr(second), device=dev)
+            dx = None
+            if need[1 + 7 * i]:
+                if ctx.shared_x[i] and dx_first is not None:
+                    gemm(rows, In, 4 * H, _ptr(g), 0, 4 * H, _ptr(w_ih), 0, In, _ptr(dx_first), In,
+                         beta=1.0, device=dev)
+                else:
+                    dx = torch.empty(B, T, In, device=dev, dtype=torch.float32)
+                    gemm(rows, In, 4 * H, _ptr(g), 0, 4 * H, _ptr(w_ih), 0, In, _ptr(dx), In, device=dev)
+                    if dx_first is None:
+                        dx_first = dx
+            out += [dx, None, None, None, None, dh0[i], dc0[i]]
+        return tuple(out)
+
+
+def lstm_layer(x, w_ih, w_hh, b_ih, b_hh, h0=None, c0=None, reverse=False, force_bs=0):
+    """One direction of one nn.LSTM layer (batch_first).  Returns (y, hT, cT)."""
+    y, hT, cT = _LSTMFn.apply((1, False, (reverse,), force_bs), x, w_ih, w_hh, b_ih, b_hh, h0, c0)
+    return y, hT, cT
+
+
+def lstm_layers_batched(problems: Sequence[Sequence], force_bs=0):
+    """Several independent same-shape unidirectional layers in ONE persistent launch.
+
+    problems: [(x, w_ih, w_hh, b_ih, b_hh)] -> [y_i]; zero initial state.
+    """
+    flat = []
+    for x, w_ih, w_hh, b_ih, b_hh in problems:
+        flat += [x, w_ih, w_hh, b_ih, b_hh, None, None]
+    n = len(problems)
+    outs = _LSTMFn.apply((n, False, (False,) * n, force_bs), *flat)
+    return list(outs[:n])
+
+
+def lstm_bidirectional_layer(x, fw, bw, h0=None, c0=None, force_bs=0):
+    """One bidirectional nn.LSTM layer: fw/bw = (w_ih, w_hh, b_ih, b_hh); returns (y[B,T,2H], hT[2,B,H], cT)."""
+    h0f = h0b = c0f = c0b = None
+    if h0 is not None:
+        h0f, h0b = h0[0], h0[1]
+    if c0 is not None:
+        c0f, c0b = c0[0], c0[1]
+    outs = _LSTMFn.apply((2, True, (False, True), force_bs), x, *fw, h0f, c0f, x, *bw, h0b, c0b)
+    y, hTf, cTf, hTb, cTb = outs
+    return y, torch.stack([hTf, hTb]), torch.stack([cTf, cTb])
+
+
+# ------------------------------------------------------------------ multi-head attention
+class _MHAFn(Function):
+    @staticmethod
+    def forward(ctx, spec, q_in, kv_in, in_w, in_b, out_w, out_b, qpad, kpad):
+        heads, causal = spec
+        _lib.require_device(q_in)
+        dev = q_in.device
+        B, Tq, E = q_in.shape
+        Tk = kv_in.shape[1]
+        D = E // heads
+        q2 = q_in.contiguous()
+        kv2 = kv_in.contiguous()
+        Q = torch.empty(B, Tq, E, device=dev, dtype=torch.float32)
+        gemm(B * Tq, E, E, _ptr(q2), 0, E, _ptr(in_w), 1, E, _ptr(Q), E, bias=_ptr(in_b), device=dev)
+        KV = torch.empty(B, Tk, 2 * E, device=dev, dtype=torch.float32)
+        gemm(B * Tk, 2 * E, E, _ptr(kv2), 0, E, _ptr(in_w, E * E), 1, E, _ptr(KV), 2 * E,
+             bias=_ptr(in_b, E), device=dev)
+        O = torch.empty(B, Tq, E, device=dev, dtype=torch.float32)
+        lse = torch.empty(B, heads, Tq, device=dev, dtype=torch.float32)
+        scale = 1.0 / math.sqrt(D)
+        lib = _lib.load()
+        _lib.check(lib.mrg_attention_fwd(B, heads, Tq, Tk, D, _ptr(Q), Tq * E, E, _ptr(KV), Tk * 2 * E,
+                                         2 * E, _ptr(KV, E), Tk * 2 * E, 2 * E, _ptr(O), Tq * E, E,
+                                         _ptr(lse), _ptr(qpad), _ptr(kpad), int(causal), scale,
+                                         _stream()), "attention fwd")
+        out = torch.empty(B, Tq, E, device=dev, dtype=torch.float32)
+        gemm(B * Tq, E, E, _ptr(O), 0, E, _ptr(out_w), 1, E, _ptr(out), E, bias=_ptr(out_b), device=dev)
+        ctx.save_for_backward(q2, kv2, Q, KV, O, lse, in_w, in_b, out_w, out_b, qpad, kpad)
+        ctx.spec = (heads, causal, scale)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q2, kv2, Q, KV, O, lse, in_w, in_b, out_w, out_b, qpad, kpad = ctx.saved_tensors
+        heads, causal, scale = ctx.spec
+        B, Tq, E = q2.shape
+        Tk = kv2.shape[1]
+        D = E // heads
+        dev = dout.device
+        lib = _lib.load()
+        do2 = dout.contiguous()
+        dO = torch.empty(B, Tq, E, device=dev, dtype=torch.float32)
+        gemm(B * Tq, E, E, _ptr(do2), 0, E, _ptr(out_w), 0, E, _ptr(dO), E, device=dev)
+        g = _gbuf(out_w)
+        if g is not None:
+            _wgrad(_ptr(do2), E, _ptr(O), E, B * Tq, E, E, g, dev)
+        g = _gbuf(out_b)
+        if g is not None:
+            colsum(B * Tq, E, _ptr(do2), E, _ptr(g), device=dev)
+        dQ = torch.empty(B, Tq, E, device=dev, dtype=torch.float32)
+        dKV = torch.empty(B, Tk, 2 * E, device=dev, dtype=torch.float32)
+        ws = _ws(lib.mrg_attention_bwd_workspace_bytes(B, heads, Tq), dev)
+        _lib.check(lib.mrg_attention_bwd(
+            B, heads, Tq, Tk, D, _ptr(Q), Tq * E, E, _ptr(KV), Tk * 2 * E, 2 * E, _ptr(KV, E), Tk * 2 * E,
+            2 * E, _ptr(O), Tq * E, E, _ptr(lse), _ptr(qpad), _ptr(kpad), int(causal), scale,
+            _ptr(dO), Tq * E, E, _ptr(dQ), Tq * E, E, _ptr(dKV), Tk * 2 * E, 2 * E, _ptr(dKV, E),
+            Tk * 2 * E, 2 * E, _ptr(ws), _stream()), "attention bwd")
+        gw = _gbuf(in_w)
+        if gw is not None:
+            _wgrad(_ptr(dQ), E, _ptr(q2), E, B * Tq, E, E, gw[:E], dev)
+            _wgrad(_ptr(dKV), 2 * E, _ptr(kv2), E, B * Tk, 2 * E, E, gw[E:], dev)
+        gb = _gbuf(in_b)
+        if gb is not None:
+            colsum(B * Tq, E, _ptr(dQ), E, _ptr(gb), device=dev)
+            colsum(B * Tk, 2 * E, _ptr(dKV), 2 * E, _ptr(gb, E), device=dev)
+        dq_in = dkv_in = None
+        if ctx.needs_input_grad[1]:
+            dq_in = torch.empty(B, Tq, E, device=dev, dtype=torch.float32)
+            gemm(B * Tq, E, E, _ptr(dQ), 0, E, _ptr(in_w), 0, E, _ptr(dq_in), E, device=dev)
+        if ctx.needs_input_grad[2]:
+            dkv_in = torch.empty(B, Tk, E, device=dev, dtype=torch.float32)
+            gemm(B * Tk, E, 2 * E, _ptr(dKV), 0, 2 * E, _ptr(in_w, E * E), 0, E, _ptr(dkv_in), E,
+                 device=dev)
+        return None, dq_in, dkv_in, None, None, None, None, None, None
+
+
+def mha(q, kv, in_proj_weight, in_proj_bias, out_weight, out_bias, heads, causal=False,
+        qpad=None, kpad=None):
+    """nn.MultiheadAttention(batch_first, kdim=vdim=E)(q, kv, kv) with the reference mask rules."""
+    if in_proj_weight.shape[0] != 3 * q.shape[-1]:
+        raise ValueError("in_proj_weight must be [3E, E]")
+    return _MHAFn.apply((heads, bool(causal)), q, kv, in_proj_weight, in_proj_bias, out_weight,
+                        out_bias, qpad, kpad)
+
+
+def padding_flags(x: torch.Tensor, padding_value: float = -100.0) -> torch.Tensor:
+    """uint8 [B, T]: frame is padding (x[:, :, 0] == -100), as gen_attention_mask tests it."""
+    return (x[:, :, 0] == padding_value).to(torch.uint8).contiguous()
+
+
+# ------------------------------------------------------------------ loss
+_LOSS_TYPES = {"huber": 0, "mse": 1, "mae": 2, "smoothl1": 3}
+
+
+class _LossFn(Function):
+    @staticmethod
+    def forward(ctx, y, target, lead, spec):
+        _lib.require_device(y)
+        y = y.contiguous()
+        target = target.contiguous()
+        B, Ttot, F = y.shape
+        T = target.shape[1]
+        if Ttot - lead != T or target.shape[0] != B or target.shape[2] != F:
+            raise RuntimeError(f"loss shape mismatch: y{tuple(y.shape)}[:, {lead}:] vs target{tuple(target.shape)}")
+        lib = _lib.load()
+        loss = torch.empty(1, device=y.device, dtype=torch.float32)
+        ws = _ws(lib.mrg_loss_workspace_bytes(B, T, F), y.device)
+        _lib.check(lib.mrg_masked_loss_fwd(B, T, F, _ptr(y, lead * F), Ttot * F, _ptr(target), *spec,
+                                           _ptr(loss), _ptr(ws), _stream()), "loss fwd")
+        ctx.save_for_backward(y, target)
+        ctx.lead, ctx.spec = lead, spec
+        return loss.view(())
+
+    @staticmethod
+    def backward(ctx, gout):
+        y, target = ctx.saved_tensors
+        B, Ttot, F = y.shape
+        T = target.shape[1]
+        dy = torch.zeros_like(y)
+        go = gout.reshape(1).contiguous()
+        _lib.check(_lib.load().mrg_masked_loss_bwd(B, T, F, _ptr(y, ctx.lead * F), Ttot * F, _ptr(target),
+                                                   *ctx.spec, _ptr(go), _ptr(dy, ctx.lead * F), _stream()),
+                   "loss bwd")
+        return dy, None, None, None
+
+
+def masked_loss(y, target, lead=0, loss_type="huber", delta=1.0, beta=1.0, mask_padding=True,
+                delta_order=0, delta_loss_scale=1.0):
+    """Masked regression loss of the reference training_step on y[:, lead:] vs target."""
+    F = y.shape[2]
+    spec = (_LOSS_TYPES[loss_type], float(delta), float(beta), int(mask_padding),
+            int(F // (delta_order + 1)), float(math.sqrt(delta_loss_scale)))
+    return _LossFn.apply(y, target, int(lead), spec)

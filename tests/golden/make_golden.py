@@ -190,7 +190,7 @@ def op_cases():
     for nm, t in dict(dx=x.grad, dh0=h0.grad, dc0=c0.grad).items():
         out[f"lstm1/{nm}"] = _np(t)
     # bi-directional 2-layer (LSTMModule, lstm_block.py:21-28)
-    lstm = nn.LSTM(16, 12, num_layers=2, batch_first=True, bidirectional=True)
+    lstm = nn.LSTM(16, 16, num_layers=2, batch_first=True, bidirectional=True)
     x = torch.randn(2, 6, 16, requires_grad=True)
     y, (hT, cT) = lstm(x)
     dy = torch.randn_like(y)

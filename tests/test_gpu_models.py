@@ -1,0 +1,163 @@
+"""Model-level parity on the MI355X: full training steps of the three models vs the reference goldens.
+
+Each case loads the reference's weights (or regenerates them with the same
+RandomState filler), runs ``training_step`` + backward + the fused AdamW on
+the GPU, and compares loss, forward output, every parameter gradient and the
+post-step parameters with what the reference itself produced
+(tests/golden/*.npz).  Tolerance 1e-4 relative (fp32).
+"""
+import numpy as np
+import pytest
+import torch
+
+from tests.golden_util import load, config, batch_from, prefixed, rel_err
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _done():
+    yield
+    from multimodalreactiongeneration_amd import functional as Fn
+    torch.cuda.synchronize()
+    Fn.check_errors()
+
+
+def _build(cls, d, full_width_seed=None):
+    cfg = config(d)
+    m = cls(cfg["model"], cfg["optim"], cfg["metrics"])
+    if full_width_seed is None:
+        m.load_state_dict(prefixed(d, "param/"))
+    else:
+        from multimodalreactiongeneration_amd.synthetic import fill_params_randomstate
+        fill_params_randomstate(m, full_width_seed)
+    return m.to(DEV), cfg
+
+
+def _check(d, m, loss, full=True):
+    assert abs(loss.item() - float(d["loss"])) / abs(float(d["loss"])) < TOL
+    for k, p in m.named_parameters():
+        g = p.grad
+        if f"grad/{k}" in d.files:
+            assert rel_err(g, d[f"grad/{k}"]) < TOL, k
+        elif f"gradsum/{k}" in d.files:
+            ref = d[f"gradsum/{k}"]
+            gg = g.double().cpu()
+            assert abs(gg.sum().item() - ref[0]) <= TOL * max(abs(ref[0]), np.sqrt(ref[1]), 1e-6), k
+            assert abs((gg ** 2).sum().item() - ref[1]) <= 1e-3 * max(ref[1], 1e-12), k
+
+
+def _check_after(d, m):
+    for k, p in m.named_parameters():
+        if f"after/{k}" not in d.files:
+            continue
+        gref = torch.from_numpy(d[f"grad/{k}"])
+        sel = gref.abs() > 1e-5 * gref.abs().max().clamp_min(1e-30)
+        if sel.any():
+            assert rel_err(p.detach().cpu()[sel], torch.from_numpy(d[f"after/{k}"])[sel]) < TOL, k
+
+
+def _train_step(m, batch, **kw):
+    opt = m.configure_optimizers()["optimizer"]
+    loss = m.training_step(batch, **kw)["loss"]
+    loss.backward()
+    torch.cuda.synchronize()
+    return loss, opt
+
+
+@pytest.mark.parametrize("name", ["metaformer_small_r1", "metaformer_small_r2_pad"])
+def test_metaformer_small_train_step(name):
+    from multimodalreactiongeneration_amd.model import Metaformer
+    d = load(name)
+    m, cfg = _build(Metaformer, d)
+    batch = batch_from(d, DEV)
+    with torch.no_grad():
+        m.eval()
+        y_eval, _ = m.forward(*[(x.clone(), n) for x, n in batch[:-1]])
+        assert rel_err(y_eval, d["y_eval"]) < TOL
+        m.train()
+        b2 = [(x.clone(), n) for x, n in batch]
+        ms = b2[2][0]
+        b2[2] = (ms * (ms != -100).float(), b2[2][1])
+        y, _ = m.forward(*b2[:-1])
+        assert rel_err(y, d["y"]) < TOL
+    loss, opt = _train_step(m, batch)
+    _check(d, m, loss)
+    opt.step()
+    torch.cuda.synchronize()
+    _check_after(d, m)
+
+
+def test_metaformer_full_width_train_step():
+    from multimodalreactiongeneration_amd.model import Metaformer
+    d = load("metaformer_full_r1")
+    m, cfg = _build(Metaformer, d, full_width_seed=2)
+    batch = batch_from(d, DEV)
+    loss, _ = _train_step(m, batch)
+    _check(d, m, loss)
+
+
+def test_lstm_with_sample_teacher_forced():
+    from multimodalreactiongeneration_amd.model import LSTMwithSample
+    d = load("lstm_with_sample_tf")
+    m, cfg = _build(LSTMwithSample, d)
+    batch = batch_from(d, DEV)
+    with torch.no_grad():
+        y, _, _ = m.forward(*batch[:-1])
+        assert rel_err(y, d["y"]) < TOL
+    loss, opt = _train_step(m, batch)
+    _check(d, m, loss)
+    opt.step()
+    torch.cuda.synchronize()
+    _check_after(d, m)
+
+
+def test_lstm_with_sample_scheduled_sampling():
+    from multimodalreactiongeneration_amd.model import LSTMwithSample
+    d = load("lstm_with_sample_ss")
+    m, cfg = _build(LSTMwithSample, d)
+    m.current_epoch = int(d["meta/epoch"])
+    batch = batch_from(d, DEV)
+    loss, opt = _train_step(m, batch, sampling_mask=torch.from_numpy(d["sampling_mask"]))
+    _check(d, m, loss)
+    opt.step()
+    torch.cuda.synchronize()
+    _check_after(d, m)
+
+
+def test_simple_lstm_train_step():
+    from multimodalreactiongeneration_amd.model import SimpleLSTM
+    d = load("simple_lstm_small")
+    m, cfg = _build(SimpleLSTM, d)
+    a, mo, t = (torch.from_numpy(d[k]).to(DEV) for k in ("in/audio", "in/motion", "in/target"))
+    with torch.no_grad():
+        assert rel_err(m.forward(a, mo), d["y"]) < TOL
+    loss, opt = _train_step(m, (a, mo, t))
+    _check(d, m, loss)
+    opt.step()
+    torch.cuda.synchronize()
+    _check_after(d, m)
+
+
+@pytest.mark.parametrize("ratio,B,T", [(1, 4, 300), (8, 2, 60)])
+def test_metaformer_benchmark_width_vs_oracle(ratio, B, T):
+    """Full benchmark architecture (H=256, 5 blocks, 5 encoder layers) at T=300 vs the CPU oracle."""
+    from multimodalreactiongeneration_amd import configs as C
+    from multimodalreactiongeneration_amd.model import Metaformer
+    from multimodalreactiongeneration_amd.synthetic import make_batch, clone_batch
+    from oracle import mrg_oracle as O
+    mc, oc, me = C.lstmformer_config(ratio=ratio)
+    torch.manual_seed(0)
+    m = Metaformer(mc, oc, me)
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.to(DEV)
+    batch = make_batch(B=B, T=T, ratio=ratio, seed=11)
+    loss = m.training_step(clone_batch(batch, DEV))["loss"]
+    loss.backward()
+    torch.cuda.synchronize()
+    ref_loss, ref_y, grads, _ = O.run_train_step(O.metaformer_training_loss, sd, oc, mc, clone_batch(batch))
+    assert abs(loss.item() - ref_loss.item()) / abs(ref_loss.item()) < TOL
+    worst = max(rel_err(p.grad, grads[k]) for k, p in m.named_parameters())
+    assert worst < TOL, worst

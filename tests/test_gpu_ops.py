@@ -1,0 +1,314 @@
+"""Op-level parity of the HIP kernels (libmrg.so) on a real MI355X.
+
+Floating-point bar: max|a-b| / max|b| <= 1e-4 (fp32, BASELINE north_star),
+checked against the reference's own golden vectors where they exist
+(tests/golden/ops.npz, produced by torch.nn.LSTM / nn.MultiheadAttention as
+the reference instantiates them) and against the CPU oracle / a plain torch
+fp32 reference otherwise.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from tests.golden_util import load, prefixed, rel_err
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    from multimodalreactiongeneration_amd import _lib as L
+    L.load()
+    yield
+    from multimodalreactiongeneration_amd import functional as Fn
+    torch.cuda.synchronize()
+    Fn.check_errors()
+
+
+def _param(t):
+    return torch.nn.Parameter(t.clone().to(DEV))
+
+
+@pytest.mark.parametrize("M,N,K", [(19200, 1024, 256), (600, 6, 64), (37, 45, 53), (2048, 256, 512)])
+def test_linear_fwd_bwd_vs_torch_fp32(M, N, K):
+    from multimodalreactiongeneration_amd import functional as Fn
+    g = torch.Generator().manual_seed(M + N)
+    x = torch.randn(M, K, generator=g)
+    w = torch.randn(N, K, generator=g) / math.sqrt(K)
+    b = torch.randn(N, generator=g)
+    dy = torch.randn(M, N, generator=g)
+    xd = x.to(DEV).requires_grad_(True)
+    wd, bd = _param(w), _param(b)
+    y = Fn.linear(xd, wd, bd)
+    y.backward(dy.to(DEV))
+    xr = x.double().requires_grad_(True)
+    wr = w.double().requires_grad_(True)
+    br = b.double().requires_grad_(True)
+    yr = torch.nn.functional.linear(xr, wr, br)
+    yr.backward(dy.double())
+    assert rel_err(y, yr) < TOL
+    assert rel_err(xd.grad, xr.grad) < TOL
+    assert rel_err(wd.grad, wr.grad) < TOL
+    assert rel_err(bd.grad, br.grad) < TOL
+
+
+def test_ffn_relu_fused_vs_torch():
+    from multimodalreactiongeneration_amd import functional as Fn
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(3000, 256, generator=g)
+    w1, b1 = torch.randn(64, 256, generator=g) / 16, torch.randn(64, generator=g)
+    w2, b2 = torch.randn(6, 64, generator=g) / 8, torch.randn(6, generator=g)
+    dz = torch.randn(3000, 6, generator=g)
+    ps = [_param(t) for t in (w1, b1, w2, b2)]
+    xd = x.to(DEV).requires_grad_(True)
+    z = Fn.ffn(xd, *ps)
+    z.backward(dz.to(DEV))
+    rs = [t.double().requires_grad_(True) for t in (x, w1, b1, w2, b2)]
+    zr = torch.nn.functional.linear(torch.relu(torch.nn.functional.linear(rs[0], rs[1], rs[2])), rs[3], rs[4])
+    zr.backward(dz.double())
+    assert rel_err(z, zr) < TOL
+    assert rel_err(xd.grad, rs[0].grad) < TOL
+    for p, r in zip(ps, rs[1:]):
+        assert rel_err(p.grad, r.grad) < TOL
+
+
+@pytest.mark.parametrize("E", [64, 128, 256, 512])
+def test_residual_layernorm_vs_torch(E):
+    from multimodalreactiongeneration_amd import functional as Fn
+    g = torch.Generator().manual_seed(E)
+    a, b = torch.randn(1000, E, generator=g), torch.randn(1000, E, generator=g)
+    gam, bet = 1 + 0.1 * torch.randn(E, generator=g), 0.1 * torch.randn(E, generator=g)
+    dy = torch.randn(1000, E, generator=g)
+    ad, bd = a.to(DEV).requires_grad_(True), b.to(DEV).requires_grad_(True)
+    gd, btd = _param(gam), _param(bet)
+    y = Fn.residual_layernorm(ad, bd, gd, btd)
+    y.backward(dy.to(DEV))
+    ar, br = a.double().requires_grad_(True), b.double().requires_grad_(True)
+    gr, btr = gam.double().requires_grad_(True), bet.double().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(ar + br, (E,), gr, btr, 1e-5)
+    yr.backward(dy.double())
+    assert rel_err(y, yr) < TOL
+    assert rel_err(ad.grad, ar.grad) < TOL and rel_err(bd.grad, br.grad) < TOL
+    assert rel_err(gd.grad, gr.grad) < TOL and rel_err(btd.grad, btr.grad) < TOL
+
+
+@pytest.mark.parametrize("loss_type", ["huber", "mse", "mae", "smoothl1"])
+def test_masked_loss_vs_oracle(loss_type):
+    from multimodalreactiongeneration_amd import functional as Fn
+    from oracle import mrg_oracle as O
+    g = torch.Generator().manual_seed(3)
+    y = torch.randn(4, 12, 6, generator=g) * 2
+    t = torch.randn(4, 9, 6, generator=g) * 2
+    t[1, 6:] = -100.0
+    yd = y.to(DEV).requires_grad_(True)
+    loss = Fn.masked_loss(yd, t.to(DEV), lead=3, loss_type=loss_type)
+    loss.backward()
+    yr = y.clone().requires_grad_(True)
+    lr = O.masked_regression_loss(yr[:, 3:], t, loss_type)
+    lr.backward()
+    assert abs(loss.item() - lr.item()) <= 1e-5 * max(1.0, abs(lr.item()))
+    assert rel_err(yd.grad, yr.grad) < TOL
+
+
+def test_lstm_layer_matches_nn_lstm_golden():
+    from multimodalreactiongeneration_amd import functional as Fn
+    d = load("ops")
+    p = {k: _param(v) for k, v in prefixed(d, "lstm1/param/").items()}
+    x = torch.from_numpy(d["lstm1/x"]).to(DEV).requires_grad_(True)
+    h0 = torch.from_numpy(d["lstm1/h0"])[0].to(DEV).requires_grad_(True)
+    c0 = torch.from_numpy(d["lstm1/c0"])[0].to(DEV).requires_grad_(True)
+    y, hT, cT = Fn.lstm_layer(x, p["weight_ih_l0"], p["weight_hh_l0"], p["bias_ih_l0"], p["bias_hh_l0"], h0, c0)
+    assert rel_err(y, d["lstm1/y"]) < TOL
+    assert rel_err(hT, d["lstm1/hT"][0]) < TOL
+    assert rel_err(cT, d["lstm1/cT"][0]) < TOL
+    loss = (y * torch.from_numpy(d["lstm1/dy"]).to(DEV)).sum() \
+        + (hT * torch.from_numpy(d["lstm1/dhT"])[0].to(DEV)).sum() \
+        + (cT * torch.from_numpy(d["lstm1/dcT"])[0].to(DEV)).sum()
+    loss.backward()
+    torch.cuda.synchronize()
+    assert rel_err(x.grad, d["lstm1/dx"]) < TOL
+    assert rel_err(h0.grad, d["lstm1/dh0"][0]) < TOL
+    assert rel_err(c0.grad, d["lstm1/dc0"][0]) < TOL
+    for k in p:
+        assert rel_err(p[k].grad, d[f"lstm1/grad/{k}"]) < TOL, k
+
+
+def test_bidirectional_two_layer_lstm_golden():
+    from multimodalreactiongeneration_amd.model.layers import LSTM
+    d = load("ops")
+    lstm = LSTM(16, 16, num_layers=2, bidirectional=True)
+    lstm.load_state_dict(prefixed(d, "lstm2/param/"))
+    lstm = lstm.to(DEV)
+    x = torch.from_numpy(d["lstm2/x"]).to(DEV).requires_grad_(True)
+    y, (hT, cT) = lstm(x)
+    assert rel_err(y, d["lstm2/y"]) < TOL
+    assert rel_err(hT, d["lstm2/hT"]) < TOL
+    assert rel_err(cT, d["lstm2/cT"]) < TOL
+    y.backward(torch.from_numpy(d["lstm2/dy"]).to(DEV))
+    torch.cuda.synchronize()
+    assert rel_err(x.grad, d["lstm2/dx"]) < TOL
+    for k, prm in lstm.named_parameters():
+        assert rel_err(prm.grad, d[f"lstm2/grad/{k}"]) < TOL, k
+
+
+def test_unsupported_hidden_size_fails_loudly():
+    from multimodalreactiongeneration_amd.model.layers import LSTM
+    lstm = LSTM(8, 12).to(DEV)
+    with pytest.raises(RuntimeError):
+        lstm(torch.randn(2, 3, 8, device=DEV))
+
+
+@pytest.mark.parametrize("H,In,B,T,rev", [(256, 256, 64, 300, False), (128, 128, 64, 300, True),
+                                          (64, 40, 5, 50, False), (32, 16, 3, 20, True), (16, 8, 2, 9, False)])
+def test_lstm_layer_vs_oracle(H, In, B, T, rev):
+    from multimodalreactiongeneration_amd import functional as Fn
+    from oracle import mrg_oracle as O
+    g = torch.Generator().manual_seed(H + T)
+    k = 1 / math.sqrt(H)
+    w_ih = (torch.rand(4 * H, In, generator=g) * 2 - 1) * k
+    w_hh = (torch.rand(4 * H, H, generator=g) * 2 - 1) * k
+    b_ih = (torch.rand(4 * H, generator=g) * 2 - 1) * k
+    b_hh = (torch.rand(4 * H, generator=g) * 2 - 1) * k
+    x = torch.randn(B, T, In, generator=g)
+    dy = torch.randn(B, T, H, generator=g)
+    ps = [_param(t) for t in (w_ih, w_hh, b_ih, b_hh)]
+    xd = x.to(DEV).requires_grad_(True)
+    y, hT, cT = Fn.lstm_layer(xd, *ps, reverse=rev)
+    y.backward(dy.to(DEV))
+    torch.cuda.synchronize()
+    rs = [t.clone().requires_grad_(True) for t in (w_ih, w_hh, b_ih, b_hh)]
+    xr = x.clone().requires_grad_(True)
+    yr, hr, cr = O.lstm_layer(xr, *rs, reverse=rev)
+    yr.backward(dy)
+    assert rel_err(y, yr) < TOL
+    assert rel_err(cT, cr) < TOL
+    assert rel_err(xd.grad, xr.grad) < TOL
+    for p, r in zip(ps, rs):
+        assert rel_err(p.grad, r.grad) < TOL
+
+
+@pytest.mark.parametrize("bs", [1, 2, 4, 8])
+def test_lstm_batched_problems_and_forced_tiling(bs):
+    """3 independent recurrences in one launch, every batch-tile size, vs the oracle."""
+    from multimodalreactiongeneration_amd import functional as Fn
+    from oracle import mrg_oracle as O
+    H, B, T = 256, 16, 40
+    g = torch.Generator().manual_seed(bs)
+    probs, refs = [], []
+    for _ in range(3):
+        w = [torch.randn(4 * H, H, generator=g) * 0.06 for _ in range(2)]
+        bb = [torch.randn(4 * H, generator=g) * 0.06 for _ in range(2)]
+        x = torch.randn(B, T, H, generator=g)
+        probs.append((x.to(DEV), _param(w[0]), _param(w[1]), _param(bb[0]), _param(bb[1])))
+        refs.append(O.lstm_layer(x, w[0], w[1], bb[0], bb[1])[0])
+    ys = Fn.lstm_layers_batched(probs, force_bs=bs)
+    sum(y.sum() for y in ys).backward()
+    torch.cuda.synchronize()
+    for y, r in zip(ys, refs):
+        assert rel_err(y, r) < TOL
+
+
+@pytest.mark.parametrize("case", [0, 1, 2])
+def test_mha_with_reference_mask_golden(case):
+    from multimodalreactiongeneration_amd.model.layers import MultiheadAttention
+    from multimodalreactiongeneration_amd.model.masks import gen_attention_mask
+    d = load("ops")
+    p = f"mha{case}/"
+    heads = int(d[p + "heads"])
+    q = torch.from_numpy(d[p + "q"])
+    kv = torch.from_numpy(d[p + "kv"])
+    E = q.shape[-1]
+    mha = MultiheadAttention(E, heads, batch_first=True, kdim=E, vdim=E)
+    mha.load_state_dict(prefixed(d, p + "param/"))
+    mha = mha.to(DEV)
+    mq, mk = q.clone(), kv.clone()
+    mq[1, q.shape[1] - 2:] = -100
+    mk[1, kv.shape[1] - 3:] = -100
+    mask = gen_attention_mask(mq.to(DEV), mk.to(DEV), heads)
+    assert torch.equal(mask.dense().reshape(-1, q.shape[1], kv.shape[1]).cpu(), torch.from_numpy(d[p + "mask"]))
+    qd = q.to(DEV).requires_grad_(True)
+    kvd = kv.to(DEV).requires_grad_(True)
+    o, _ = mha(qd, kvd, kvd, None, False, mask, False, False)
+    o.backward(torch.from_numpy(d[p + "do"]).to(DEV))
+    torch.cuda.synchronize()
+    assert rel_err(o, d[p + "o"]) < TOL
+    assert rel_err(qd.grad, d[p + "dq"]) < TOL
+    assert rel_err(kvd.grad, d[p + "dkv"]) < TOL
+    for k, prm in mha.named_parameters():
+        assert rel_err(prm.grad, d[p + f"grad/{k}"]) < TOL, k
+
+
+@pytest.mark.parametrize("Tq,Tk,E,heads,causal", [(300, 300, 256, 4, True), (300, 2400, 256, 4, True),
+                                                  (100, 100, 256, 8, False), (37, 74, 64, 2, True),
+                                                  (40, 20, 128, 4, True)])
+def test_attention_vs_oracle(Tq, Tk, E, heads, causal):
+    from multimodalreactiongeneration_amd import functional as Fn
+    from oracle import mrg_oracle as O
+    B = 3
+    g = torch.Generator().manual_seed(Tq + Tk)
+    q, kv = torch.randn(B, Tq, E, generator=g), torch.randn(B, Tk, E, generator=g)
+    sd = {"in_proj_weight": torch.randn(3 * E, E, generator=g) / math.sqrt(E),
+          "in_proj_bias": torch.randn(3 * E, generator=g) * 0.1,
+          "out_proj.weight": torch.randn(E, E, generator=g) / math.sqrt(E),
+          "out_proj.bias": torch.randn(E, generator=g) * 0.1}
+    do = torch.randn(B, Tq, E, generator=g)
+    ps = {k: _param(v) for k, v in sd.items()}
+    qd, kvd = q.to(DEV).requires_grad_(True), kv.to(DEV).requires_grad_(True)
+    qpad = torch.zeros(B, Tq, dtype=torch.uint8, device=DEV) if causal else None
+    kpad = torch.zeros(B, Tk, dtype=torch.uint8, device=DEV) if causal else None
+    o = Fn.mha(qd, kvd, ps["in_proj_weight"], ps["in_proj_bias"], ps["out_proj.weight"], ps["out_proj.bias"],
+               heads, causal, qpad, kpad)
+    o.backward(do.to(DEV))
+    torch.cuda.synchronize()
+    rs = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    qr, kvr = q.clone().requires_grad_(True), kv.clone().requires_grad_(True)
+    mask = O.gen_attention_mask(qr, kvr, heads).reshape(-1, Tq, Tk) if causal else None
+    orf = O.mha(qr, kvr, rs, "", heads, mask)
+    orf.backward(do)
+    assert rel_err(o, orf) < TOL
+    assert rel_err(qd.grad, qr.grad) < TOL
+    assert rel_err(kvd.grad, kvr.grad) < TOL
+    for k in sd:
+        assert rel_err(ps[k].grad, rs[k].grad) < TOL, k
+
+
+def test_attention_fully_masked_row_is_nan_like_reference():
+    """A query row whose every visible key is padding (AND rule) -> NaN, as softmax(-inf row)."""
+    from multimodalreactiongeneration_amd import functional as Fn
+    from oracle import mrg_oracle as O
+    B, T, E, heads = 1, 4, 16, 2
+    q = torch.randn(B, T, E)
+    kv = torch.randn(B, T, E)
+    q[0, 0] = -100
+    kv[0, 0] = -100   # query 0 sees only key 0, both padded -> masked
+    sd = {"in_proj_weight": torch.randn(3 * E, E) * 0.2, "in_proj_bias": torch.zeros(3 * E),
+          "out_proj.weight": torch.randn(E, E) * 0.2, "out_proj.bias": torch.zeros(E)}
+    ps = {k: _param(v) for k, v in sd.items()}
+    o = Fn.mha(q.to(DEV), kv.to(DEV), ps["in_proj_weight"], ps["in_proj_bias"], ps["out_proj.weight"],
+               ps["out_proj.bias"], heads, True, Fn.padding_flags(q.to(DEV)), Fn.padding_flags(kv.to(DEV)))
+    ref = O.mha(q, kv, sd, "", heads, O.gen_attention_mask(q, kv, heads).reshape(-1, T, T))
+    assert torch.isnan(ref[0, 0]).all() and torch.isnan(o[0, 0].cpu()).all()
+    assert rel_err(o[0, 1:], ref[0, 1:]) < TOL
+
+
+def test_adamw_matches_oracle_over_three_steps():
+    from multimodalreactiongeneration_amd.optim import FusedAdamW
+    from oracle import mrg_oracle as O
+    g = torch.Generator().manual_seed(9)
+    p0 = [torch.randn(300, 7, generator=g), torch.randn(1000, generator=g)]
+    params = [torch.nn.Parameter(t.clone().to(DEV)) for t in p0]
+    opt = FusedAdamW(params, lr=1e-3, weight_decay=1e-2)
+    ref = {str(i): t.clone() for i, t in enumerate(p0)}
+    state = {}
+    for step in range(3):
+        grads = [torch.randn(t.shape, generator=g) for t in p0]
+        for p, gr in zip(params, grads):
+            p.grad.copy_(gr.to(DEV))
+        opt.step()
+        O.adamw_step(ref, {str(i): gr for i, gr in enumerate(grads)}, state, 1e-3, 1e-2)
+    for i, p in enumerate(params):
+        assert rel_err(p.detach(), ref[str(i)]) < 1e-6
