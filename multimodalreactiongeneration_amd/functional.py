@@ -29,6 +29,47 @@ from . import _lib
 F32 = 4
 _ERR = {}
 
+# --- optional live kernel timing (bench.py): HIP events recorded on the launch stream
+_PROBE_ON = set()
+_PROBES = {}
+
+
+class _probe:
+    """Bracket one library launch with timing events when ``name`` is being probed."""
+    __slots__ = ("name", "e0")
+
+    def __init__(self, name):
+        self.name = name
+        self.e0 = None
+
+    def __enter__(self):
+        if self.name in _PROBE_ON:
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e0.record()
+        return self
+
+    def __exit__(self, *exc):
+        if self.e0 is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            _PROBES.setdefault(self.name, []).append((self.e0, e1))
+        return False
+
+
+def probe_start(*names):
+    _PROBE_ON.clear()
+    _PROBE_ON.update(names)
+    _PROBES.clear()
+
+
+def probe_stop():
+    """Stop probing; returns {name: [ms per launch]} (synchronises)."""
+    _PROBE_ON.clear()
+    torch.cuda.synchronize()
+    out = {k: [a.elapsed_time(b) for a, b in v] for k, v in _PROBES.items()}
+    _PROBES.clear()
+    return out
+
 
 def _ptr(t: Optional[torch.Tensor], elem_offset: int = 0):
     if t is None:
@@ -79,8 +120,9 @@ def gemm(M, N, K, A, transA, lda, B, transB, ldb, C, ldc, *, alpha=1.0, beta=0.0
     ws = None
     if splits > 1:
         ws = _ws(lib.mrg_gemm_workspace_bytes(M, N, splits), device)
-    rc = lib.mrg_gemm_f32(M, N, K, alpha, A, transA, lda, a_hi, a_div, B, transB, ldb, b_hi, b_div,
-                          beta, C, ldc, bias, epi, aux, ldaux, _ptr(ws), splits, _stream())
+    with _probe("gemm"):
+        rc = lib.mrg_gemm_f32(M, N, K, alpha, A, transA, lda, a_hi, a_div, B, transB, ldb, b_hi, b_div,
+                              beta, C, ldc, bias, epi, aux, ldaux, _ptr(ws), splits, _stream())
     _lib.check(rc, "gemm")
 
 
@@ -299,6 +341,7 @@ class _LSTMFn(Function):
         def arr(ctype, vals):
             return (ctype * nprob)(*vals)
         VP = ctypes.c_void_p
+        pr = _probe("lstm_fwd").__enter__()
         rc = lib.mrg_lstm_fwd(
             nprob, B, T, H,
             arr(VP, [_ptr(g) for g in gxs]), arr(ctypes.c_long, [T * 4 * H] * nprob),
@@ -311,6 +354,7 @@ class _LSTMFn(Function):
             arr(ctypes.c_int, [int(r) for r in reverse]),
             arr(VP, [_ptr(xbuf[i]) for i in range(nprob)]), _ptr(_err_flag(dev)),
             _lib.cu_count(dev.index or 0), force_bs, _stream())
+        pr.__exit__()
         _lib.check(rc, "lstm fwd")
         ctx.spec = (nprob, concat, tuple(reverse), force_bs, B, T, H)
         ctx.has_h0 = [h is not None for h in h0]
@@ -371,6 +415,7 @@ class _LSTMFn(Function):
         def arr(ctype, vals):
             return (ctype * nprob)(*vals)
         VP = ctypes.c_void_p
+        pr = _probe("lstm_bwd").__enter__()
         rc = lib.mrg_lstm_bwd(
             nprob, B, T, H,
             arr(VP, [_ptr(p[2]) for p in per]), arr(VP, [_ptr(p[5]) for p in per]),
@@ -381,6 +426,7 @@ class _LSTMFn(Function):
             arr(VP, [_ptr(t) for t in dc0]), arr(ctypes.c_int, [int(r) for r in reverse]),
             arr(VP, [_ptr(xbuf[i]) for i in range(nprob)]), _ptr(_err_flag(dev)),
             _lib.cu_count(dev.index or 0), force_bs, _stream())
+        pr.__exit__()
         _lib.check(rc, "lstm bwd")
 
         out = [None]
@@ -477,10 +523,12 @@ class _MHAFn(Function):
         lse = torch.empty(B, heads, Tq, device=dev, dtype=torch.float32)
         scale = 1.0 / math.sqrt(D)
         lib = _lib.load()
-        _lib.check(lib.mrg_attention_fwd(B, heads, Tq, Tk, D, _ptr(Q), Tq * E, E, _ptr(KV), Tk * 2 * E,
+        with _probe("attn_fwd"):
+            rc = lib.mrg_attention_fwd(B, heads, Tq, Tk, D, _ptr(Q), Tq * E, E, _ptr(KV), Tk * 2 * E,
                                          2 * E, _ptr(KV, E), Tk * 2 * E, 2 * E, _ptr(O), Tq * E, E,
-                                         _ptr(lse), _ptr(qpad), _ptr(kpad), int(causal), scale,
-                                         _stream()), "attention fwd")
+                                       _ptr(lse), _ptr(qpad), _ptr(kpad), int(causal), scale,
+                                       _stream())
+        _lib.check(rc, "attention fwd")
         out = torch.empty(B, Tq, E, device=dev, dtype=torch.float32)
         gemm(B * Tq, E, E, _ptr(O), 0, E, _ptr(out_w), 1, E, _ptr(out), E, bias=_ptr(out_b), device=dev)
         ctx.save_for_backward(q2, kv2, Q, KV, O, lse, in_w, in_b, out_w, out_b, qpad, kpad)
@@ -508,11 +556,13 @@ class _MHAFn(Function):
         dQ = torch.empty(B, Tq, E, device=dev, dtype=torch.float32)
         dKV = torch.empty(B, Tk, 2 * E, device=dev, dtype=torch.float32)
         ws = _ws(lib.mrg_attention_bwd_workspace_bytes(B, heads, Tq), dev)
-        _lib.check(lib.mrg_attention_bwd(
+        with _probe("attn_bwd"):
+            rc = lib.mrg_attention_bwd(
             B, heads, Tq, Tk, D, _ptr(Q), Tq * E, E, _ptr(KV), Tk * 2 * E, 2 * E, _ptr(KV, E), Tk * 2 * E,
             2 * E, _ptr(O), Tq * E, E, _ptr(lse), _ptr(qpad), _ptr(kpad), int(causal), scale,
             _ptr(dO), Tq * E, E, _ptr(dQ), Tq * E, E, _ptr(dKV), Tk * 2 * E, 2 * E, _ptr(dKV, E),
-            Tk * 2 * E, 2 * E, _ptr(ws), _stream()), "attention bwd")
+            Tk * 2 * E, 2 * E, _ptr(ws), _stream())
+        _lib.check(rc, "attention bwd")
         gw = _gbuf(in_w)
         if gw is not None:
             _wgrad(_ptr(dQ), E, _ptr(q2), E, B * Tq, E, E, gw[:E], dev)
