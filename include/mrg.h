@@ -83,6 +83,14 @@ int mrg_lstm_bwd(int nprob, int B, int T, int H,
                  float* const* dG, float* const* dh0, float* const* dc0, const int* reverse,
                  void* const* xbuf, int* err, int cus, int force_bs, hipStream_t stream);
 
+/* Tuning knob: number of workgroups that share one batch row group at H = 256
+ * (8 or 16; default 16).  Process-wide; set before capture, not during. */
+int mrg_lstm_config(int group256);
+
+/* Diagnostics only: record per-step phase clocks (s_memtime) of block 0 of the next
+ * LSTM launches into buf ([T][8] u64); null disables.  Never in timed runs. */
+int mrg_lstm_debug_stamps(void* buf);
+
 /* ---------------------------------------------------------------- attention
  * Scaled-dot-product core of nn.MultiheadAttention as the reference calls it
  * (MHAforSequentail.forward, for_sequential.py:42-51;
@@ -108,7 +116,7 @@ int mrg_attention_bwd(int B, int heads, int Tq, int Tk, int D,
 
 /* ---------------------------------------------------------------- LayerNorm
  * y = LayerNorm(a + b) (ResidualConnection.forward, residual_connection.py:
- * 20-37), rows x E, E in {64, 128, 256, 512}; mean/rstd saved per row.     */
+ * 20-37), rows x E, 1 <= E <= 1024; mean/rstd saved per row.     */
 int mrg_residual_layernorm_fwd(int rows, int E, const float* a, const float* b,
                                const float* gamma, const float* beta, float eps, float* y,
                                float* mean, float* rstd, hipStream_t stream);

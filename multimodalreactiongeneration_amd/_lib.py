@@ -47,6 +47,8 @@ SIGNATURES = {
     "mrg_lstm_bwd": (c_int, [c_int, c_int, c_int, c_int,
                              PP, PP, PP, PP, PP, PL, PL, PP, PP,
                              PP, PP, PP, PI, PP, P, c_int, c_int, P]),
+    "mrg_lstm_config": (c_int, [c_int]),
+    "mrg_lstm_debug_stamps": (c_int, [P]),
     "mrg_attention_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int,
                                   P, c_long, c_long, P, c_long, c_long, P, c_long, c_long,
                                   P, c_long, c_long, P, P, P, c_int, c_float, P]),

@@ -183,19 +183,29 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   }
 }
 
-// dlt[b,h,q] = sum_d dO * O
-__global__ void attn_dlt_kernel(AttnArgs a, int D) {
-  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  long total = (long)a.B * a.Hh * a.Tq;
-  if (idx >= total) return;
-  int qi = idx % a.Tq;
-  int h = (idx / a.Tq) % a.Hh;
-  int b = idx / ((long)a.Tq * a.Hh);
-  const float* po = a.o + (long)b * a.o_bs + (long)qi * a.o_ts + h * D;
-  const float* pd = a.dout + (long)b * a.do_bs + (long)qi * a.do_ts + h * D;
-  float s = 0.0f;
-  for (int d = 0; d < D; ++d) s += po[d] * pd[d];
-  a.dlt[idx] = s;
+// dlt[b,h,q] = sum_d dO * O.  One wave per (b, q) row of all heads: float4 per
+// lane (coalesced 1-KiB row segments), per-head sums by shuffles within the
+// D/4 lanes that hold one head.
+__global__ __launch_bounds__(256) void attn_dlt_kernel(AttnArgs a, int D) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= (long)a.B * a.Tq) return;
+  const int b = row / a.Tq, qi = row % a.Tq;
+  const int E = a.Hh * D;
+  const float* po = a.o + (long)b * a.o_bs + (long)qi * a.o_ts;
+  const float* pd = a.dout + (long)b * a.do_bs + (long)qi * a.do_ts;
+  const int gl = D / 4;  // lanes per head
+  for (int e0 = 0; e0 < E; e0 += 256) {
+    const int e = e0 + lane * 4;
+    float s = 0.0f;
+    if (e < E) {
+      float4 o4 = *reinterpret_cast<const float4*>(po + e);
+      float4 d4 = *reinterpret_cast<const float4*>(pd + e);
+      s = o4.x * d4.x + o4.y * d4.y + o4.z * d4.z + o4.w * d4.w;
+    }
+    for (int off = gl / 2; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+    if (e < E && (lane % gl) == 0) a.dlt[((long)b * a.Hh + e / D) * a.Tq + qi] = s;
+  }
 }
 
 // dQ for 64 queries of one (b, head): recompute P^T, dP^T = V dO^T, dS^T, dQ^T += K^T dS^T
@@ -421,8 +431,10 @@ MRG_API int mrg_attention_bwd(int B, int Hh, int Tq, int Tk, int D,
   a.dout = dout; a.do_bs = do_bs; a.do_ts = do_ts; a.dlt = workspace;
   a.dq = dq; a.dq_bs = dq_bs; a.dq_ts = dq_ts; a.dk = dk; a.dk_bs = dk_bs; a.dk_ts = dk_ts;
   a.dv = dv; a.dv_bs = dv_bs; a.dv_ts = dv_ts;
-  long rows = (long)B * Hh * Tq;
-  attn_dlt_kernel<<<(unsigned)((rows + 255) / 256), 256, 0, stream>>>(a, D);
+  MRG_REQUIRE((o_ts & 3) == 0 && (do_ts & 3) == 0 && (o_bs & 3) == 0 && (do_bs & 3) == 0 &&
+              (((uintptr_t)o | (uintptr_t)dout) & 15) == 0, "attention bwd: O/dO rows must be 16-B aligned");
+  long rows = (long)B * Tq;
+  attn_dlt_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, stream>>>(a, D);
   if (check_launch("attn_dlt_kernel")) return 1;
   dim3 gq((Tq + 63) / 64, Hh, B);
   MRG_ATTN_DISPATCH(attn_bwd_dq_kernel, gq, a);

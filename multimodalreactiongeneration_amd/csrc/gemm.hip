@@ -40,7 +40,7 @@ struct GemmArgs {
   int kchunk;
 };
 
-static constexpr int BK = 16;
+static constexpr int BK = 32;
 static constexpr int NT = 256;
 
 __device__ __forceinline__ float apply_epi(const GemmArgs& a, float v, int m, int n) {
@@ -52,68 +52,92 @@ __device__ __forceinline__ float apply_epi(const GemmArgs& a, float v, int m, in
   return v;
 }
 
-template <int BM, int BN>
-__global__ __launch_bounds__(NT) void gemm_f32_kernel(GemmArgs a) {
-  constexpr int PAD = 1;
-  constexpr int LA = BM * BK / NT;  // A elements per thread per tile
-  constexpr int LB = BN * BK / NT;
-  constexpr int TM = BM / 64, TN = BN / 64;
-  __shared__ float As[BK][BM + PAD];
-  __shared__ float Bs[BK][BN + PAD];
+// One operand tile (rows of the MFMA M or N dimension x BK) staged k-major in LDS:
+// S[k][x], x = m (or n).  TR says which index is contiguous in memory:
+//   TR = 1 : memory row = k, contiguous along x  -> float4 along x, ds_write_b128
+//   TR = 0 : memory row = x, contiguous along k  -> float4 along k (8 lanes cover
+//            one 128-B k-run of a row), four scalar LDS writes; row pitch X + 1
+//            keeps those writes bank-conflict free.
+template <int X, int TR, bool VEC>
+struct TileIO {
+  static constexpr int PAD = TR ? 4 : 1;
+  static constexpr int LD = X + PAD;
+  static constexpr int NV = X * BK / 4 / NT;  // float4 per thread per tile
+  float4 r[NV];
 
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
+  __device__ __forceinline__ void load(const float* base, const RowMap& map, int x0, int xlim, int k0,
+                                       int kend) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      int e = tid + i * NT;
+      int x, k;
+      if (TR) { x = (e % (X / 4)) * 4; k = e / (X / 4); } else { k = (e % (BK / 4)) * 4; x = e / (BK / 4); }
+      int gx = x0 + x, gk = k0 + k;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (TR) {
+        if (gk < kend) {
+          const float* p = base + map.off(gk) + gx;
+          if (VEC && gx + 3 < xlim) v = *reinterpret_cast<const float4*>(p);
+          else {
+            if (gx < xlim) v.x = p[0];
+            if (gx + 1 < xlim) v.y = p[1];
+            if (gx + 2 < xlim) v.z = p[2];
+            if (gx + 3 < xlim) v.w = p[3];
+          }
+        }
+      } else {
+        if (gx < xlim) {
+          const float* p = base + map.off(gx) + gk;
+          if (VEC && gk + 3 < kend) v = *reinterpret_cast<const float4*>(p);
+          else {
+            if (gk < kend) v.x = p[0];
+            if (gk + 1 < kend) v.y = p[1];
+            if (gk + 2 < kend) v.z = p[2];
+            if (gk + 3 < kend) v.w = p[3];
+          }
+        }
+      }
+      r[i] = v;
+    }
+  }
+
+  __device__ __forceinline__ void store(float* S) const {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      int e = tid + i * NT;
+      if (TR) {
+        int x = (e % (X / 4)) * 4, k = e / (X / 4);
+        *reinterpret_cast<float4*>(S + k * LD + x) = r[i];
+      } else {
+        int k = (e % (BK / 4)) * 4, x = e / (BK / 4);
+        S[(k + 0) * LD + x] = r[i].x;
+        S[(k + 1) * LD + x] = r[i].y;
+        S[(k + 2) * LD + x] = r[i].z;
+        S[(k + 3) * LD + x] = r[i].w;
+      }
+    }
+  }
+};
+
+template <int BM, int BN, int TA, int TB, bool VA, bool VB>
+__global__ __launch_bounds__(NT) void gemm_f32_kernel(GemmArgs a) {
+  using IA = TileIO<BM, TA, VA>;
+  using IB = TileIO<BN, !TB, VB>;  // B(k, n): memory row k when TB == 0 (contiguous along n)
+  constexpr int TM = BM / 64, TN = BN / 64;
+  __shared__ __attribute__((aligned(16))) float As[BK * IA::LD];
+  __shared__ __attribute__((aligned(16))) float Bs[BK * IB::LD];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
   const int m0 = blockIdx.y * BM;
   const int n0 = blockIdx.x * BN;
   const int kbeg = blockIdx.z * a.kchunk;
   const int kend = min(a.K, kbeg + a.kchunk);
 
-  float ra[LA], rb[LB];
-
-  auto load_tile = [&](int k0) {
-#pragma unroll
-    for (int i = 0; i < LA; ++i) {
-      int e = tid + i * NT;
-      int m, k;
-      if (a.transA) { m = e % BM; k = e / BM; } else { m = e / BK; k = e % BK; }
-      int gm = m0 + m, gk = k0 + k;
-      float v = 0.0f;
-      if (gm < a.M && gk < kend) {
-        v = a.transA ? a.A[a.amap.off(gk) + gm] : a.A[a.amap.off(gm) + gk];
-      }
-      ra[i] = v;
-    }
-#pragma unroll
-    for (int i = 0; i < LB; ++i) {
-      int e = tid + i * NT;
-      int n, k;
-      if (a.transB) { k = e % BK; n = e / BK; } else { n = e % BN; k = e / BN; }
-      int gn = n0 + n, gk = k0 + k;
-      float v = 0.0f;
-      if (gn < a.N && gk < kend) {
-        v = a.transB ? a.B[a.bmap.off(gn) + gk] : a.B[a.bmap.off(gk) + gn];
-      }
-      rb[i] = v;
-    }
-  };
-  auto store_tile = [&]() {
-#pragma unroll
-    for (int i = 0; i < LA; ++i) {
-      int e = tid + i * NT;
-      int m, k;
-      if (a.transA) { m = e % BM; k = e / BM; } else { m = e / BK; k = e % BK; }
-      As[k][m] = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < LB; ++i) {
-      int e = tid + i * NT;
-      int n, k;
-      if (a.transB) { k = e % BK; n = e / BK; } else { n = e % BN; k = e / BN; }
-      Bs[k][n] = rb[i];
-    }
-  };
-
+  IA ia;
+  IB ib;
   f32x16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -126,18 +150,25 @@ __global__ __launch_bounds__(NT) void gemm_f32_kernel(GemmArgs a) {
   const int wn = (wave & 1) * (BN / 2);
   const int lr = lane & 31, lk = lane >> 5;
 
-  if (kbeg < kend) load_tile(kbeg);
+  if (kbeg < kend) {
+    ia.load(a.A, a.amap, m0, a.M, kbeg, kend);
+    ib.load(a.B, a.bmap, n0, a.N, kbeg, kend);
+  }
   for (int k0 = kbeg; k0 < kend; k0 += BK) {
-    store_tile();
+    ia.store(As);
+    ib.store(Bs);
     __syncthreads();
-    if (k0 + BK < kend) load_tile(k0 + BK);
+    if (k0 + BK < kend) {  // next tile's global loads fly under this tile's MFMAs
+      ia.load(a.A, a.amap, m0, a.M, k0 + BK, kend);
+      ib.load(a.B, a.bmap, n0, a.N, k0 + BK, kend);
+    }
 #pragma unroll
     for (int kk = 0; kk < BK / 2; ++kk) {
       float fa[TM], fb[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) fa[i] = As[2 * kk + lk][wm + i * 32 + lr];
+      for (int i = 0; i < TM; ++i) fa[i] = As[(2 * kk + lk) * IA::LD + wm + i * 32 + lr];
 #pragma unroll
-      for (int j = 0; j < TN; ++j) fb[j] = Bs[2 * kk + lk][wn + j * 32 + lr];
+      for (int j = 0; j < TN; ++j) fb[j] = Bs[(2 * kk + lk) * IB::LD + wn + j * 32 + lr];
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -173,27 +204,78 @@ __global__ void splitk_reduce_kernel(GemmArgs a, int splits) {
   a.C[(long)m * a.ldc + n] = apply_epi(a, s, m, n);
 }
 
-// column sums: part[s][n] = sum over rows [s*rows_per, ...) of X(row, n)
-__global__ void colsum_partial_kernel(const float* X, RowMap map, int rows, int N,
-                                      int rows_per, float* part) {
-  int n = blockIdx.x * blockDim.x + threadIdx.x;
-  int s = blockIdx.y;
-  if (n >= N) return;
-  int r0 = s * rows_per, r1 = min(rows, r0 + rows_per);
+// column sums, stage 1: part[s][n] = sum of X(row, n) over rows [s*rows_per, (s+1)*rows_per).
+// A block owns 64 columns (one per lane: 256-B coalesced row segments); its 4 waves
+// interleave over the rows, then combine through LDS.
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const float* X, RowMap map, int rows, int N,
+                                                             int rows_per, float* part) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + lane;
+  const int s = blockIdx.y;
+  const int r0 = s * rows_per, r1 = min(rows, r0 + rows_per);
   float acc = 0.0f;
-  for (int r = r0; r < r1; ++r) acc += X[map.off(r) + n];
-  part[(long)s * N + n] = acc;
+  if (n < N) {
+    int r = r0 + wave;
+    for (; r + 12 < r1; r += 16) {  // 4 independent loads in flight per lane
+      float a0 = X[map.off(r) + n], a1 = X[map.off(r + 4) + n];
+      float a2 = X[map.off(r + 8) + n], a3 = X[map.off(r + 12) + n];
+      acc += (a0 + a1) + (a2 + a3);
+    }
+    for (; r < r1; r += 4) acc += X[map.off(r) + n];
+  }
+  red[wave][lane] = acc;
+  __syncthreads();
+  if (wave == 0 && n < N) part[(long)s * N + n] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
-__global__ void colsum_final_kernel(const float* part, int S, int N, float beta, float* out,
-                                    float* out2) {
-  int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
+// stage 2: out[n] = beta*out[n] + sum_s part[s][n]; out2 (nullable) receives the same update.
+// 16 waves per 64 columns, fixed combine order (deterministic).
+__global__ __launch_bounds__(1024) void colsum_final_kernel(const float* part, int S, int N, float beta, float* out,
+                                                            float* out2) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + lane;
   float acc = 0.0f;
-  for (int s = 0; s < S; ++s) acc += part[(long)s * N + n];
-  float v = (beta != 0.0f ? beta * out[n] : 0.0f) + acc;
-  out[n] = v;
-  if (out2) out2[n] = (beta != 0.0f ? beta * out2[n] : 0.0f) + acc;
+  if (n < N) {
+#pragma unroll 4
+    for (int s = wave; s < S; s += 16) acc += part[(long)s * N + n];
+  }
+  red[wave][lane] = acc;
+  __syncthreads();
+  if (wave == 0 && n < N) {
+    float v = 0.0f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) v += red[w][lane];
+    out[n] = (beta != 0.0f ? beta * out[n] : 0.0f) + v;
+    if (out2) out2[n] = (beta != 0.0f ? beta * out2[n] : 0.0f) + v;
+  }
+}
+
+template <int BM, int BN>
+static void launch_tile(const GemmArgs& a, int ta, int tb, bool va, bool vb, int splits, hipStream_t s) {
+  dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM, splits);
+  const int code = (ta << 3) | (tb << 2) | ((int)va << 1) | (int)vb;
+  switch (code) {
+#define MRG_G(TA, TB, VA, VB) \
+    case (TA << 3) | (TB << 2) | (VA << 1) | VB: \
+      gemm_f32_kernel<BM, BN, TA, TB, (bool)VA, (bool)VB><<<grid, NT, 0, s>>>(a); break;
+    MRG_G(0, 0, 0, 0) MRG_G(0, 0, 0, 1) MRG_G(0, 0, 1, 0) MRG_G(0, 0, 1, 1)
+    MRG_G(0, 1, 0, 0) MRG_G(0, 1, 0, 1) MRG_G(0, 1, 1, 0) MRG_G(0, 1, 1, 1)
+    MRG_G(1, 0, 0, 0) MRG_G(1, 0, 0, 1) MRG_G(1, 0, 1, 0) MRG_G(1, 0, 1, 1)
+    MRG_G(1, 1, 0, 0) MRG_G(1, 1, 0, 1) MRG_G(1, 1, 1, 0) MRG_G(1, 1, 1, 1)
+#undef MRG_G
+  }
+}
+
+static int launch_gemm(const GemmArgs& a, int tile, int ta, int tb, bool va, bool vb, int splits,
+                       hipStream_t s) {
+  ta = ta ? 1 : 0;
+  tb = tb ? 1 : 0;
+  if (tile == 0) launch_tile<128, 128>(a, ta, tb, va, vb, splits, s);
+  else if (tile == 1) launch_tile<128, 64>(a, ta, tb, va, vb, splits, s);
+  else launch_tile<64, 64>(a, ta, tb, va, vb, splits, s);
+  return 0;
 }
 
 }  // namespace mrg
@@ -228,18 +310,16 @@ MRG_API int mrg_gemm_f32(int M, int N, int K, float alpha,
   if (splits < 1) splits = 1;
   a.kchunk = kc;
   a.ws = splits > 1 ? workspace : nullptr;
-  const bool bigM = M >= 2048, bigN = N > 64;
-  dim3 block(NT);
-  if (bigM && bigN) {
-    dim3 grid((N + 127) / 128, (M + 127) / 128, splits);
-    gemm_f32_kernel<128, 128><<<grid, block, 0, stream>>>(a);
-  } else if (bigM) {
-    dim3 grid((N + 63) / 64, (M + 127) / 128, splits);
-    gemm_f32_kernel<128, 64><<<grid, block, 0, stream>>>(a);
-  } else {
-    dim3 grid((N + 63) / 64, (M + 63) / 64, splits);
-    gemm_f32_kernel<64, 64><<<grid, block, 0, stream>>>(a);
-  }
+  // vector (float4) global loads need 16-B aligned rows along the contiguous index
+  auto aligned = [](const float* p, const RowMap& m) {
+    return ((uintptr_t)p & 15) == 0 && (m.ld_lo & 3) == 0 && (m.rdiv <= 0 || (m.ld_hi & 3) == 0);
+  };
+  const bool va = aligned(A, a.amap), vb = aligned(B, a.bmap);
+  int tile;  // 0: 128x128, 1: 128x64, 2: 64x64
+  if (M >= 2048 && N > 64) tile = ((long)((M + 127) / 128) * ((N + 127) / 128) * splits >= 400) ? 0 : 1;
+  else if (M >= 2048) tile = 1;
+  else tile = 2;
+  if (launch_gemm(a, tile, transA, transB, va, vb, splits, stream)) return 2;
   if (check_launch("gemm_f32_kernel")) return 1;
   if (splits > 1) {
     long total = (long)M * N;
@@ -249,9 +329,13 @@ MRG_API int mrg_gemm_f32(int M, int N, int K, float alpha,
   return 0;
 }
 
+static int colsum_splits(int rows) {
+  int s = (rows + 63) / 64;  // 64 rows per stage-1 block
+  return s < 1 ? 1 : (s > 512 ? 512 : s);
+}
+
 MRG_API size_t mrg_colsum_workspace_bytes(int rows, int N) {
-  int S = rows >= 4096 ? 64 : (rows >= 256 ? 16 : 1);
-  return (size_t)S * N * sizeof(float);
+  return (size_t)colsum_splits(rows) * N * sizeof(float);
 }
 
 // out[n] = beta*out[n] + sum_rows X(row, n)   (bias gradients; out2 optional mirror for b_hh)
@@ -259,13 +343,12 @@ MRG_API int mrg_colsum_f32(int rows, int N, const float* X, long ld, long ld_hi,
                            float beta, float* out, float* out2, float* workspace,
                            hipStream_t stream) {
   if (N == 0) return 0;
-  int S = rows >= 4096 ? 64 : (rows >= 256 ? 16 : 1);
+  int S = colsum_splits(rows);
   int rows_per = (rows + S - 1) / S;
   if (rows_per == 0) rows_per = 1;
-  dim3 grid((N + 255) / 256, S);
-  colsum_partial_kernel<<<grid, 256, 0, stream>>>(X, RowMap{ld, ld_hi, rdiv}, rows, N, rows_per,
-                                                  workspace);
+  dim3 grid((N + 63) / 64, S);
+  colsum_partial_kernel<<<grid, 256, 0, stream>>>(X, RowMap{ld, ld_hi, rdiv}, rows, N, rows_per, workspace);
   if (check_launch("colsum_partial_kernel")) return 1;
-  colsum_final_kernel<<<(N + 255) / 256, 256, 0, stream>>>(workspace, S, N, beta, out, out2);
+  colsum_final_kernel<<<(N + 63) / 64, 1024, 0, stream>>>(workspace, S, N, beta, out, out2);
   return check_launch("colsum_final_kernel");
 }

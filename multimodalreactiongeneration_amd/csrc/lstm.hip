@@ -37,7 +37,6 @@
 
 namespace mrg {
 
-static constexpr int NT = 256;
 static constexpr int MAXP = 4;
 
 struct LstmFwdProblem {
@@ -77,12 +76,24 @@ struct LstmFwdArgs {
   LstmFwdProblem p[MAXP];
   int nprob, B, T;
   int* err;
+  unsigned long long* stamps;  // diagnostics only (mrg_lstm_debug_stamps); null in normal use
 };
 struct LstmBwdArgs {
   LstmBwdProblem p[MAXP];
   int nprob, B, T;
   int* err;
+  unsigned long long* stamps;
 };
+
+// Phase stamps of block 0 / thread 0 (shader-clock s_memtime), [T][8] per launch.
+#define MRG_STAMP(ph)                                                                  \
+  do {                                                                                 \
+    if (args.stamps && blockIdx.x == 0 && threadIdx.x == 0) {                          \
+      unsigned long long _t;                                                           \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");     \
+      args.stamps[(long)tt * 8 + (ph)] = _t;                                           \
+    }                                                                                  \
+  } while (0)
 
 static constexpr unsigned SPIN_LIMIT = 1u << 22;
 
@@ -94,23 +105,48 @@ __device__ __forceinline__ void put_granule(unsigned long long* g, unsigned tag,
   __hip_atomic_store(g, make_granule(tag, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Poll one granule until its tag matches; bounded.  `dead` latches after a
-// timeout so a broken launch drains quickly instead of spinning every step.
-__device__ __forceinline__ float get_granule(unsigned long long* g, unsigned tag, int* err, bool& dead) {
-  unsigned long long v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if ((unsigned)(v >> 32) != tag && !dead) {
-    unsigned spins = 0;
-    do {
-      __builtin_amdgcn_s_sleep(1);
-      v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (++spins > SPIN_LIMIT) {
-        atomicOr(err, 1);
-        dead = true;
-        break;
-      }
-    } while ((unsigned)(v >> 32) != tag);
+// Sum over aligned groups of N consecutive lanes with DPP (VALU, no LDS traffic):
+// quad_perm xor1, xor2, then row_half_mirror and row_mirror pair the quads / octets.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int N>
+__device__ __forceinline__ float group_sum(float v) {
+  static_assert(N == 1 || N == 2 || N == 4 || N == 8 || N == 16, "group_sum");
+  if (N >= 2) v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+  if (N >= 4) v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
+  if (N >= 8) v += dpp_f<0x141>(v);  // row_half_mirror
+  if (N >= 16) v += dpp_f<0x140>(v); // row_mirror
+  return v;
+}
+
+// Poll N granules at once: all loads issued back-to-back (one round trip), then
+// only the stale ones are re-polled.  Bounded like get_granule.
+template <int N>
+__device__ __forceinline__ void get_granules(unsigned long long* base, long stride, unsigned tag, float (&out)[N],
+                                             int* err, bool& dead) {
+  unsigned long long v[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = __hip_atomic_load(base + i * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned spins = 0;
+  while (!dead) {
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < N; ++i) ok &= (unsigned)(v[i] >> 32) == tag;
+    if (ok) break;
+    if (++spins > SPIN_LIMIT) {
+      atomicOr(err, 1);
+      dead = true;
+      break;
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      if ((unsigned)(v[i] >> 32) != tag)
+        v[i] = __hip_atomic_load(base + i * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  return __uint_as_float((unsigned)v);
+#pragma unroll
+  for (int i = 0; i < N; ++i) out[i] = __uint_as_float((unsigned)v[i]);
 }
 
 // block -> (problem, group, member); members of a group share blockIdx % 8 (one XCD)
@@ -131,14 +167,31 @@ __device__ __forceinline__ void decompose(int G, int ngroups_per_prob, int nprob
   grp = gid % ngroups_per_prob;
 }
 
+// Threads per workgroup and resident workgroups per CU for a (hidden size, group size):
+//   H = 256, G = 8  : 512 threads (64 W_hh values per lane), 2 workgroups per CU
+//   H = 256, G = 16 : 256 threads (64 W_hh values per lane), 4 workgroups per CU
+//   H <= 128        : 256 threads, 2 workgroups per CU
+// waves_per_simd bounds VGPRs at 512 / waves (128 here) so the whole grid stays resident.
+template <int H, int G>
+struct LstmNT {
+  static constexpr int value = (H >= 256 && H / G >= 32) ? 512 : 256;
+  static constexpr int waves_per_simd = H >= 256 ? 4 : 2;
+};
+
 template <int H, int G, int BS>
-__global__ __launch_bounds__(NT) void lstm_fwd_kernel(LstmFwdArgs args) {
+__global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_simd)) void lstm_fwd_kernel(LstmFwdArgs args) {
+  constexpr int NT = LstmNT<H, G>::value;
   constexpr int U = H / G;
   constexpr int R = 4 * U;
-  constexpr int KC = NT / R;
+  // register blocking of the recurrent GEMV: a thread owns RT gate rows x KL hidden inputs, the
+  // KC lanes of a row group split the hidden dimension (DPP-reduced), so every h value read from
+  // LDS feeds RT FMAs (the GEMV is LDS-issue bound otherwise)
+  // (fewer rows per thread at large batch tiles keeps acc[RT][BS] + W inside 128 VGPRs)
+  constexpr int KC = (H >= 128) ? ((BS >= 4 ? 2 : 4) * NT / R) : ((H / 4 < 16) ? H / 4 : 16);
+  constexpr int RT = R * KC / NT;
   constexpr int KL = H / KC;
-  constexpr int KLP = KL + 4;
-  static_assert(NT % R == 0 && H % KC == 0 && BS * U <= NT && (KL % 4) == 0, "bad LSTM tiling");
+  constexpr int KLP = ((KL / 4) % 2 == 0) ? KL + 4 : KL;  // odd 16-B chunk pitch: conflict-free b128
+  static_assert(RT >= 1 && RT * NT == R * KC && (KL % 4) == 0 && BS * U <= NT, "bad LSTM tiling");
   __shared__ __attribute__((aligned(16))) float hs[BS][KC][KLP];
   __shared__ float pre[BS][R];
 
@@ -151,14 +204,18 @@ __global__ __launch_bounds__(NT) void lstm_fwd_kernel(LstmFwdArgs args) {
   const int b0 = grp * BS;
   bool dead = false;
 
-  // dot role: gate row r, k-chunk kc
-  const int r = tid / KC, kc = tid % KC;
-  const int grow = (r / U) * H + j * U + (r % U);
-  float w[KL];
+  // dot role: row group rg (rows rg*RT .. +RT-1), k-chunk kc
+  const int rg = tid / KC, kc = tid % KC;
+  float w[RT][KL];
 #pragma unroll
-  for (int i = 0; i < KL; i += 4) {
-    float4 v = *reinterpret_cast<const float4*>(P.w_hh + (long)grow * H + kc * KL + i);
-    w[i] = v.x; w[i + 1] = v.y; w[i + 2] = v.z; w[i + 3] = v.w;
+  for (int q = 0; q < RT; ++q) {
+    const int r = rg * RT + q;
+    const int grow = (r / U) * H + j * U + (r % U);
+#pragma unroll
+    for (int i = 0; i < KL; i += 4) {
+      float4 v = *reinterpret_cast<const float4*>(P.w_hh + (long)grow * H + kc * KL + i);
+      w[q][i] = v.x; w[q][i + 1] = v.y; w[q][i + 2] = v.z; w[q][i + 3] = v.w;
+    }
   }
 
   // cell role
@@ -196,31 +253,36 @@ __global__ __launch_bounds__(NT) void lstm_fwd_kernel(LstmFwdArgs args) {
   unsigned long long* xb = P.xbuf;
   for (int tt = 0; tt < T; ++tt) {
     const int t = P.reverse ? T - 1 - tt : tt;
-    // 1. recurrent GEMV for this member's R gate rows
-    float acc[BS];
+    MRG_STAMP(0);
+    // 1. recurrent GEMV for this member's R gate rows, one batch row at a time (short live ranges)
 #pragma unroll
     for (int b = 0; b < BS; ++b) {
-      float s = 0.0f;
+      float acc[RT];
+#pragma unroll
+      for (int q = 0; q < RT; ++q) acc[q] = 0.0f;
       const float* hp = &hs[b][kc][0];
 #pragma unroll
       for (int i = 0; i < KL; i += 4) {
         float4 hv = *reinterpret_cast<const float4*>(hp + i);
-        s = fmaf(w[i], hv.x, s);
-        s = fmaf(w[i + 1], hv.y, s);
-        s = fmaf(w[i + 2], hv.z, s);
-        s = fmaf(w[i + 3], hv.w, s);
+#pragma unroll
+        for (int q = 0; q < RT; ++q) {
+          acc[q] = fmaf(w[q][i], hv.x, acc[q]);
+          acc[q] = fmaf(w[q][i + 1], hv.y, acc[q]);
+          acc[q] = fmaf(w[q][i + 2], hv.z, acc[q]);
+          acc[q] = fmaf(w[q][i + 3], hv.w, acc[q]);
+        }
       }
-      acc[b] = s;
+      if (b == 0) MRG_STAMP(1);
+#pragma unroll
+      for (int q = 0; q < RT; ++q) acc[q] = group_sum<KC>(acc[q]);
+      if (kc == 0) {
+#pragma unroll
+        for (int q = 0; q < RT; ++q) pre[b][rg * RT + q] = acc[q];
+      }
     }
-#pragma unroll
-    for (int off = KC / 2; off >= 1; off >>= 1)
-#pragma unroll
-      for (int b = 0; b < BS; ++b) acc[b] += __shfl_xor(acc[b], off, 64);
-    if (kc == 0) {
-#pragma unroll
-      for (int b = 0; b < BS; ++b) pre[b][r] = acc[b];
-    }
+    MRG_STAMP(2);
     __syncthreads();
+    MRG_STAMP(3);
     // 2. gates + cell update, 3. publish
     const int par = tt & 1;
     if (cvalid) {
@@ -238,17 +300,38 @@ __global__ __launch_bounds__(NT) void lstm_fwd_kernel(LstmFwdArgs args) {
       P.cs[((long)bg * T + t) * H + hcol] = c;
       if (tt + 1 < T) load_gx(P.reverse ? t - 1 : t + 1);
     }
+    MRG_STAMP(4);
     // 4. gather h_t of the whole group
     if (tt + 1 < T) {
-      for (int e = tid; e < BS * H; e += NT) {
-        int b = e / H, k = e % H;
-        float v = 0.0f;
-        if (b0 + b < B)
-          v = get_granule(xb + ((long)par * B + b0 + b) * H + k, (unsigned)(tt + 1), args.err, dead);
-        hs[b][k / KL][k % KL] = v;
+      constexpr int NG = (BS * H + NT - 1) / NT;  // granules per thread, NT apart
+      float gv[NG];
+      // the group's rows are contiguous in the ring: granule e of the group sits at row_base + e.
+      // A ragged last group (b0 + b >= B) re-reads its last valid row (published, value unused).
+      const int nvalid = min(BS, B - b0) * H;
+      unsigned long long* rb = xb + ((long)par * B + b0) * H;
+      if ((BS * H) % NT == 0 && nvalid == BS * H) {
+        get_granules<NG>(rb + tid, NT, (unsigned)(tt + 1), gv, args.err, dead);
+      } else {
+#pragma unroll
+        for (int i = 0; i < NG; ++i) {
+          float one[1];
+          int e = min(tid + i * NT, nvalid - 1);
+          get_granules<1>(rb + e, 0, (unsigned)(tt + 1), one, args.err, dead);
+          gv[i] = one[0];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NG; ++i) {
+        int e = tid + i * NT;
+        if (e < BS * H) {
+          int b = e / H, k = e % H;
+          hs[b][k / KL][k % KL] = (b0 + b < B) ? gv[i] : 0.0f;
+        }
       }
     }
+    MRG_STAMP(5);
     __syncthreads();
+    MRG_STAMP(6);
   }
   if (cvalid) {
     if (P.hT) P.hT[(long)bg * H + hcol] = h;
@@ -257,13 +340,19 @@ __global__ __launch_bounds__(NT) void lstm_fwd_kernel(LstmFwdArgs args) {
 }
 
 template <int H, int G, int BS>
-__global__ __launch_bounds__(NT) void lstm_bwd_kernel(LstmBwdArgs args) {
+__global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_simd)) void lstm_bwd_kernel(LstmBwdArgs args) {
+  constexpr int NT = LstmNT<H, G>::value;
   constexpr int U = H / G;
   constexpr int R = 4 * U;
-  constexpr int TP = NT / H;  // threads per output column of the partial product
-  constexpr int RL = R / TP;  // W rows per thread
-  static_assert(NT % H == 0 && R % TP == 0 && BS * U <= NT && (RL % 4) == 0, "bad LSTM bwd tiling");
-  __shared__ __attribute__((aligned(16))) float dgl[BS][R];
+  // a thread owns OT consecutive outputs (hidden units of dh_{t-1}) x RL gate rows; the RC lanes of
+  // an output group split the rows (DPP-reduced): each dG value read from LDS feeds OT FMAs
+  constexpr int RC = (H >= 128) ? 8 : 16;
+  constexpr int OT = RC * H / NT;
+  constexpr int RL = R / RC;
+  constexpr int RLP = ((RL / 4) % 2 == 0) ? RL + 4 : RL;
+  static_assert(OT >= 1 && OT * NT == RC * H && RL * RC == R && (RL % 4) == 0 && BS * U <= NT &&
+                (U % OT) == 0, "bad LSTM bwd tiling");
+  __shared__ __attribute__((aligned(16))) float dgl[BS][RC][RLP];
 
   int prob, grp, j;
   const int ngroups = (args.B + BS - 1) / BS;
@@ -274,14 +363,15 @@ __global__ __launch_bounds__(NT) void lstm_bwd_kernel(LstmBwdArgs args) {
   const int b0 = grp * BS;
   bool dead = false;
 
-  // dot role: output column hout, row chunk rc; w[i] = W_hh[grow(rc*RL+i)][hout]
-  const int hout = tid / TP, rc = tid % TP;
-  float w[RL];
+  // dot role: w[o][i] = W_hh[grow(rc*RL + i)][ogr*OT + o]
+  const int ogr = tid / RC, rc = tid % RC;
+  float w[OT][RL];
 #pragma unroll
   for (int i = 0; i < RL; ++i) {
-    int rr = rc * RL + i;
-    int grow = (rr / U) * H + j * U + (rr % U);
-    w[i] = P.w_hh[(long)grow * H + hout];
+    const int rr = rc * RL + i;
+    const int grow = (rr / U) * H + j * U + (rr % U);
+#pragma unroll
+    for (int o = 0; o < OT; ++o) w[o][i] = P.w_hh[(long)grow * H + ogr * OT + o];
   }
 
   const bool cell = tid < BS * U;
@@ -298,110 +388,180 @@ __global__ __launch_bounds__(NT) void lstm_bwd_kernel(LstmBwdArgs args) {
 
   unsigned long long* xb = P.xbuf;
   const long xstride_b = (long)G * H;  // per batch row: [dest G][src G][U]
+  // saved activations of the next step to process, prefetched one step ahead so
+  // their HBM latency hides under the hand-off wait
+  float ig = 0.f, fg = 0.f, gg = 0.f, og = 0.f, cc = 0.f, cp = 0.f, dyv = 0.f;
+  auto prefetch = [&](int t) {
+    if (!cvalid) return;
+    const int tp = P.reverse ? t + 1 : t - 1;
+    const float* gs = P.gates + ((long)bg * T + t) * 4 * H + hcol;
+    ig = gs[0]; fg = gs[H]; gg = gs[2 * H]; og = gs[3 * H];
+    cc = P.cs[((long)bg * T + t) * H + hcol];
+    cp = (tp >= 0 && tp < T) ? P.cs[((long)bg * T + tp) * H + hcol] : (P.c0 ? P.c0[(long)bg * H + hcol] : 0.0f);
+    dyv = P.dy ? P.dy[(long)bg * P.dy_bs + (long)t * P.dy_ts + hcol] : 0.0f;
+  };
+  prefetch(P.reverse ? 0 : T - 1);
   for (int tt = 0; tt < T; ++tt) {
     const int t = P.reverse ? tt : T - 1 - tt;
-    const int tprev = P.reverse ? t + 1 : t - 1;  // forward-time predecessor
+    MRG_STAMP(0);
     if (cvalid) {
       if (tt > 0) {
         const int par = (tt - 1) & 1;
         unsigned long long* g = xb + ((long)par * B + bg) * xstride_b + (long)j * H + cu;
+        float gv[G];
+        get_granules<G>(g, U, (unsigned)tt, gv, args.err, dead);
         float s = 0.0f;
 #pragma unroll
-        for (int src = 0; src < G; ++src) s += get_granule(g + src * U, (unsigned)tt, args.err, dead);
+        for (int src = 0; src < G; ++src) s += gv[src];
         dhrec = s;
       }
-      float dh = dhrec;
-      if (P.dy) dh += P.dy[(long)bg * P.dy_bs + (long)t * P.dy_ts + hcol];
-      const float* gs = P.gates + ((long)bg * T + t) * 4 * H + hcol;
-      float ig = gs[0], fg = gs[H], gg = gs[2 * H], og = gs[3 * H];
-      float cc = P.cs[((long)bg * T + t) * H + hcol];
-      float cp = 0.0f;
-      if (tprev >= 0 && tprev < T) cp = P.cs[((long)bg * T + tprev) * H + hcol];
-      else if (P.c0) cp = P.c0[(long)bg * H + hcol];
-      float tc = tanhf_(cc);
-      float dc = dh * og * (1.0f - tc * tc) + dcn;
-      float d_o = dh * tc * og * (1.0f - og);
-      float d_i = dc * gg * ig * (1.0f - ig);
-      float d_f = dc * cp * fg * (1.0f - fg);
-      float d_g = dc * ig * (1.0f - gg * gg);
+      MRG_STAMP(1);
+      const float dh = dhrec + dyv;
+      const float tc = tanhf_(cc);
+      const float dc = dh * og * (1.0f - tc * tc) + dcn;
+      const float d_o = dh * tc * og * (1.0f - og);
+      const float d_i = dc * gg * ig * (1.0f - ig);
+      const float d_f = dc * cp * fg * (1.0f - fg);
+      const float d_g = dc * ig * (1.0f - gg * gg);
       dcn = dc * fg;
       float* dgp = P.dG + ((long)bg * T + t) * 4 * H + hcol;
       dgp[0] = d_i; dgp[H] = d_f; dgp[2 * H] = d_g; dgp[3 * H] = d_o;
-      dgl[cb][0 * U + cu] = d_i;
-      dgl[cb][1 * U + cu] = d_f;
-      dgl[cb][2 * U + cu] = d_g;
-      dgl[cb][3 * U + cu] = d_o;
+      {
+        const int r0 = 0 * U + cu, r1 = 1 * U + cu, r2 = 2 * U + cu, r3 = 3 * U + cu;
+        dgl[cb][r0 / RL][r0 % RL] = d_i;
+        dgl[cb][r1 / RL][r1 % RL] = d_f;
+        dgl[cb][r2 / RL][r2 % RL] = d_g;
+        dgl[cb][r3 / RL][r3 % RL] = d_o;
+      }
+      if (tt + 1 < T) prefetch(P.reverse ? t + 1 : t - 1);
+      MRG_STAMP(2);
     } else if (cell) {
-      dgl[cb][cu] = 0.0f; dgl[cb][U + cu] = 0.0f; dgl[cb][2 * U + cu] = 0.0f; dgl[cb][3 * U + cu] = 0.0f;
-    }
-    __syncthreads();
-    // partial dh_{t-1}[b][hout] = sum over this member's rows of dG[b][row] * W_hh[row][hout]
-    // (batch loop kept rolled: the 128 W registers stay resident without spilling)
-    {
-      const int par = tt & 1;
-      const int dest = hout / U, du = hout % U;
-#pragma unroll 1
-      for (int b = 0; b < BS; ++b) {
-        float s = 0.0f;
-        const float* dp = &dgl[b][rc * RL];
 #pragma unroll
-        for (int i = 0; i < RL; i += 4) {
-          float4 dv = *reinterpret_cast<const float4*>(dp + i);
-          s = fmaf(dv.x, w[i], s);
-          s = fmaf(dv.y, w[i + 1], s);
-          s = fmaf(dv.z, w[i + 2], s);
-          s = fmaf(dv.w, w[i + 3], s);
-        }
-#pragma unroll
-        for (int off = TP / 2; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
-        if (rc == 0 && b0 + b < B)
-          put_granule(xb + ((long)par * B + b0 + b) * xstride_b + (long)dest * H + (long)j * U + du,
-                      (unsigned)(tt + 1), s);
+      for (int q = 0; q < 4; ++q) {
+        const int rr = q * U + cu;
+        dgl[cb][rr / RL][rr % RL] = 0.0f;
       }
     }
     __syncthreads();
+    MRG_STAMP(3);
+    // partial dh_{t-1}[b][hout] = sum over this member's rows of dG[b][row] * W_hh[row][hout]
+    {
+      const int par = tt & 1;
+      float acc[OT][BS];
+#pragma unroll
+      for (int o = 0; o < OT; ++o)
+#pragma unroll
+        for (int b = 0; b < BS; ++b) acc[o][b] = 0.0f;
+#pragma unroll
+      for (int b = 0; b < BS; ++b) {
+        const float* dp = &dgl[b][rc][0];
+#pragma unroll
+        for (int i = 0; i < RL; i += 4) {
+          float4 dv = *reinterpret_cast<const float4*>(dp + i);
+#pragma unroll
+          for (int o = 0; o < OT; ++o) {
+            acc[o][b] = fmaf(dv.x, w[o][i], acc[o][b]);
+            acc[o][b] = fmaf(dv.y, w[o][i + 1], acc[o][b]);
+            acc[o][b] = fmaf(dv.z, w[o][i + 2], acc[o][b]);
+            acc[o][b] = fmaf(dv.w, w[o][i + 3], acc[o][b]);
+          }
+        }
+      }
+      MRG_STAMP(4);
+#pragma unroll
+      for (int o = 0; o < OT; ++o)
+#pragma unroll
+        for (int b = 0; b < BS; ++b) acc[o][b] = group_sum<RC>(acc[o][b]);
+      if (rc == 0) {
+        const int h0 = ogr * OT;
+        const int dest = h0 / U, du = h0 % U;
+#pragma unroll
+        for (int b = 0; b < BS; ++b) {
+          if (b0 + b < B) {
+            unsigned long long* gq = xb + ((long)par * B + b0 + b) * xstride_b + (long)dest * H + (long)j * U + du;
+#pragma unroll
+            for (int o = 0; o < OT; ++o) put_granule(gq + o, (unsigned)(tt + 1), acc[o][b]);
+          }
+        }
+      }
+    }
+    MRG_STAMP(5);
+    __syncthreads();
+    MRG_STAMP(6);
   }
   if (cvalid) {
     if (P.dh0) {
       const int par = (T - 1) & 1;
       unsigned long long* g = xb + ((long)par * B + bg) * xstride_b + (long)j * H + cu;
+      float gv[G];
+      get_granules<G>(g, U, (unsigned)T, gv, args.err, dead);
       float s = 0.0f;
 #pragma unroll
-      for (int src = 0; src < G; ++src) s += get_granule(g + src * U, (unsigned)T, args.err, dead);
+      for (int src = 0; src < G; ++src) s += gv[src];
       P.dh0[(long)bg * H + hcol] = s;
     }
     if (P.dc0) P.dc0[(long)bg * H + hcol] = dcn;
   }
 }
 
-template <int H, int G>
-static int launch_fwd(const LstmFwdArgs& a, int BS, int nblk, hipStream_t s) {
-  switch (BS) {
-    case 1: lstm_fwd_kernel<H, G, 1><<<nblk, NT, 0, s>>>(a); break;
-    case 2: lstm_fwd_kernel<H, G, 2><<<nblk, NT, 0, s>>>(a); break;
-    case 4: lstm_fwd_kernel<H, G, 4><<<nblk, NT, 0, s>>>(a); break;
-    case 8: lstm_fwd_kernel<H, G, 8><<<nblk, NT, 0, s>>>(a); break;
-    default: set_error("lstm fwd: bad BS %d", BS); return 2;
-  }
-  return check_launch("lstm_fwd_kernel");
+// Persistent launches need every workgroup of a group resident: pick the smallest
+// batch tile BS whose grid fits the occupancy the HW reports for that kernel, or fail.
+template <typename K>
+static bool fits(K kernel, int nt, long nblk, int cus) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kernel), nt, 0) !=
+      hipSuccess)
+    return false;
+  return nblk <= (long)per_cu * cus;
 }
 
 template <int H, int G>
-static int launch_bwd(const LstmBwdArgs& a, int BS, int nblk, hipStream_t s) {
-  switch (BS) {
-    case 1: lstm_bwd_kernel<H, G, 1><<<nblk, NT, 0, s>>>(a); break;
-    case 2: lstm_bwd_kernel<H, G, 2><<<nblk, NT, 0, s>>>(a); break;
-    case 4: lstm_bwd_kernel<H, G, 4><<<nblk, NT, 0, s>>>(a); break;
-    case 8: lstm_bwd_kernel<H, G, 8><<<nblk, NT, 0, s>>>(a); break;
-    default: set_error("lstm bwd: bad BS %d", BS); return 2;
+static int launch_fwd(const LstmFwdArgs& a, int force_bs, int cus, hipStream_t s) {
+  constexpr int NT = LstmNT<H, G>::value;
+  const long groups1 = a.B;
+  for (int bs = 1; bs <= 8; bs *= 2) {
+    if (force_bs > 0 && bs != force_bs) continue;
+    long nblk = (long)a.nprob * ((groups1 + bs - 1) / bs) * G;
+    bool ok;
+    switch (bs) {
+      case 1: ok = fits(lstm_fwd_kernel<H, G, 1>, NT, nblk, cus); if (ok) lstm_fwd_kernel<H, G, 1><<<nblk, NT, 0, s>>>(a); break;
+      case 2: ok = fits(lstm_fwd_kernel<H, G, 2>, NT, nblk, cus); if (ok) lstm_fwd_kernel<H, G, 2><<<nblk, NT, 0, s>>>(a); break;
+      case 4: ok = fits(lstm_fwd_kernel<H, G, 4>, NT, nblk, cus); if (ok) lstm_fwd_kernel<H, G, 4><<<nblk, NT, 0, s>>>(a); break;
+      default: ok = fits(lstm_fwd_kernel<H, G, 8>, NT, nblk, cus); if (ok) lstm_fwd_kernel<H, G, 8><<<nblk, NT, 0, s>>>(a); break;
+    }
+    if (ok) return check_launch("lstm_fwd_kernel");
   }
-  return check_launch("lstm_bwd_kernel");
+  set_error("lstm fwd: persistent grid does not fit the GPU (nprob=%d B=%d H=%d force_bs=%d)", a.nprob, a.B, H,
+            force_bs);
+  return 4;
+}
+
+template <int H, int G>
+static int launch_bwd(const LstmBwdArgs& a, int force_bs, int cus, hipStream_t s) {
+  constexpr int NT = LstmNT<H, G>::value;
+  for (int bs = 1; bs <= 8; bs *= 2) {
+    if (force_bs > 0 && bs != force_bs) continue;
+    long nblk = (long)a.nprob * ((a.B + bs - 1) / bs) * G;
+    bool ok;
+    switch (bs) {
+      case 1: ok = fits(lstm_bwd_kernel<H, G, 1>, NT, nblk, cus); if (ok) lstm_bwd_kernel<H, G, 1><<<nblk, NT, 0, s>>>(a); break;
+      case 2: ok = fits(lstm_bwd_kernel<H, G, 2>, NT, nblk, cus); if (ok) lstm_bwd_kernel<H, G, 2><<<nblk, NT, 0, s>>>(a); break;
+      case 4: ok = fits(lstm_bwd_kernel<H, G, 4>, NT, nblk, cus); if (ok) lstm_bwd_kernel<H, G, 4><<<nblk, NT, 0, s>>>(a); break;
+      default: ok = fits(lstm_bwd_kernel<H, G, 8>, NT, nblk, cus); if (ok) lstm_bwd_kernel<H, G, 8><<<nblk, NT, 0, s>>>(a); break;
+    }
+    if (ok) return check_launch("lstm_bwd_kernel");
+  }
+  set_error("lstm bwd: persistent grid does not fit the GPU (nprob=%d B=%d H=%d force_bs=%d)", a.nprob, a.B, H,
+            force_bs);
+  return 4;
 }
 
 // members per group for a hidden size (U = 32 at H=256, U = 16 below)
+static int g_group256 = 16;  // members per group at H = 256 (8 or 16), mrg_lstm_config
+
 static int group_size(int H) {
   switch (H) {
-    case 256: return 8;
+    case 256: return g_group256;
     case 128: return 8;
     case 64: return 4;
     case 32: return 2;
@@ -410,27 +570,35 @@ static int group_size(int H) {
   }
 }
 
-// batch rows per group: keep the persistent grid <= 2 workgroups per CU
-static int pick_bs(int nprob, int B, int G, int cus) {
-  for (int bs = 1; bs <= 8; bs *= 2) {
-    long groups = (long)nprob * ((B + bs - 1) / bs);
-    if (groups * G <= 2L * cus) return bs;
-  }
-  return 8;
-}
-
 }  // namespace mrg
 
 using namespace mrg;
 
+static unsigned long long* g_stamps = nullptr;
+
+// Diagnostics: next LSTM launches record per-step phase clocks of block 0 into buf ([T][8] u64);
+// pass null to disable.  Not for timed runs.
+MRG_API int mrg_lstm_debug_stamps(void* buf) {
+  g_stamps = (unsigned long long*)buf;
+  return 0;
+}
+
 // Exchange-ring bytes (zeroed by the caller before every launch).
 MRG_API size_t mrg_lstm_fwd_xbuf_bytes(int B, int H) { return (size_t)2 * B * H * 8; }
 MRG_API size_t mrg_lstm_bwd_xbuf_bytes(int B, int H) {
-  int G = group_size(H);
+  // sized for the largest group the runtime may select, so mrg_lstm_config can change it
+  int G = H == 256 ? 16 : group_size(H);
   return (size_t)2 * B * (G > 0 ? G : 1) * H * 8;
 }
 
 MRG_API int mrg_lstm_supported_hidden(int H) { return group_size(H) > 0; }
+
+// Tuning: workgroups per recurrence group at H = 256 (8 or 16).  Affects the bwd xbuf size.
+MRG_API int mrg_lstm_config(int group256) {
+  MRG_REQUIRE(group256 == 8 || group256 == 16, "mrg_lstm_config: group must be 8 or 16");
+  g_group256 = group256;
+  return 0;
+}
 
 // nprob independent same-shape recurrences in one persistent launch.
 // Arrays are indexed by problem; strides in elements.  See lstm.hip header.
@@ -448,7 +616,7 @@ MRG_API int mrg_lstm_fwd(int nprob, int B, int T, int H,
   if (B == 0 || T == 0) return 0;
   LstmFwdArgs a;
   memset(&a, 0, sizeof(a));
-  a.nprob = nprob; a.B = B; a.T = T; a.err = err;
+  a.nprob = nprob; a.B = B; a.T = T; a.err = err; a.stamps = g_stamps;
   for (int i = 0; i < nprob; ++i) {
     LstmFwdProblem& p = a.p[i];
     p.gx = gx[i]; p.gx_bs = gx_bs[i]; p.gx_ts = gx_ts[i];
@@ -458,14 +626,13 @@ MRG_API int mrg_lstm_fwd(int nprob, int B, int T, int H,
     p.xbuf = (unsigned long long*)xbuf[i]; p.reverse = reverse ? reverse[i] : 0;
     MRG_REQUIRE(((uintptr_t)p.w_hh & 15) == 0, "mrg_lstm_fwd: w_hh must be 16-byte aligned");
   }
-  int BS = force_bs > 0 ? force_bs : pick_bs(nprob, B, G, cus > 0 ? cus : 256);
-  int nblk = nprob * ((B + BS - 1) / BS) * G;
+  if (cus <= 0) cus = 256;
   switch (H) {
-    case 256: return launch_fwd<256, 8>(a, BS, nblk, stream);
-    case 128: return launch_fwd<128, 8>(a, BS, nblk, stream);
-    case 64: return launch_fwd<64, 4>(a, BS, nblk, stream);
-    case 32: return launch_fwd<32, 2>(a, BS, nblk, stream);
-    case 16: return launch_fwd<16, 1>(a, BS, nblk, stream);
+    case 256: return G == 8 ? launch_fwd<256, 8>(a, force_bs, cus, stream) : launch_fwd<256, 16>(a, force_bs, cus, stream);
+    case 128: return launch_fwd<128, 8>(a, force_bs, cus, stream);
+    case 64: return launch_fwd<64, 4>(a, force_bs, cus, stream);
+    case 32: return launch_fwd<32, 2>(a, force_bs, cus, stream);
+    case 16: return launch_fwd<16, 1>(a, force_bs, cus, stream);
   }
   return 2;
 }
@@ -482,7 +649,7 @@ MRG_API int mrg_lstm_bwd(int nprob, int B, int T, int H,
   if (B == 0 || T == 0) return 0;
   LstmBwdArgs a;
   memset(&a, 0, sizeof(a));
-  a.nprob = nprob; a.B = B; a.T = T; a.err = err;
+  a.nprob = nprob; a.B = B; a.T = T; a.err = err; a.stamps = g_stamps;
   for (int i = 0; i < nprob; ++i) {
     LstmBwdProblem& p = a.p[i];
     p.w_hh = w_hh[i]; p.gates = gates[i]; p.cs = cs[i]; p.c0 = c0 ? c0[i] : nullptr;
@@ -491,14 +658,13 @@ MRG_API int mrg_lstm_bwd(int nprob, int B, int T, int H,
     p.dh0 = dh0 ? dh0[i] : nullptr; p.dc0 = dc0 ? dc0[i] : nullptr;
     p.xbuf = (unsigned long long*)xbuf[i]; p.reverse = reverse ? reverse[i] : 0;
   }
-  int BS = force_bs > 0 ? force_bs : pick_bs(nprob, B, G, cus > 0 ? cus : 256);
-  int nblk = nprob * ((B + BS - 1) / BS) * G;
+  if (cus <= 0) cus = 256;
   switch (H) {
-    case 256: return launch_bwd<256, 8>(a, BS, nblk, stream);
-    case 128: return launch_bwd<128, 8>(a, BS, nblk, stream);
-    case 64: return launch_bwd<64, 4>(a, BS, nblk, stream);
-    case 32: return launch_bwd<32, 2>(a, BS, nblk, stream);
-    case 16: return launch_bwd<16, 1>(a, BS, nblk, stream);
+    case 256: return G == 8 ? launch_bwd<256, 8>(a, force_bs, cus, stream) : launch_bwd<256, 16>(a, force_bs, cus, stream);
+    case 128: return launch_bwd<128, 8>(a, force_bs, cus, stream);
+    case 64: return launch_bwd<64, 4>(a, force_bs, cus, stream);
+    case 32: return launch_bwd<32, 2>(a, force_bs, cus, stream);
+    case 16: return launch_bwd<16, 1>(a, force_bs, cus, stream);
   }
   return 2;
 }

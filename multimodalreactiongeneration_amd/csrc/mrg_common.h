@@ -43,10 +43,14 @@ inline int check_launch(const char* what) {
     }                                                                        \
   } while (0)
 
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
-
-// Exact-ish tanh: __expf based, matches libm tanhf to ~1 ulp-scale for |x| < 9.
-__device__ __forceinline__ float tanhf_(float x) { return tanhf(x); }
+// Gate nonlinearities on the native v_exp_f32 / v_rcp_f32 (1-ulp class; absolute error ~1e-7,
+// far inside the 1e-4 parity budget).  exp overflow saturates correctly: rcp(inf) = 0.
+__device__ __forceinline__ float sigmoidf_(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+}
+__device__ __forceinline__ float tanhf_(float x) {
+  return fmaf(2.0f, __builtin_amdgcn_rcpf(1.0f + __expf(-2.0f * x)), -1.0f);
+}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -9,12 +9,11 @@ namespace mrg {
 
 // ------------------------------------------------------------- residual + LayerNorm
 // y = LN(a + b) * gamma + beta (ResidualConnection, residual_connection.py:20-37)
-template <int EPL>  // elements per lane: E = 64 * EPL
+template <int EPL>  // elements per lane: E <= 64 * EPL (lanes past E idle)
 __global__ __launch_bounds__(256) void resln_fwd_kernel(const float* __restrict__ a, const float* __restrict__ b,
                                                         const float* __restrict__ gamma, const float* __restrict__ beta,
                                                         float* __restrict__ y, float* __restrict__ mean_out,
-                                                        float* __restrict__ rstd_out, int rows, float eps) {
-  constexpr int E = 64 * EPL;
+                                                        float* __restrict__ rstd_out, int rows, float eps, int E) {
   int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   int lane = threadIdx.x & 63;
   if (row >= rows) return;
@@ -25,23 +24,24 @@ __global__ __launch_bounds__(256) void resln_fwd_kernel(const float* __restrict_
 #pragma unroll
   for (int i = 0; i < EPL; ++i) {
     int c = i * 64 + lane;
-    x[i] = pa[c] + pb[c];
+    x[i] = c < E ? pa[c] + pb[c] : 0.0f;
     s += x[i];
   }
-  float mean = wave_sum(s) * (1.0f / E);
+  const float invE = 1.0f / (float)E;
+  float mean = wave_sum(s) * invE;
   float v = 0.0f;
 #pragma unroll
   for (int i = 0; i < EPL; ++i) {
-    float d = x[i] - mean;
+    float d = (i * 64 + lane) < E ? x[i] - mean : 0.0f;
     v += d * d;
   }
-  float var = wave_sum(v) * (1.0f / E);
+  float var = wave_sum(v) * invE;
   float rstd = rsqrtf(var + eps);
   float* py = y + (long)row * E;
 #pragma unroll
   for (int i = 0; i < EPL; ++i) {
     int c = i * 64 + lane;
-    py[c] = (x[i] - mean) * rstd * gamma[c] + beta[c];
+    if (c < E) py[c] = (x[i] - mean) * rstd * gamma[c] + beta[c];
   }
   if (lane == 0) {
     mean_out[row] = mean;
@@ -56,9 +56,9 @@ __global__ __launch_bounds__(256) void resln_bwd_kernel(const float* __restrict_
                                                         const float* __restrict__ b, const float* __restrict__ gamma,
                                                         const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
                                                         float* __restrict__ dx, float* __restrict__ part,
-                                                        int rows, int rows_per_block) {
-  constexpr int E = 64 * EPL;
-  __shared__ float red[4][2][E];
+                                                        int rows, int rows_per_block, int E) {
+  constexpr int EMAX = 64 * EPL;
+  __shared__ float red[4][2][EMAX];
   int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float dg[EPL], db[EPL];
 #pragma unroll
@@ -75,25 +75,28 @@ __global__ __launch_bounds__(256) void resln_bwd_kernel(const float* __restrict_
 #pragma unroll
     for (int i = 0; i < EPL; ++i) {
       int c = i * 64 + lane;
-      float d = pdy[c];
-      xh[i] = (pa[c] + pb[c] - mean) * rstd;
-      g[i] = d * gamma[c];
+      bool ok = c < E;
+      float d = ok ? pdy[c] : 0.0f;
+      xh[i] = ok ? (pa[c] + pb[c] - mean) * rstd : 0.0f;
+      g[i] = ok ? d * gamma[c] : 0.0f;
       s1 += g[i];
       s2 += g[i] * xh[i];
       dg[i] += d * xh[i];
       db[i] += d;
     }
-    float m1 = wave_sum(s1) * (1.0f / E);
-    float m2 = wave_sum(s2) * (1.0f / E);
+    const float invE = 1.0f / (float)E;
+    float m1 = wave_sum(s1) * invE;
+    float m2 = wave_sum(s2) * invE;
     float* pdx = dx + (long)row * E;
 #pragma unroll
-    for (int i = 0; i < EPL; ++i) pdx[i * 64 + lane] = rstd * (g[i] - m1 - xh[i] * m2);
+    for (int i = 0; i < EPL; ++i)
+      if (i * 64 + lane < E) pdx[i * 64 + lane] = rstd * (g[i] - m1 - xh[i] * m2);
   }
 #pragma unroll
   for (int i = 0; i < EPL; ++i) {
     red[wave][0][i * 64 + lane] = dg[i];
     red[wave][1][i * 64 + lane] = db[i];
-  }
+  }  // lanes past E hold zeros; only c < E is read below
   __syncthreads();
   for (int c = threadIdx.x; c < 2 * E; c += 256) {
     int k = c / E, e = c % E;
@@ -102,15 +105,27 @@ __global__ __launch_bounds__(256) void resln_bwd_kernel(const float* __restrict_
   }
 }
 
-__global__ void resln_param_reduce_kernel(const float* part, int nblk, int E, float* dgamma,
-                                          float* dbeta, int accumulate) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= 2 * E) return;
-  int k = c / E, e = c % E;
+// dgamma / dbeta: sum the per-block partials part[nblk][2][E]; one lane per column,
+// 16 waves interleave over the blocks, then combine in LDS (fixed order -> deterministic)
+__global__ __launch_bounds__(1024) void resln_param_reduce_kernel(const float* part, int nblk, int E, float* dgamma,
+                                                                  float* dbeta, int accumulate) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
   float s = 0.0f;
-  for (int i = 0; i < nblk; ++i) s += part[((long)i * 2 + k) * E + e];
-  float* out = k == 0 ? dgamma : dbeta;
-  out[e] = accumulate ? out[e] + s : s;
+  if (c < 2 * E) {
+#pragma unroll 4
+    for (int i = wave; i < nblk; i += 16) s += part[(long)i * 2 * E + c];
+  }
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && c < 2 * E) {
+    float v = 0.0f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) v += red[w][lane];
+    float* out = c < E ? dgamma + c : dbeta + (c - E);
+    *out = accumulate ? *out + v : v;
+  }
 }
 
 // ------------------------------------------------------------------ loss
@@ -232,18 +247,20 @@ MRG_API int mrg_residual_layernorm_fwd(int rows, int E, const float* a, const fl
                                        float* mean, float* rstd, hipStream_t stream) {
   if (rows == 0) return 0;
   dim3 grid((rows + 3) / 4);
-  switch (E) {
-    case 64: resln_fwd_kernel<1><<<grid, 256, 0, stream>>>(a, b, gamma, beta, y, mean, rstd, rows, eps); break;
-    case 128: resln_fwd_kernel<2><<<grid, 256, 0, stream>>>(a, b, gamma, beta, y, mean, rstd, rows, eps); break;
-    case 256: resln_fwd_kernel<4><<<grid, 256, 0, stream>>>(a, b, gamma, beta, y, mean, rstd, rows, eps); break;
-    case 512: resln_fwd_kernel<8><<<grid, 256, 0, stream>>>(a, b, gamma, beta, y, mean, rstd, rows, eps); break;
-    default: set_error("mrg_residual_layernorm_fwd: unsupported E=%d", E); return 2;
-  }
+  MRG_REQUIRE(E >= 1 && E <= 1024, "mrg_residual_layernorm_fwd: unsupported E=%d", E);
+  const int epl = (E + 63) / 64;
+  if (epl <= 1) resln_fwd_kernel<1><<<grid, 256, 0, stream>>>(a, b, gamma, beta, y, mean, rstd, rows, eps, E);
+  else if (epl <= 2) resln_fwd_kernel<2><<<grid, 256, 0, stream>>>(a, b, gamma, beta, y, mean, rstd, rows, eps, E);
+  else if (epl <= 4) resln_fwd_kernel<4><<<grid, 256, 0, stream>>>(a, b, gamma, beta, y, mean, rstd, rows, eps, E);
+  else if (epl <= 8) resln_fwd_kernel<8><<<grid, 256, 0, stream>>>(a, b, gamma, beta, y, mean, rstd, rows, eps, E);
+  else resln_fwd_kernel<16><<<grid, 256, 0, stream>>>(a, b, gamma, beta, y, mean, rstd, rows, eps, E);
   return check_launch("resln_fwd_kernel");
 }
 
+static constexpr int RESLN_RPB = 32;  // rows per backward block (600 blocks at B*T = 19200)
+
 MRG_API size_t mrg_residual_layernorm_bwd_workspace_bytes(int rows, int E) {
-  int nblk = (rows + 127) / 128;
+  int nblk = (rows + RESLN_RPB - 1) / RESLN_RPB;
   return (size_t)nblk * 2 * E * sizeof(float);
 }
 
@@ -252,18 +269,18 @@ MRG_API int mrg_residual_layernorm_bwd(int rows, int E, const float* dy, const f
                                        const float* rstd, float* dx, float* dgamma, float* dbeta,
                                        int accumulate, float* workspace, hipStream_t stream) {
   if (rows == 0) return 0;
-  const int rpb = 128;
+  const int rpb = RESLN_RPB;
   int nblk = (rows + rpb - 1) / rpb;
-  switch (E) {
-    case 64: resln_bwd_kernel<1><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, rpb); break;
-    case 128: resln_bwd_kernel<2><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, rpb); break;
-    case 256: resln_bwd_kernel<4><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, rpb); break;
-    case 512: resln_bwd_kernel<8><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, rpb); break;
-    default: set_error("mrg_residual_layernorm_bwd: unsupported E=%d", E); return 2;
-  }
+  MRG_REQUIRE(E >= 1 && E <= 1024, "mrg_residual_layernorm_bwd: unsupported E=%d", E);
+  const int epl = (E + 63) / 64;
+  if (epl <= 1) resln_bwd_kernel<1><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, rpb, E);
+  else if (epl <= 2) resln_bwd_kernel<2><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, rpb, E);
+  else if (epl <= 4) resln_bwd_kernel<4><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, rpb, E);
+  else if (epl <= 8) resln_bwd_kernel<8><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, rpb, E);
+  else resln_bwd_kernel<16><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, rpb, E);
   if (check_launch("resln_bwd_kernel")) return 1;
-  resln_param_reduce_kernel<<<(2 * E + 255) / 256, 256, 0, stream>>>(workspace, nblk, E, dgamma, dbeta,
-                                                                     accumulate);
+  resln_param_reduce_kernel<<<(2 * E + 63) / 64, 1024, 0, stream>>>(workspace, nblk, E, dgamma, dbeta,
+                                                                   accumulate);
   return check_launch("resln_param_reduce_kernel");
 }
 

@@ -215,8 +215,10 @@ class MultiModalMetaformer(nn.Module):
             for i in active:
                 groups.setdefault((tuple(xs[i].shape), chains[i][layer].lstm_params()[1].shape[1]), []).append(i)
             for idxs in groups.values():
-                for start in range(0, len(idxs), 4):
-                    part = idxs[start:start + 4]
+                # at most two recurrences per launch: two batch-tile-2 problems fill the chip's
+                # 512 resident workgroups; three would need batch tiles of 4 (longer GEMV per step)
+                for start in range(0, len(idxs), 2):
+                    part = idxs[start:start + 2]
                     ys = Fn.lstm_layers_batched([(xs[i], *chains[i][layer].lstm_params()) for i in part])
                     for i, y in zip(part, ys):
                         xs[i] = _lstm_block_tail(chains[i][layer], y, xs[i])

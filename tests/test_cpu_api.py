@@ -36,7 +36,7 @@ def test_workspace_size_helpers():
     assert lib.mrg_gemm_workspace_bytes(256, 256, 8) == 8 * 256 * 256 * 4
     assert lib.mrg_gemm_workspace_bytes(256, 256, 1) == 0
     assert lib.mrg_lstm_fwd_xbuf_bytes(64, 256) == 2 * 64 * 256 * 8
-    assert lib.mrg_lstm_bwd_xbuf_bytes(64, 256) == 2 * 64 * 8 * 256 * 8
+    assert lib.mrg_lstm_bwd_xbuf_bytes(64, 256) == 2 * 64 * 16 * 256 * 8
     assert lib.mrg_attention_bwd_workspace_bytes(2, 4, 300) == 2 * 4 * 300 * 4
 
 
