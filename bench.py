@@ -40,6 +40,7 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--probe", default="lstm_fwd", help="kernel family for the live roofline")
+    ap.add_argument("--lstm-group", type=int, default=0, help="workgroups per LSTM row group at H=256 (8|16; 0 = library default)")
     return ap.parse_args()
 
 
@@ -97,6 +98,9 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     mc, oc, me = C.lstmformer_config(ratio=args.ratio)
+    if args.lstm_group:
+        from multimodalreactiongeneration_amd import _lib
+        _lib.check(_lib.load().mrg_lstm_config(args.lstm_group), "mrg_lstm_config")
     torch.manual_seed(0)
     model = Metaformer(mc, oc, me).to(dev)
     broadcast_parameters(model)

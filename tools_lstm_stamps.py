@@ -55,5 +55,8 @@ def run(nprob, force_bs=0):
 
 
 if __name__ == "__main__":
-    for nprob, bs in [(1, 0), (2, 0), (3, 0), (1, 2), (1, 4)]:
-        run(nprob, bs)
+    for grp in (16, 8):
+        _lib.check(lib.mrg_lstm_config(grp), "config")
+        print(f"== group256 = {grp}")
+        for nprob, bs in [(1, 0), (2, 0), (3, 0), (1, 1), (1, 2)]:
+            run(nprob, bs)
