@@ -84,7 +84,7 @@ int mrg_lstm_bwd(int nprob, int B, int T, int H,
                  void* const* xbuf, int* err, int cus, int force_bs, hipStream_t stream);
 
 /* Tuning knob: number of workgroups that share one batch row group at H = 256
- * (8 or 16; default 16).  Process-wide; set before capture, not during. */
+ * (8 or 16; default 8).  Process-wide; set before capture, not during. */
 int mrg_lstm_config(int group256);
 
 /* Diagnostics only: record per-step phase clocks (s_memtime) of block 0 of the next

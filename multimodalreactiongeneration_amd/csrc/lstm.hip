@@ -149,6 +149,33 @@ __device__ __forceinline__ void get_granules(unsigned long long* base, long stri
   for (int i = 0; i < N; ++i) out[i] = __uint_as_float((unsigned)v[i]);
 }
 
+// As get_granules, for N granules at arbitrary offsets from base.
+template <int N>
+__device__ __forceinline__ void get_granules_idx(unsigned long long* base, const int (&idx)[N], unsigned tag,
+                                                 float (&out)[N], int* err, bool& dead) {
+  unsigned long long v[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = __hip_atomic_load(base + idx[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned spins = 0;
+  while (!dead) {
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < N; ++i) ok &= (unsigned)(v[i] >> 32) == tag;
+    if (ok) break;
+    if (++spins > SPIN_LIMIT) {
+      atomicOr(err, 1);
+      dead = true;
+      break;
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      if ((unsigned)(v[i] >> 32) != tag)
+        v[i] = __hip_atomic_load(base + idx[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) out[i] = __uint_as_float((unsigned)v[i]);
+}
+
 // block -> (problem, group, member); members of a group share blockIdx % 8 (one XCD)
 __device__ __forceinline__ void decompose(int G, int ngroups_per_prob, int nprob, int& prob, int& grp,
                                           int& member) {
@@ -194,6 +221,11 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
   static_assert(RT >= 1 && RT * NT == R * KC && (KL % 4) == 0 && BS * U <= NT, "bad LSTM tiling");
   __shared__ __attribute__((aligned(16))) float hs[BS][KC][KLP];
   __shared__ float pre[BS][R];
+  // cell threads occupy the first CW waves; the rest gather (all threads if the cells fill the block)
+  constexpr int CW = (BS * U + 63) / 64;
+  constexpr int GOFF = (CW * 64 < NT) ? CW * 64 : 0;
+  constexpr int GT = NT - GOFF;
+  constexpr int NG = (BS * H + GT - 1) / GT;
 
   int prob, grp, j;
   const int ngroups = (args.B + BS - 1) / BS;
@@ -301,28 +333,21 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
       if (tt + 1 < T) load_gx(P.reverse ? t - 1 : t + 1);
     }
     MRG_STAMP(4);
-    // 4. gather h_t of the whole group
-    if (tt + 1 < T) {
-      constexpr int NG = (BS * H + NT - 1) / NT;  // granules per thread, NT apart
-      float gv[NG];
-      // the group's rows are contiguous in the ring: granule e of the group sits at row_base + e.
-      // A ragged last group (b0 + b >= B) re-reads its last valid row (published, value unused).
+    // 4. gather h_t of the whole group.  Done by the waves after the cell waves: on gfx9 one vmcnt
+    // covers loads and stores, so a wave that just issued the y/gates/cs stores and the gx prefetch
+    // would wait for all of them before its first poll returned.
+    if (tt + 1 < T && tid >= GOFF) {
+      const int gt = tid - GOFF;
       const int nvalid = min(BS, B - b0) * H;
       unsigned long long* rb = xb + ((long)par * B + b0) * H;
-      if ((BS * H) % NT == 0 && nvalid == BS * H) {
-        get_granules<NG>(rb + tid, NT, (unsigned)(tt + 1), gv, args.err, dead);
-      } else {
+      float gv[NG];
+      int idx[NG];
 #pragma unroll
-        for (int i = 0; i < NG; ++i) {
-          float one[1];
-          int e = min(tid + i * NT, nvalid - 1);
-          get_granules<1>(rb + e, 0, (unsigned)(tt + 1), one, args.err, dead);
-          gv[i] = one[0];
-        }
-      }
+      for (int i = 0; i < NG; ++i) idx[i] = min(gt + i * GT, nvalid - 1);
+      get_granules_idx<NG>(rb, idx, (unsigned)(tt + 1), gv, args.err, dead);
 #pragma unroll
       for (int i = 0; i < NG; ++i) {
-        int e = tid + i * NT;
+        int e = gt + i * GT;
         if (e < BS * H) {
           int b = e / H, k = e % H;
           hs[b][k / KL][k % KL] = (b0 + b < B) ? gv[i] : 0.0f;
@@ -353,6 +378,10 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
   static_assert(OT >= 1 && OT * NT == RC * H && RL * RC == R && (RL % 4) == 0 && BS * U <= NT &&
                 (U % OT) == 0, "bad LSTM bwd tiling");
   __shared__ __attribute__((aligned(16))) float dgl[BS][RC][RLP];
+  __shared__ float sv[2][7][BS * U];  // saved i, f, g, o, c_t, c_{t-1}, dy of the cells, by step parity
+  constexpr int CW = (BS * U + 63) / 64;
+  constexpr int IOFF = CW * 64;  // first io thread
+  static_assert(IOFF + BS * U <= NT, "LSTM bwd: no room for the io waves");
 
   int prob, grp, j;
   const int ngroups = (args.B + BS - 1) / BS;
@@ -386,21 +415,38 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
     if (P.dhT) dhrec = P.dhT[(long)bg * H + hcol];
   }
 
+  // io role: a shadow thread per cell, in waves the cells do not use, moves the saved activations
+  // HBM -> LDS two steps ahead and dG LDS -> HBM, so the cell waves' vmcnt only ever covers
+  // hand-off traffic (gfx9 has one vmcnt for loads and stores).
+  const int iot = tid - IOFF;
+  const bool io = iot >= 0 && iot < BS * U;
+  const int ib = io ? iot / U : 0, iu = iot % U;
+  const int ibg = b0 + ib;
+  const bool iovalid = io && ibg < B;
+  const int iocol = j * U + iu;
+  float pf[7];
+  auto io_load = [&](int tt2) {  // saved values of processing step tt2 -> pf
+    if (!iovalid || tt2 >= T) return;
+    const int t = P.reverse ? tt2 : T - 1 - tt2;
+    const int tp = P.reverse ? t + 1 : t - 1;
+    const float* gs = P.gates + ((long)ibg * T + t) * 4 * H + iocol;
+    pf[0] = gs[0]; pf[1] = gs[H]; pf[2] = gs[2 * H]; pf[3] = gs[3 * H];
+    pf[4] = P.cs[((long)ibg * T + t) * H + iocol];
+    pf[5] = (tp >= 0 && tp < T) ? P.cs[((long)ibg * T + tp) * H + iocol] : (P.c0 ? P.c0[(long)ibg * H + iocol] : 0.0f);
+    pf[6] = P.dy ? P.dy[(long)ibg * P.dy_bs + (long)t * P.dy_ts + iocol] : 0.0f;
+  };
+  auto io_stage = [&](int tt2) {  // pf -> sv slot of step tt2
+    if (!iovalid || tt2 >= T) return;
+#pragma unroll
+    for (int q = 0; q < 7; ++q) sv[tt2 & 1][q][iot] = pf[q];
+  };
+  io_load(0);
+  io_stage(0);
+  io_load(1);
+  __syncthreads();
+
   unsigned long long* xb = P.xbuf;
   const long xstride_b = (long)G * H;  // per batch row: [dest G][src G][U]
-  // saved activations of the next step to process, prefetched one step ahead so
-  // their HBM latency hides under the hand-off wait
-  float ig = 0.f, fg = 0.f, gg = 0.f, og = 0.f, cc = 0.f, cp = 0.f, dyv = 0.f;
-  auto prefetch = [&](int t) {
-    if (!cvalid) return;
-    const int tp = P.reverse ? t + 1 : t - 1;
-    const float* gs = P.gates + ((long)bg * T + t) * 4 * H + hcol;
-    ig = gs[0]; fg = gs[H]; gg = gs[2 * H]; og = gs[3 * H];
-    cc = P.cs[((long)bg * T + t) * H + hcol];
-    cp = (tp >= 0 && tp < T) ? P.cs[((long)bg * T + tp) * H + hcol] : (P.c0 ? P.c0[(long)bg * H + hcol] : 0.0f);
-    dyv = P.dy ? P.dy[(long)bg * P.dy_bs + (long)t * P.dy_ts + hcol] : 0.0f;
-  };
-  prefetch(P.reverse ? 0 : T - 1);
   for (int tt = 0; tt < T; ++tt) {
     const int t = P.reverse ? tt : T - 1 - tt;
     MRG_STAMP(0);
@@ -416,6 +462,9 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
         dhrec = s;
       }
       MRG_STAMP(1);
+      const int sl = tt & 1;
+      const float ig = sv[sl][0][tid], fg = sv[sl][1][tid], gg = sv[sl][2][tid], og = sv[sl][3][tid];
+      const float cc = sv[sl][4][tid], cp = sv[sl][5][tid], dyv = sv[sl][6][tid];
       const float dh = dhrec + dyv;
       const float tc = tanhf_(cc);
       const float dc = dh * og * (1.0f - tc * tc) + dcn;
@@ -424,8 +473,6 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
       const float d_f = dc * cp * fg * (1.0f - fg);
       const float d_g = dc * ig * (1.0f - gg * gg);
       dcn = dc * fg;
-      float* dgp = P.dG + ((long)bg * T + t) * 4 * H + hcol;
-      dgp[0] = d_i; dgp[H] = d_f; dgp[2 * H] = d_g; dgp[3 * H] = d_o;
       {
         const int r0 = 0 * U + cu, r1 = 1 * U + cu, r2 = 2 * U + cu, r3 = 3 * U + cu;
         dgl[cb][r0 / RL][r0 % RL] = d_i;
@@ -433,7 +480,6 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
         dgl[cb][r2 / RL][r2 % RL] = d_g;
         dgl[cb][r3 / RL][r3 % RL] = d_o;
       }
-      if (tt + 1 < T) prefetch(P.reverse ? t + 1 : t - 1);
       MRG_STAMP(2);
     } else if (cell) {
 #pragma unroll
@@ -447,43 +493,45 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
     // partial dh_{t-1}[b][hout] = sum over this member's rows of dG[b][row] * W_hh[row][hout]
     {
       const int par = tt & 1;
-      float acc[OT][BS];
 #pragma unroll
-      for (int o = 0; o < OT; ++o)
+      for (int b = 0; b < BS; ++b) {  // one batch row at a time: short live ranges
+        float acc[OT];
 #pragma unroll
-        for (int b = 0; b < BS; ++b) acc[o][b] = 0.0f;
-#pragma unroll
-      for (int b = 0; b < BS; ++b) {
+        for (int o = 0; o < OT; ++o) acc[o] = 0.0f;
         const float* dp = &dgl[b][rc][0];
 #pragma unroll
         for (int i = 0; i < RL; i += 4) {
           float4 dv = *reinterpret_cast<const float4*>(dp + i);
 #pragma unroll
           for (int o = 0; o < OT; ++o) {
-            acc[o][b] = fmaf(dv.x, w[o][i], acc[o][b]);
-            acc[o][b] = fmaf(dv.y, w[o][i + 1], acc[o][b]);
-            acc[o][b] = fmaf(dv.z, w[o][i + 2], acc[o][b]);
-            acc[o][b] = fmaf(dv.w, w[o][i + 3], acc[o][b]);
+            acc[o] = fmaf(dv.x, w[o][i], acc[o]);
+            acc[o] = fmaf(dv.y, w[o][i + 1], acc[o]);
+            acc[o] = fmaf(dv.z, w[o][i + 2], acc[o]);
+            acc[o] = fmaf(dv.w, w[o][i + 3], acc[o]);
           }
         }
-      }
-      MRG_STAMP(4);
+        if (b == 0) MRG_STAMP(4);
 #pragma unroll
-      for (int o = 0; o < OT; ++o)
+        for (int o = 0; o < OT; ++o) acc[o] = group_sum<RC>(acc[o]);
+        if (rc == 0 && b0 + b < B) {
+          const int h0 = ogr * OT;
+          const int dest = h0 / U, du = h0 % U;
+          unsigned long long* gq = xb + ((long)par * B + b0 + b) * xstride_b + (long)dest * H + (long)j * U + du;
 #pragma unroll
-        for (int b = 0; b < BS; ++b) acc[o][b] = group_sum<RC>(acc[o][b]);
-      if (rc == 0) {
-        const int h0 = ogr * OT;
-        const int dest = h0 / U, du = h0 % U;
-#pragma unroll
-        for (int b = 0; b < BS; ++b) {
-          if (b0 + b < B) {
-            unsigned long long* gq = xb + ((long)par * B + b0 + b) * xstride_b + (long)dest * H + (long)j * U + du;
-#pragma unroll
-            for (int o = 0; o < OT; ++o) put_granule(gq + o, (unsigned)(tt + 1), acc[o][b]);
-          }
+          for (int o = 0; o < OT; ++o) put_granule(gq + o, (unsigned)(tt + 1), acc[o]);
         }
       }
+    }
+    if (iovalid) {
+      // dG of this step (still in dgl until the barrier), then stage step tt+1, prefetch tt+2
+      float* dgp = P.dG + ((long)ibg * T + t) * 4 * H + iocol;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int rr = q * U + iu;
+        dgp[q * H] = dgl[ib][rr / RL][rr % RL];
+      }
+      io_stage(tt + 1);
+      io_load(tt + 2);
     }
     MRG_STAMP(5);
     __syncthreads();
@@ -557,7 +605,7 @@ static int launch_bwd(const LstmBwdArgs& a, int force_bs, int cus, hipStream_t s
 }
 
 // members per group for a hidden size (U = 32 at H=256, U = 16 below)
-static int g_group256 = 16;  // members per group at H = 256 (8 or 16), mrg_lstm_config
+static int g_group256 = 8;  // members per group at H = 256 (8 or 16), mrg_lstm_config
 
 static int group_size(int H) {
   switch (H) {

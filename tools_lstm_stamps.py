@@ -3,6 +3,7 @@
     python tools_lstm_stamps.py            (on a GPU box)
 """
 import ctypes
+import os
 import sys
 import time
 
@@ -55,7 +56,7 @@ def run(nprob, force_bs=0):
 
 
 if __name__ == "__main__":
-    for grp in (16, 8):
+    for grp in [int(g) for g in os.environ.get("GROUPS", "8").split(",")]:
         _lib.check(lib.mrg_lstm_config(grp), "config")
         print(f"== group256 = {grp}")
         for nprob, bs in [(1, 0), (2, 0), (3, 0), (1, 1), (1, 2)]:
