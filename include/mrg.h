@@ -63,7 +63,8 @@ int mrg_colsum_f32(int rows, int N, const float* X, long ld, long ld_hi, int rdi
  * (e.g. the audio and partner encoders of block 0).  Arrays are indexed by
  * problem.  xbuf[i] must be zeroed before every call
  * (mrg_lstm_fwd_xbuf_bytes / mrg_lstm_bwd_xbuf_bytes); *err is OR-ed with 1
- * if a hand-off spin times out.  H in {16, 32, 64, 128, 256}.            */
+ * if a hand-off spin times out; cus = CU count (<= 0: query the current device).
+ * H in {16, 32, 64, 128, 256}.             */
 int mrg_lstm_supported_hidden(int H);
 size_t mrg_lstm_fwd_xbuf_bytes(int B, int H);
 size_t mrg_lstm_bwd_xbuf_bytes(int B, int H);

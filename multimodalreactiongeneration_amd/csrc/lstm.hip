@@ -605,6 +605,14 @@ static int launch_bwd(const LstmBwdArgs& a, int force_bs, int cus, hipStream_t s
 }
 
 // members per group for a hidden size (U = 32 at H=256, U = 16 below)
+// CU count of the current device (occupancy check of the persistent grids)
+static int device_cus() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  return n;
+}
+
 static int g_group256 = 8;  // members per group at H = 256 (8 or 16), mrg_lstm_config
 
 static int group_size(int H) {
@@ -674,7 +682,7 @@ MRG_API int mrg_lstm_fwd(int nprob, int B, int T, int H,
     p.xbuf = (unsigned long long*)xbuf[i]; p.reverse = reverse ? reverse[i] : 0;
     MRG_REQUIRE(((uintptr_t)p.w_hh & 15) == 0, "mrg_lstm_fwd: w_hh must be 16-byte aligned");
   }
-  if (cus <= 0) cus = 256;
+  if (cus <= 0) cus = device_cus();
   switch (H) {
     case 256: return G == 8 ? launch_fwd<256, 8>(a, force_bs, cus, stream) : launch_fwd<256, 16>(a, force_bs, cus, stream);
     case 128: return launch_fwd<128, 8>(a, force_bs, cus, stream);
@@ -706,7 +714,7 @@ MRG_API int mrg_lstm_bwd(int nprob, int B, int T, int H,
     p.dh0 = dh0 ? dh0[i] : nullptr; p.dc0 = dc0 ? dc0[i] : nullptr;
     p.xbuf = (unsigned long long*)xbuf[i]; p.reverse = reverse ? reverse[i] : 0;
   }
-  if (cus <= 0) cus = 256;
+  if (cus <= 0) cus = device_cus();
   switch (H) {
     case 256: return G == 8 ? launch_bwd<256, 8>(a, force_bs, cus, stream) : launch_bwd<256, 16>(a, force_bs, cus, stream);
     case 128: return launch_bwd<128, 8>(a, force_bs, cus, stream);
