@@ -375,7 +375,7 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
   constexpr int OT = RC * H / NT;
   constexpr int RL = R / RC;
   constexpr int RLP = ((RL / 4) % 2 == 0) ? RL + 4 : RL;
-  static_assert(OT >= 1 && OT * NT == RC * H && RL * RC == R && (RL % 4) == 0 && BS * U <= NT &&
+  static_assert(OT >= 1 && OT <= RC && OT * NT == RC * H && RL * RC == R && (RL % 4) == 0 && BS * U <= NT &&
                 (U % OT) == 0, "bad LSTM bwd tiling");
   __shared__ __attribute__((aligned(16))) float dgl[BS][RC][RLP];
   __shared__ float sv[2][7][BS * U];  // saved i, f, g, o, c_t, c_{t-1}, dy of the cells, by step parity
@@ -513,12 +513,16 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
         if (b == 0) MRG_STAMP(4);
 #pragma unroll
         for (int o = 0; o < OT; ++o) acc[o] = group_sum<RC>(acc[o]);
-        if (rc == 0 && b0 + b < B) {
+        // every lane of the RC group holds the sums: lanes rc < OT each publish granule o = rc, so
+        // a wave's puts are contiguous 8-B granules in ONE store instruction (full 128-B lines)
+        if (rc < OT && b0 + b < B) {
           const int h0 = ogr * OT;
           const int dest = h0 / U, du = h0 % U;
-          unsigned long long* gq = xb + ((long)par * B + b0 + b) * xstride_b + (long)dest * H + (long)j * U + du;
+          float v = acc[0];
 #pragma unroll
-          for (int o = 0; o < OT; ++o) put_granule(gq + o, (unsigned)(tt + 1), acc[o]);
+          for (int o = 1; o < OT; ++o) v = (rc == o) ? acc[o] : v;
+          unsigned long long* gq = xb + ((long)par * B + b0 + b) * xstride_b + (long)dest * H + (long)j * U + du;
+          put_granule(gq + rc, (unsigned)(tt + 1), v);
         }
       }
     }

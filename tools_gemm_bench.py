@@ -1,0 +1,88 @@
+"""Per-shape timing of mrg_gemm_f32 on the GEMM shapes of the lstmformer step (B=64, T=300, H=256).
+
+    python tools_gemm_bench.py            (on a GPU box)
+
+Prints TFLOP/s per shape against the 157.3 TF f32 MFMA peak, plus the step-weighted total.
+"""
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from multimodalreactiongeneration_amd import functional as Fn  # noqa: E402
+
+R = 64 * 300
+# (name, M, N, K, transA, transB, calls per step, wgrad)
+SHAPES = [
+    ("lstm Gx  X W_ih^T", R, 1024, 256, 0, 1, 15, False),
+    ("lstm dX  dG W_ih", R, 256, 1024, 0, 0, 15, False),
+    ("lstm dW  dG^T X", 1024, 256, R, 1, 0, 30, True),
+    ("lin256 fwd", R, 256, 256, 0, 1, 35, False),
+    ("lin256 dX", R, 256, 256, 0, 0, 35, False),
+    ("lin256 dW", 256, 256, R, 1, 0, 35, True),
+    ("kv512 fwd", R, 512, 256, 0, 1, 10, False),
+    ("kv512 dX", R, 256, 512, 0, 0, 10, False),
+    ("kv512 dW", 512, 256, R, 1, 0, 10, True),
+    ("cat512 fwd", R, 256, 512, 0, 1, 5, False),
+    ("ffn 256->64", R, 64, 256, 0, 1, 6, False),
+    ("ffn 64->256", R, 256, 64, 0, 1, 5, False),
+]
+PROBES = [
+    ("square NN 4096^3", 4096, 4096, 4096, 0, 0, 0, False),
+    ("square NT 4096^3", 4096, 4096, 4096, 0, 1, 0, False),
+    ("square TN 4096^3", 4096, 4096, 4096, 1, 0, 0, False),
+    ("4096x4096 K=256 NT", 4096, 4096, 256, 0, 1, 0, False),
+    ("19200x1024 K=1024 NT", R, 1024, 1024, 0, 1, 0, False),
+]
+
+
+def run_shape(M, N, K, ta, tb, wgrad, iters=20):
+    dev = "cuda:0"
+    A = torch.randn((K, M) if ta else (M, K), device=dev)
+    B = torch.randn((N, K) if tb else (K, N), device=dev)
+    C = torch.zeros(M, N, device=dev)
+    lda = A.shape[1]
+    ldb = B.shape[1]
+    splits = Fn.wgrad_splits(M, N, K) if wgrad else 1
+
+    def go():
+        Fn.gemm(M, N, K, Fn._ptr(A), ta, lda, Fn._ptr(B), tb, ldb, Fn._ptr(C), N,
+                beta=1.0 if wgrad else 0.0, splits=splits, device=A.device)
+    for _ in range(3):
+        go()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        go()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    # check one shape's numerics against torch fp32 (different summation order: loose)
+    ref = (A.t() if ta else A) @ (B.t() if tb else B)
+    if not wgrad:
+        err = (C - ref).abs().max().item() / ref.abs().max().item()
+    else:
+        err = float("nan")
+    return ms, splits, err
+
+
+def main():
+    tot_ms = tot_fl = 0.0
+    for name, M, N, K, ta, tb, calls, wgrad in SHAPES:
+        ms, splits, err = run_shape(M, N, K, ta, tb, wgrad)
+        fl = 2.0 * M * N * K
+        tf = fl / (ms / 1e3) / 1e12
+        tot_ms += ms * calls
+        tot_fl += fl * calls
+        print(f"{name:20s} M={M:6d} N={N:5d} K={K:6d} splits={splits:3d}  {ms*1e3:8.1f} us  "
+              f"{tf:6.1f} TF/s ({tf/157.3*100:5.1f}%)  x{calls}/step  err={err:.1e}")
+    print(f"step-weighted: {tot_ms:.2f} ms/step, {tot_fl/(tot_ms/1e3)/1e12:.1f} TF/s")
+    for name, M, N, K, ta, tb, calls, wgrad in PROBES:
+        ms, splits, err = run_shape(M, N, K, ta, tb, wgrad, iters=5)
+        tf = 2.0 * M * N * K / (ms / 1e3) / 1e12
+        print(f"{name:20s} {ms*1e3:8.1f} us  {tf:6.1f} TF/s ({tf/157.3*100:5.1f}%)  err={err:.1e}")
+
+
+if __name__ == "__main__":
+    main()
