@@ -213,8 +213,8 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
   // register blocking of the recurrent GEMV: a thread owns RT gate rows x KL hidden inputs, the
   // KC lanes of a row group split the hidden dimension (DPP-reduced), so every h value read from
   // LDS feeds RT FMAs (the GEMV is LDS-issue bound otherwise)
-  // (fewer rows per thread at large batch tiles keeps acc[RT][BS] + W inside 128 VGPRs)
-  constexpr int KC = (H >= 128) ? ((BS >= 4 ? 2 : 4) * NT / R) : ((H / 4 < 16) ? H / 4 : 16);
+  // (KC = 8 lanes x 2 rows measured fastest at H = 256: 3 DPP levels, 128-B LDS reads per lane)
+  constexpr int KC = (H >= 128) ? (2 * NT / R) : ((H / 4 < 16) ? H / 4 : 16);
   constexpr int RT = R * KC / NT;
   constexpr int KL = H / KC;
   constexpr int KLP = ((KL / 4) % 2 == 0) ? KL + 4 : KL;  // odd 16-B chunk pitch: conflict-free b128
