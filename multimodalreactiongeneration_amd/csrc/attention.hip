@@ -5,20 +5,25 @@
 // multi_modal_att.py:22-31).  The mask of gen_attention_mask
 // (multi_modal_metaformer.py:32-79) is evaluated from indices, never
 // materialised:
-//   causal, Tk = r*Tq : query i sees key j  iff  j / r <= i
+//   causal, Tk = r*Tq : query i sees key j  iff  j / r <= i   (j < (i+1) r)
 //   causal, Tq = r*Tk : query i sees key j  iff  j <= i / r
 //   padding           : masked iff qpad[b][i] && kpad[b][j]   (the AND rule)
 // A fully masked row yields NaN exactly like softmax over all -inf.
 //
 // Layouts: element (b, t, head, d) of q/k/v/o lives at
-//   base + b*bs + t*ts + head*D + d      (the [B, T, E] projections, no copy)
+//   base + b*bs + t*ts + head*D + d      (the [B, T, E] projections, no copy;
+//   rows 16-B aligned, loaded as float4)
 // Forward: one workgroup = 4 waves = 64 queries of one (b, head); each wave
 // keeps 16 queries' Q^T in registers and computes S^T = K Q^T so a query is a
 // lane column: the online-softmax row max/sum is 4 registers + 2 shuffles,
 // and P^T feeds the P.V MFMA straight from the accumulator (k-order permuted
-// identically on both operands, no transpose).  Backward (deterministic, no
-// atomics): one kernel per 64-key block for dK/dV, one per 64-query block for
-// dQ, both recomputing P from the forward's log-sum-exp.
+// identically on both operands, no transpose).  K/V tiles of 64 keys go
+// HBM -> registers (the next tile's loads fly under this tile's MFMAs) -> LDS.
+// The causal limit is one compare per element against a per-lane bound, and
+// the mask is skipped entirely for sub-tiles every query of the wave sees.
+// Backward (deterministic, no atomics): a dQ kernel per 64-query block (which
+// also forms delta = rowsum(dO * O) for its rows) and then a dK/dV kernel per
+// 64-key block, both recomputing P from the forward's log-sum-exp.
 #include "mrg_common.h"
 
 namespace mrg {
@@ -43,71 +48,99 @@ struct AttnArgs {
   float scale;
 };
 
-__device__ __forceinline__ bool visible(const AttnArgs& a, int b, int i, int j) {
-  if (i >= a.Tq || j >= a.Tk) return false;
-  if (a.causal) {
-    if (a.Tk % a.Tq == 0) {
-      if (j / (a.Tk / a.Tq) > i) return false;
-    } else {
-      if (j > i / (a.Tq / a.Tk)) return false;
-    }
-  }
-  if (a.qpad && a.kpad && a.qpad[(long)b * a.Tq + i] && a.kpad[(long)b * a.Tk + j]) return false;
-  return true;
-}
-
-// exclusive upper bound of keys any query in [q_lo, q_hi] can see
-__device__ __forceinline__ int key_limit(const AttnArgs& a, int q_hi) {
+// exclusive upper bound of the keys query i may see (causal rule only; Tk when not causal)
+__device__ __forceinline__ int key_bound(const AttnArgs& a, int i) {
   if (!a.causal) return a.Tk;
-  q_hi = min(q_hi, a.Tq - 1);
-  int lim;
-  if (a.Tk % a.Tq == 0) lim = (q_hi + 1) * (a.Tk / a.Tq);
-  else lim = q_hi / (a.Tq / a.Tk) + 1;
+  i = min(i, a.Tq - 1);
+  int lim = (a.Tk >= a.Tq) ? (i + 1) * (a.Tk / a.Tq) : i / (a.Tq / a.Tk) + 1;
   return min(lim, a.Tk);
 }
 
-// first query that can see key j_lo
-__device__ __forceinline__ int query_start(const AttnArgs& a, int j_lo) {
+// first query that may see key j (causal rule only)
+__device__ __forceinline__ int query_start(const AttnArgs& a, int j) {
   if (!a.causal) return 0;
-  if (a.Tk % a.Tq == 0) return j_lo / (a.Tk / a.Tq);
-  return j_lo * (a.Tq / a.Tk);
+  return (a.Tk >= a.Tq) ? j / (a.Tk / a.Tq) : j * (a.Tq / a.Tk);
 }
 
-static constexpr int KT = 32;  // keys (or queries) per LDS tile
+static constexpr int TT = 64;  // keys (forward, dQ) or queries (dK/dV) per LDS tile
 
 template <int D>
 struct AttnCfg {
-  static constexpr int DT = (D + 15) / 16;  // 16-wide d tiles
+  static constexpr int DT = (D + 15) / 16;  // 16-wide d tiles of the output
   static constexpr int DP = DT * 16;
   static constexpr int KS = D / 4;          // k-steps over d
-  static constexpr int SA = DP + 2;         // row stride for [row = lane&15] reads
+  static constexpr int SA = DP + 2;         // row stride for [row = lane&15][4s + lane>>4] reads
+  static constexpr int SV = DP + 4;         // row stride for [row = 4(lane>>4)+s][16dt + lane&15] reads
+  static constexpr int NV = TT * (D / 4) / 256;  // float4 per thread per tile (0 at D = 8: half the threads load)
+  static constexpr int NVR = NV > 0 ? NV : 1;
 };
 
-// load a [KT rows][D] tile (rows r0.., zero-filled past nrows) into LDS with row stride S
-template <int D, int S>
-__device__ __forceinline__ void load_rows(float* lds, const float* base, long bs_off, long ts, int hoff,
-                                          int r0, int nrows) {
-  constexpr int DP = AttnCfg<D>::DP;
-  for (int e = threadIdx.x; e < KT * DP; e += 256) {
-    int r = e / DP, d = e % DP;
-    float v = 0.0f;
-    if (d < D && r0 + r < nrows) v = base[bs_off + (long)(r0 + r) * ts + hoff + d];
-    lds[r * S + d] = v;
+// TT rows x D of a [T, ...] operand -> registers (float4, zero past nrows), then -> LDS.
+template <int D>
+struct TileRegs {
+  float4 r[AttnCfg<D>::NVR];
+  __device__ __forceinline__ void load(const float* base, long ts, int r0, int nrows) {
+    constexpr int C4 = D / 4;
+#pragma unroll
+    for (int i = 0; i < AttnCfg<D>::NVR; ++i) {
+      const int e = threadIdx.x + i * 256;
+      const int row = e / C4, c = (e % C4) * 4;
+      r[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < TT * C4 && r0 + row < nrows) r[i] = *reinterpret_cast<const float4*>(base + (long)(r0 + row) * ts + c);
+    }
   }
+  template <int S>
+  __device__ __forceinline__ void store(float* lds) const {
+    constexpr int C4 = D / 4;
+#pragma unroll
+    for (int i = 0; i < AttnCfg<D>::NVR; ++i) {
+      const int e = threadIdx.x + i * 256;
+      if (e < TT * C4) {
+        const int row = e / C4, c = (e % C4) * 4;
+        float* p = lds + row * S + c;
+        if (S % 4 == 0) {
+          *reinterpret_cast<float4*>(p) = r[i];
+        } else {
+          *reinterpret_cast<float2*>(p) = make_float2(r[i].x, r[i].y);
+          *reinterpret_cast<float2*>(p + 2) = make_float2(r[i].z, r[i].w);
+        }
+      }
+    }
+  }
+};
+
+// S^T tile (16 keys x 16 queries) = K rows [kr..kr+15] . Q^T, two accumulation chains
+template <int D>
+__device__ __forceinline__ f32x4 qk16(const float* Ks, int rowbase, const float (&qreg)[AttnCfg<D>::KS], int lq,
+                                      int lg) {
+  using C = AttnCfg<D>;
+  f32x4 s0 = f32x4{0.f, 0.f, 0.f, 0.f}, s1 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < C::KS; s += 2) {
+    s0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ks[(rowbase + lq) * C::SA + 4 * s + lg], qreg[s], s0, 0, 0, 0);
+    if (s + 1 < C::KS)
+      s1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ks[(rowbase + lq) * C::SA + 4 * (s + 1) + lg], qreg[s + 1], s1, 0,
+                                                0, 0);
+  }
+  return s0 + s1;
 }
 
 template <int D>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   using C = AttnCfg<D>;
-  __shared__ float Ks[KT * C::SA];
-  __shared__ float Vs[KT * (C::DP + 4)];
-  constexpr int SV = C::DP + 4;
+  __shared__ __attribute__((aligned(16))) float Ks[TT * C::SA];
+  __shared__ __attribute__((aligned(16))) float Vs[TT * C::SV];
+  __shared__ unsigned char Kp[TT];
   const int b = blockIdx.z, h = blockIdx.y;
   const int q0 = blockIdx.x * 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int lq = lane & 15, lg = lane >> 4;
   const int qi = q0 + wave * 16 + lq;
   const int hoff = h * D;
+  const bool pad = a.qpad && a.kpad;
+  const bool qp = pad && qi < a.Tq && a.qpad[(long)b * a.Tq + qi];
+  const int kmax = key_bound(a, qi);                    // this lane's query
+  const int wmin = key_bound(a, q0 + wave * 16);        // smallest bound in the wave (monotone in i)
 
   float qreg[C::KS];
 #pragma unroll
@@ -119,34 +152,45 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   for (int dt = 0; dt < C::DT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = -INFINITY, l = 0.0f;
 
-  const int klim = key_limit(a, q0 + 63);
-  for (int k0 = 0; k0 < klim; k0 += KT) {
+  const int klim = key_bound(a, q0 + 63);
+  const float* kb_ = a.k + (long)b * a.k_bs + hoff;
+  const float* vb_ = a.v + (long)b * a.v_bs + hoff;
+  TileRegs<D> tk, tv;
+  tk.load(kb_, a.k_ts, 0, a.Tk);
+  tv.load(vb_, a.v_ts, 0, a.Tk);
+  for (int k0 = 0; k0 < klim; k0 += TT) {
     __syncthreads();
-    load_rows<D, C::SA>(Ks, a.k, (long)b * a.k_bs, a.k_ts, hoff, k0, a.Tk);
-    load_rows<D, SV>(Vs, a.v, (long)b * a.v_bs, a.v_ts, hoff, k0, a.Tk);
+    tk.template store<C::SA>(Ks);
+    tv.template store<C::SV>(Vs);
+    if (pad && threadIdx.x < TT) Kp[threadIdx.x] = (k0 + threadIdx.x < a.Tk) ? a.kpad[(long)b * a.Tk + k0 + threadIdx.x] : 0;
     __syncthreads();
+    if (k0 + TT < klim) {
+      tk.load(kb_, a.k_ts, k0 + TT, a.Tk);
+      tv.load(vb_, a.v_ts, k0 + TT, a.Tk);
+    }
 #pragma unroll
-    for (int sub = 0; sub < KT / 16; ++sub) {
+    for (int sub = 0; sub < TT / 16; ++sub) {
       const int kb = k0 + sub * 16;
       if (kb >= klim) break;
-      f32x4 s4 = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < C::KS; ++s) {
-        float av = Ks[(sub * 16 + lq) * C::SA + 4 * s + lg];
-        s4 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, qreg[s], s4, 0, 0, 0);
-      }
+      f32x4 s4 = qk16<D>(Ks, sub * 16, qreg, lq, lg);
       float sv[4];
       float mx = -INFINITY;
+      if (!pad && kb + 16 <= wmin) {  // every query of the wave sees all 16 keys
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        int kj = kb + lg * 4 + r;
-        sv[r] = visible(a, b, qi, kj) ? s4[r] : -INFINITY;
-        mx = fmaxf(mx, sv[r]);
+        for (int r = 0; r < 4; ++r) { sv[r] = s4[r]; mx = fmaxf(mx, sv[r]); }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int kl = sub * 16 + lg * 4 + r;
+          const bool vis = (k0 + kl < kmax) && !(qp && Kp[kl]);
+          sv[r] = vis ? s4[r] : -INFINITY;
+          mx = fmaxf(mx, sv[r]);
+        }
       }
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      float mn = fmaxf(m, mx);
-      float alpha = (mn == -INFINITY) ? 1.0f : __expf(m - mn);
+      const float mn = fmaxf(m, mx);
+      const float alpha = (mn == -INFINITY) ? 1.0f : __expf(m - mn);
       float p[4];
       float ps = 0.0f;
 #pragma unroll
@@ -159,61 +203,37 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
       l = l * alpha + ps;
       m = mn;
 #pragma unroll
-      for (int dt = 0; dt < C::DT; ++dt) {
-        o[dt] *= alpha;
+      for (int dt = 0; dt < C::DT; ++dt) o[dt] *= alpha;
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          float av = Vs[(sub * 16 + 4 * lg + s) * SV + dt * 16 + lq];
-          o[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, p[s], o[dt], 0, 0, 0);
-        }
-      }
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int dt = 0; dt < C::DT; ++dt)
+          o[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Vs[(sub * 16 + 4 * lg + s) * C::SV + dt * 16 + lq], p[s],
+                                                       o[dt], 0, 0, 0);
     }
   }
   if (qi < a.Tq) {
-    float inv = 1.0f / l;  // l == 0 (fully masked row) -> NaN like softmax(-inf row)
+    const float inv = 1.0f / l;  // l == 0 (fully masked row) -> NaN like softmax(-inf row)
     float* op = a.o + (long)b * a.o_bs + (long)qi * a.o_ts + hoff;
 #pragma unroll
     for (int dt = 0; dt < C::DT; ++dt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        int d = dt * 16 + lg * 4 + r;
+        const int d = dt * 16 + lg * 4 + r;
         if (d < D) op[d] = (l == 0.0f) ? NAN : o[dt][r] * inv;
       }
     if (lg == 0) a.lse[((long)b * a.Hh + h) * a.Tq + qi] = (l == 0.0f) ? NAN : m + __logf(l);
   }
 }
 
-// dlt[b,h,q] = sum_d dO * O.  One wave per (b, q) row of all heads: float4 per
-// lane (coalesced 1-KiB row segments), per-head sums by shuffles within the
-// D/4 lanes that hold one head.
-__global__ __launch_bounds__(256) void attn_dlt_kernel(AttnArgs a, int D) {
-  const int lane = threadIdx.x & 63;
-  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= (long)a.B * a.Tq) return;
-  const int b = row / a.Tq, qi = row % a.Tq;
-  const int E = a.Hh * D;
-  const float* po = a.o + (long)b * a.o_bs + (long)qi * a.o_ts;
-  const float* pd = a.dout + (long)b * a.do_bs + (long)qi * a.do_ts;
-  const int gl = D / 4;  // lanes per head
-  for (int e0 = 0; e0 < E; e0 += 256) {
-    const int e = e0 + lane * 4;
-    float s = 0.0f;
-    if (e < E) {
-      float4 o4 = *reinterpret_cast<const float4*>(po + e);
-      float4 d4 = *reinterpret_cast<const float4*>(pd + e);
-      s = o4.x * d4.x + o4.y * d4.y + o4.z * d4.z + o4.w * d4.w;
-    }
-    for (int off = gl / 2; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
-    if (e < E && (lane % gl) == 0) a.dlt[((long)b * a.Hh + e / D) * a.Tq + qi] = s;
-  }
-}
-
-// dQ for 64 queries of one (b, head): recompute P^T, dP^T = V dO^T, dS^T, dQ^T += K^T dS^T
+// dQ for 64 queries of one (b, head): recompute P^T, dP^T = V dO^T, dS^T, dQ^T += K^T dS^T.
+// Also forms delta = rowsum(dO * O) for these rows (the dK/dV kernel reads it from a.dlt).
 template <int D>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
   using C = AttnCfg<D>;
-  __shared__ float Ks[KT * C::SA];
-  __shared__ float Vs[KT * C::SA];
+  __shared__ __attribute__((aligned(16))) float Ks[TT * C::SA];
+  __shared__ __attribute__((aligned(16))) float Vs[TT * C::SA];
+  __shared__ unsigned char Kp[TT];
   const int b = blockIdx.z, h = blockIdx.y;
   const int q0 = blockIdx.x * 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -221,51 +241,71 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
   const int qi = q0 + wave * 16 + lq;
   const int hoff = h * D;
   const bool qv = qi < a.Tq;
+  const bool pad = a.qpad && a.kpad;
+  const bool qp = pad && qv && a.qpad[(long)b * a.Tq + qi];
+  const int kmax = key_bound(a, qi);
+  const int wmin = key_bound(a, q0 + wave * 16);
   float qreg[C::KS], dreg[C::KS];
+  float dsum = 0.0f;
 #pragma unroll
   for (int s = 0; s < C::KS; ++s) {
-    qreg[s] = qv ? a.q[(long)b * a.q_bs + (long)qi * a.q_ts + hoff + 4 * s + lg] * a.scale : 0.0f;
-    dreg[s] = qv ? a.dout[(long)b * a.do_bs + (long)qi * a.do_ts + hoff + 4 * s + lg] : 0.0f;
+    const int d = 4 * s + lg;
+    qreg[s] = qv ? a.q[(long)b * a.q_bs + (long)qi * a.q_ts + hoff + d] * a.scale : 0.0f;
+    dreg[s] = qv ? a.dout[(long)b * a.do_bs + (long)qi * a.do_ts + hoff + d] : 0.0f;
+    const float ov = qv ? a.o[(long)b * a.o_bs + (long)qi * a.o_ts + hoff + d] : 0.0f;
+    dsum = fmaf(dreg[s], ov, dsum);
   }
+  dsum += __shfl_xor(dsum, 16, 64);
+  dsum += __shfl_xor(dsum, 32, 64);
   const long rowi = ((long)b * a.Hh + h) * a.Tq + qi;
   const float lse = qv ? a.lse[rowi] : 0.0f;
-  const float dl = qv ? a.dlt[rowi] : 0.0f;
+  const float dl = dsum;
+  if (qv && lg == 0) a.dlt[rowi] = dsum;
   f32x4 dq[C::DT];
 #pragma unroll
   for (int dt = 0; dt < C::DT; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int klim = key_limit(a, q0 + 63);
-  for (int k0 = 0; k0 < klim; k0 += KT) {
+  const int klim = key_bound(a, q0 + 63);
+  const float* kb_ = a.k + (long)b * a.k_bs + hoff;
+  const float* vb_ = a.v + (long)b * a.v_bs + hoff;
+  TileRegs<D> tk, tv;
+  tk.load(kb_, a.k_ts, 0, a.Tk);
+  tv.load(vb_, a.v_ts, 0, a.Tk);
+  for (int k0 = 0; k0 < klim; k0 += TT) {
     __syncthreads();
-    load_rows<D, C::SA>(Ks, a.k, (long)b * a.k_bs, a.k_ts, hoff, k0, a.Tk);
-    load_rows<D, C::SA>(Vs, a.v, (long)b * a.v_bs, a.v_ts, hoff, k0, a.Tk);
+    tk.template store<C::SA>(Ks);
+    tv.template store<C::SA>(Vs);
+    if (pad && threadIdx.x < TT) Kp[threadIdx.x] = (k0 + threadIdx.x < a.Tk) ? a.kpad[(long)b * a.Tk + k0 + threadIdx.x] : 0;
     __syncthreads();
+    if (k0 + TT < klim) {
+      tk.load(kb_, a.k_ts, k0 + TT, a.Tk);
+      tv.load(vb_, a.v_ts, k0 + TT, a.Tk);
+    }
 #pragma unroll
-    for (int sub = 0; sub < KT / 16; ++sub) {
+    for (int sub = 0; sub < TT / 16; ++sub) {
       const int kb = k0 + sub * 16;
       if (kb >= klim) break;
       f32x4 s4 = f32x4{0.f, 0.f, 0.f, 0.f};
       f32x4 dp4 = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < C::KS; ++s) {
-        float ka = Ks[(sub * 16 + lq) * C::SA + 4 * s + lg];
-        float va = Vs[(sub * 16 + lq) * C::SA + 4 * s + lg];
-        s4 = __builtin_amdgcn_mfma_f32_16x16x4f32(ka, qreg[s], s4, 0, 0, 0);
-        dp4 = __builtin_amdgcn_mfma_f32_16x16x4f32(va, dreg[s], dp4, 0, 0, 0);
+        s4 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ks[(sub * 16 + lq) * C::SA + 4 * s + lg], qreg[s], s4, 0, 0, 0);
+        dp4 = __builtin_amdgcn_mfma_f32_16x16x4f32(Vs[(sub * 16 + lq) * C::SA + 4 * s + lg], dreg[s], dp4, 0, 0, 0);
       }
+      const bool full = !pad && kb + 16 <= wmin;
       float ds[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        int kj = kb + lg * 4 + r;
-        float p = (qv && visible(a, b, qi, kj)) ? __expf(s4[r] - lse) : 0.0f;
+        const int kl = sub * 16 + lg * 4 + r;
+        const bool vis = qv && (full || ((k0 + kl < kmax) && !(qp && Kp[kl])));
+        const float p = vis ? __expf(s4[r] - lse) : 0.0f;
         ds[r] = p * (dp4[r] - dl);
       }
 #pragma unroll
-      for (int dt = 0; dt < C::DT; ++dt)
+      for (int s = 0; s < 4; ++s)
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          float ka = Ks[(sub * 16 + 4 * lg + s) * C::SA + dt * 16 + lq];
-          dq[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(ka, ds[s], dq[dt], 0, 0, 0);
-        }
+        for (int dt = 0; dt < C::DT; ++dt)
+          dq[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ks[(sub * 16 + 4 * lg + s) * C::SA + dt * 16 + lq], ds[s],
+                                                        dq[dt], 0, 0, 0);
     }
   }
   if (qv) {
@@ -274,7 +314,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
     for (int dt = 0; dt < C::DT; ++dt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        int d = dt * 16 + lg * 4 + r;
+        const int d = dt * 16 + lg * 4 + r;
         if (d < D) op[d] = dq[dt][r] * a.scale;
       }
   }
@@ -285,9 +325,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
 template <int D>
 __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
   using C = AttnCfg<D>;
-  __shared__ float Qs[KT * C::SA];
-  __shared__ float Ds[KT * C::SA];
-  __shared__ float Ls[KT], Dl[KT];
+  __shared__ __attribute__((aligned(16))) float Qs[TT * C::SA];
+  __shared__ __attribute__((aligned(16))) float Ds[TT * C::SA];
+  __shared__ float Ls[TT], Dl[TT];
+  __shared__ unsigned char Qp[TT];
   const int b = blockIdx.z, h = blockIdx.y;
   const int kb0 = blockIdx.x * 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -295,6 +336,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
   const int kj = kb0 + wave * 16 + lk;
   const int hoff = h * D;
   const bool kv = kj < a.Tk;
+  const bool pad = a.qpad && a.kpad;
+  const bool kp = pad && kv && a.kpad[(long)b * a.Tk + kj];
+  const int qmin = query_start(a, kj);                       // first query seeing this lane's key
+  const int wmax = query_start(a, min(kb0 + wave * 16 + 15, a.Tk - 1));  // largest in the wave
   float kreg[C::KS], vreg[C::KS];
 #pragma unroll
   for (int s = 0; s < C::KS; ++s) {
@@ -307,45 +352,57 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
     dkT[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
     dvT[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  const int qs = (query_start(a, kb0) / KT) * KT;
-  for (int qt0 = qs; qt0 < a.Tq; qt0 += KT) {
+  const int qs = (query_start(a, kb0) / 16) * 16;
+  const float* qb_ = a.q + (long)b * a.q_bs + hoff;
+  const float* db_ = a.dout + (long)b * a.do_bs + hoff;
+  TileRegs<D> tq, td;
+  if (qs < a.Tq) {
+    tq.load(qb_, a.q_ts, qs, a.Tq);
+    td.load(db_, a.do_ts, qs, a.Tq);
+  }
+  for (int qt0 = qs; qt0 < a.Tq; qt0 += TT) {
     __syncthreads();
-    load_rows<D, C::SA>(Qs, a.q, (long)b * a.q_bs, a.q_ts, hoff, qt0, a.Tq);
-    load_rows<D, C::SA>(Ds, a.dout, (long)b * a.do_bs, a.do_ts, hoff, qt0, a.Tq);
-    if (threadIdx.x < KT) {
-      int qq = qt0 + threadIdx.x;
-      long ri = ((long)b * a.Hh + h) * a.Tq + qq;
+    tq.template store<C::SA>(Qs);
+    td.template store<C::SA>(Ds);
+    if (threadIdx.x < TT) {
+      const int qq = qt0 + threadIdx.x;
+      const long ri = ((long)b * a.Hh + h) * a.Tq + qq;
       Ls[threadIdx.x] = qq < a.Tq ? a.lse[ri] : 0.0f;
       Dl[threadIdx.x] = qq < a.Tq ? a.dlt[ri] : 0.0f;
+      if (pad) Qp[threadIdx.x] = qq < a.Tq ? a.qpad[(long)b * a.Tq + qq] : 0;
     }
     __syncthreads();
+    if (qt0 + TT < a.Tq) {
+      tq.load(qb_, a.q_ts, qt0 + TT, a.Tq);
+      td.load(db_, a.do_ts, qt0 + TT, a.Tq);
+    }
 #pragma unroll
-    for (int sub = 0; sub < KT / 16; ++sub) {
+    for (int sub = 0; sub < TT / 16; ++sub) {
       const int qb = qt0 + sub * 16;
       if (qb >= a.Tq) break;
       f32x4 s4 = f32x4{0.f, 0.f, 0.f, 0.f};
       f32x4 dp4 = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < C::KS; ++s) {
-        float qa = Qs[(sub * 16 + lk) * C::SA + 4 * s + lg];
-        float da = Ds[(sub * 16 + lk) * C::SA + 4 * s + lg];
-        s4 = __builtin_amdgcn_mfma_f32_16x16x4f32(qa, kreg[s], s4, 0, 0, 0);
-        dp4 = __builtin_amdgcn_mfma_f32_16x16x4f32(da, vreg[s], dp4, 0, 0, 0);
+        s4 = __builtin_amdgcn_mfma_f32_16x16x4f32(Qs[(sub * 16 + lk) * C::SA + 4 * s + lg], kreg[s], s4, 0, 0, 0);
+        dp4 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ds[(sub * 16 + lk) * C::SA + 4 * s + lg], vreg[s], dp4, 0, 0, 0);
       }
+      // every key of the wave is seen by all 16 queries of the sub-tile (all < Tq)
+      const bool full = !pad && qb >= wmax && qb + 16 <= a.Tq;
       float p[4], ds[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        int ql = sub * 16 + lg * 4 + r;  // query row of this accumulator register
-        int qq = qt0 + ql;
-        bool vis = kv && visible(a, b, qq, kj);
+        const int ql = sub * 16 + lg * 4 + r;  // query row of this accumulator register
+        const int qq = qt0 + ql;
+        const bool vis = kv && (full || (qq >= qmin && qq < a.Tq && !(kp && Qp[ql])));
         p[r] = vis ? __expf(s4[r] * a.scale - Ls[ql]) : 0.0f;
         ds[r] = p[r] * (dp4[r] - Dl[ql]);
       }
 #pragma unroll
-      for (int dt = 0; dt < C::DT; ++dt)
+      for (int s = 0; s < 4; ++s)
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          int row = (sub * 16 + 4 * lg + s) * C::SA + dt * 16 + lk;
+        for (int dt = 0; dt < C::DT; ++dt) {
+          const int row = (sub * 16 + 4 * lg + s) * C::SA + dt * 16 + lk;
           dvT[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ds[row], p[s], dvT[dt], 0, 0, 0);
           dkT[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Qs[row], ds[s], dkT[dt], 0, 0, 0);
         }
@@ -358,7 +415,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
     for (int dt = 0; dt < C::DT; ++dt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        int d = dt * 16 + lg * 4 + r;
+        const int d = dt * 16 + lg * 4 + r;
         if (d < D) {
           pk[d] = dkT[dt][r] * a.scale;
           pv[d] = dvT[dt][r];
@@ -384,6 +441,10 @@ static AttnArgs attn_base(int B, int Hh, int Tq, int Tk, const float* q, long q_
   return a;
 }
 
+static bool rows16(const float* p, long bs, long ts) {
+  return p == nullptr || ((((uintptr_t)p) & 15) == 0 && (bs & 3) == 0 && (ts & 3) == 0);
+}
+
 static int attn_check(int D, int Tq, int Tk, int causal) {
   MRG_REQUIRE(D == 8 || D == 16 || D == 32 || D == 64, "attention: unsupported head dim %d", D);
   MRG_REQUIRE(!causal || Tq == 0 || Tk == 0 || Tk % Tq == 0 || Tq % Tk == 0,
@@ -406,6 +467,8 @@ MRG_API int mrg_attention_fwd(int B, int Hh, int Tq, int Tk, int D,
                               int causal, float scale, hipStream_t stream) {
   if (int e = attn_check(D, Tq, Tk, causal)) return e;
   if (B == 0 || Tq == 0) return 0;
+  MRG_REQUIRE(rows16(k, k_bs, k_ts) && rows16(v, v_bs, v_ts),
+              "attention fwd: K/V rows must be 16-B aligned (strides multiple of 4 floats)");
   AttnArgs a = attn_base(B, Hh, Tq, Tk, q, q_bs, q_ts, k, k_bs, k_ts, v, v_bs, v_ts, o, o_bs, o_ts, lse,
                          qpad, kpad, causal, scale);
   dim3 grid((Tq + 63) / 64, Hh, B);
@@ -426,18 +489,16 @@ MRG_API int mrg_attention_bwd(int B, int Hh, int Tq, int Tk, int D,
                               float* dv, long dv_bs, long dv_ts, float* workspace, hipStream_t stream) {
   if (int e = attn_check(D, Tq, Tk, causal)) return e;
   if (B == 0 || Tq == 0 || Tk == 0) return 0;
+  MRG_REQUIRE(rows16(q, q_bs, q_ts) && rows16(k, k_bs, k_ts) && rows16(v, v_bs, v_ts) &&
+              rows16(dout, do_bs, do_ts), "attention bwd: Q/K/V/dO rows must be 16-B aligned");
+  MRG_REQUIRE(workspace != nullptr, "attention bwd: workspace (B*heads*Tq floats) required");
   AttnArgs a = attn_base(B, Hh, Tq, Tk, q, q_bs, q_ts, k, k_bs, k_ts, v, v_bs, v_ts, o, o_bs, o_ts, lse,
                          qpad, kpad, causal, scale);
   a.dout = dout; a.do_bs = do_bs; a.do_ts = do_ts; a.dlt = workspace;
   a.dq = dq; a.dq_bs = dq_bs; a.dq_ts = dq_ts; a.dk = dk; a.dk_bs = dk_bs; a.dk_ts = dk_ts;
   a.dv = dv; a.dv_bs = dv_bs; a.dv_ts = dv_ts;
-  MRG_REQUIRE((o_ts & 3) == 0 && (do_ts & 3) == 0 && (o_bs & 3) == 0 && (do_bs & 3) == 0 &&
-              (((uintptr_t)o | (uintptr_t)dout) & 15) == 0, "attention bwd: O/dO rows must be 16-B aligned");
-  long rows = (long)B * Tq;
-  attn_dlt_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, stream>>>(a, D);
-  if (check_launch("attn_dlt_kernel")) return 1;
   dim3 gq((Tq + 63) / 64, Hh, B);
-  MRG_ATTN_DISPATCH(attn_bwd_dq_kernel, gq, a);
+  MRG_ATTN_DISPATCH(attn_bwd_dq_kernel, gq, a);  // also writes delta = rowsum(dO * O) to the workspace
   if (check_launch("attn_bwd_dq_kernel")) return 1;
   dim3 gk((Tk + 63) / 64, Hh, B);
   MRG_ATTN_DISPATCH(attn_bwd_dkv_kernel, gk, a);
