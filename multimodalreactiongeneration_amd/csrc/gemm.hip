@@ -16,6 +16,7 @@
 // bank-conflict free; global loads for the next K tile are issued before the
 // MFMAs of the current one (register prefetch).
 #include "mrg_common.h"
+#include <cstdlib>
 
 namespace mrg {
 
@@ -38,9 +39,11 @@ struct GemmArgs {
   long ldaux;
   float* ws;  // split-K slabs [splits][M][N] (nullptr when splits == 1)
   int kchunk;
+  int tiles_n, tiles_mn, ntiles;  // output tiles (x splits), walked by a persistent grid
+  int vec;                        // C / bias / aux / slab rows 16-B aligned: vector epilogue
 };
 
-static constexpr int BK = 32;
+static constexpr int BK = 32;  // K tile (64 measured no faster here: 2 blocks/CU instead of 3)
 static constexpr int NT = 256;
 
 __device__ __forceinline__ float apply_epi(const GemmArgs& a, float v, int m, int n) {
@@ -52,13 +55,48 @@ __device__ __forceinline__ float apply_epi(const GemmArgs& a, float v, int m, in
   return v;
 }
 
+// C[m, n..n+3] (or the split-K slab row) from four accumulators: one 16-B access per operand when
+// the rows are 16-B aligned (a.vec), element-wise at the N edge or for unaligned operands.
+__device__ __forceinline__ void store4(const GemmArgs& a, int z, int m, int n, float4 v) {
+  if (a.ws) {
+    float* p = a.ws + ((long)z * a.M + m) * a.N + n;
+    if (a.vec && n + 3 < a.N) { *reinterpret_cast<float4*>(p) = v; return; }
+    const float e[4] = {v.x, v.y, v.z, v.w};
+    for (int q = 0; q < 4 && n + q < a.N; ++q) p[q] = e[q];
+    return;
+  }
+  if (a.vec && n + 3 < a.N) {
+    float* pc = a.C + (long)m * a.ldc + n;
+    float4 o = make_float4(v.x * a.alpha, v.y * a.alpha, v.z * a.alpha, v.w * a.alpha);
+    if (a.beta != 0.0f) {
+      const float4 c = *reinterpret_cast<const float4*>(pc);
+      o.x += a.beta * c.x; o.y += a.beta * c.y; o.z += a.beta * c.z; o.w += a.beta * c.w;
+    }
+    if (a.bias) {
+      const float4 b = *reinterpret_cast<const float4*>(a.bias + n);
+      o.x += b.x; o.y += b.y; o.z += b.z; o.w += b.w;
+    }
+    if (a.epi == 1) {
+      o.x = fmaxf(o.x, 0.0f); o.y = fmaxf(o.y, 0.0f); o.z = fmaxf(o.z, 0.0f); o.w = fmaxf(o.w, 0.0f);
+    } else if (a.epi == 2) {
+      const float4 x = *reinterpret_cast<const float4*>(a.aux + (long)m * a.ldaux + n);
+      o.x = x.x > 0.0f ? o.x : 0.0f; o.y = x.y > 0.0f ? o.y : 0.0f;
+      o.z = x.z > 0.0f ? o.z : 0.0f; o.w = x.w > 0.0f ? o.w : 0.0f;
+    }
+    *reinterpret_cast<float4*>(pc) = o;
+    return;
+  }
+  const float e[4] = {v.x, v.y, v.z, v.w};
+  for (int q = 0; q < 4 && n + q < a.N; ++q) a.C[(long)m * a.ldc + n + q] = apply_epi(a, e[q], m, n + q);
+}
+
 // One operand tile (rows of the MFMA M or N dimension x BK) staged k-major in LDS:
 // S[k][x], x = m (or n).  TR says which index is contiguous in memory:
 //   TR = 1 : memory row = k, contiguous along x  -> float4 along x, ds_write_b128
 //   TR = 0 : memory row = x, contiguous along k  -> float4 along k (8 lanes cover
 //            one 128-B k-run of a row), four scalar LDS writes; row pitch X + 1
 //            keeps those writes bank-conflict free.
-template <int X, int TR, bool VEC>
+template <int X, int TR, bool VEC, int BK>
 struct TileIO {
   static constexpr int PAD = TR ? 4 : 1;
   static constexpr int LD = X + PAD;
@@ -121,77 +159,103 @@ struct TileIO {
   }
 };
 
-template <int BM, int BN, int TA, int TB, bool VA, bool VB>
-__global__ __launch_bounds__(NT) void gemm_f32_kernel(GemmArgs a) {
-  using IA = TileIO<BM, TA, VA>;
-  using IB = TileIO<BN, !TB, VB>;  // B(k, n): memory row k when TB == 0 (contiguous along n)
+template <int BM, int BN, int BK, int TA, int TB, bool VA, bool VB>
+__global__ __launch_bounds__(NT, (BK == 32 ? 3 : 2)) void gemm_f32_kernel(GemmArgs a) {
+  using IA = TileIO<BM, TA, VA, BK>;
+  using IB = TileIO<BN, !TB, VB, BK>;  // B(k, n): memory row k when TB == 0 (contiguous along n)
   constexpr int TM = BM / 64, TN = BN / 64;
   __shared__ __attribute__((aligned(16))) float As[BK * IA::LD];
   __shared__ __attribute__((aligned(16))) float Bs[BK * IB::LD];
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int m0 = blockIdx.y * BM;
-  const int n0 = blockIdx.x * BN;
-  const int kbeg = blockIdx.z * a.kchunk;
-  const int kend = min(a.K, kbeg + a.kchunk);
-
-  IA ia;
-  IB ib;
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-
   const int wm = (wave >> 1) * (BM / 2);
   const int wn = (wave & 1) * (BN / 2);
   const int lr = lane & 31, lk = lane >> 5;
 
-  if (kbeg < kend) {
-    ia.load(a.A, a.amap, m0, a.M, kbeg, kend);
-    ib.load(a.B, a.bmap, n0, a.N, kbeg, kend);
-  }
-  for (int k0 = kbeg; k0 < kend; k0 += BK) {
-    ia.store(As);
-    ib.store(Bs);
-    __syncthreads();
-    if (k0 + BK < kend) {  // next tile's global loads fly under this tile's MFMAs
-      ia.load(a.A, a.amap, m0, a.M, k0 + BK, kend);
-      ib.load(a.B, a.bmap, n0, a.N, k0 + BK, kend);
+  // Persistent walk over output tiles (n fastest, so co-running blocks share A rows in L2).
+  // The first K tile of the NEXT output tile is loaded under the last MFMAs of this one, so
+  // its HBM latency and this tile's epilogue stores overlap instead of adding up (K = 256
+  // GEMMs are 8 K tiles long: the per-tile prologue was a third of their time).
+  auto coords = [&](int t, int& m0, int& n0, int& kbeg, int& kend) {
+    const int z = t / a.tiles_mn, r = t - z * a.tiles_mn;
+    m0 = (r / a.tiles_n) * BM;
+    n0 = (r % a.tiles_n) * BN;
+    kbeg = z * a.kchunk;
+    kend = min(a.K, kbeg + a.kchunk);
+  };
+  IA ia;
+  IB ib;
+  int t = blockIdx.x;
+  int m0, n0, kbeg, kend;
+  if (t < a.ntiles) {
+    coords(t, m0, n0, kbeg, kend);
+    if (kbeg < kend) {
+      ia.load(a.A, a.amap, m0, a.M, kbeg, kend);
+      ib.load(a.B, a.bmap, n0, a.N, kbeg, kend);
     }
-#pragma unroll
-    for (int kk = 0; kk < BK / 2; ++kk) {
-      float fa[TM], fb[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) fa[i] = As[(2 * kk + lk) * IA::LD + wm + i * 32 + lr];
-#pragma unroll
-      for (int j = 0; j < TN; ++j) fb[j] = Bs[(2 * kk + lk) * IB::LD + wn + j * 32 + lr];
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
-    }
-    __syncthreads();
   }
+  for (; t < a.ntiles; t += gridDim.x) {
+    const int tn = t + gridDim.x;
+    int m1 = 0, n1 = 0, kb1 = 0, ke1 = 0;
+    if (tn < a.ntiles) coords(tn, m1, n1, kb1, ke1);
 
-  // epilogue: C/D map of the 32x32 f32 MFMA: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
+    f32x16 acc[TM][TN];
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        int m = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
-        int n = n0 + wn + j * 32 + lr;
-        if (m < a.M && n < a.N) {
-          if (a.ws) a.ws[((long)blockIdx.z * a.M + m) * a.N + n] = acc[i][j][r];
-          else a.C[(long)m * a.ldc + n] = apply_epi(a, acc[i][j][r], m, n);
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+    for (int k0 = kbeg; k0 < kend; k0 += BK) {
+      ia.store(As);
+      ib.store(Bs);
+      __syncthreads();
+      {  // next K tile's global loads fly under this tile's MFMAs (or the next output tile's first)
+        const bool more = k0 + BK < kend;
+        const int lm = more ? m0 : m1, ln = more ? n0 : n1;
+        const int lk = more ? k0 + BK : kb1, lke = more ? kend : ke1;
+        if (more || (tn < a.ntiles && kb1 < ke1)) {
+          ia.load(a.A, a.amap, lm, a.M, lk, lke);
+          ib.load(a.B, a.bmap, ln, a.N, lk, lke);
         }
       }
+#pragma unroll
+      for (int kk = 0; kk < BK / 2; ++kk) {
+        float fa[TM], fb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[i] = As[(2 * kk + lk) * IA::LD + wm + i * 32 + lr];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[j] = Bs[(2 * kk + lk) * IB::LD + wn + j * 32 + lr];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fb[j], fa[i], acc[i][j], 0, 0, 0);
+      }
+      __syncthreads();
+    }
+
+    // epilogue.  The MFMA computes C^T (B fragment as its first operand), so with its C/D map
+    // (col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)) a lane holds, for ONE row m of C, four
+    // consecutive columns per r>>2: every C access is a 16-B vector.
+    const int z = t / a.tiles_mn;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wm + i * 32 + lr;
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) {
+          const int n = n0 + wn + j * 32 + 8 * r4 + 4 * lk;
+          const float4 v = make_float4(acc[i][j][4 * r4], acc[i][j][4 * r4 + 1], acc[i][j][4 * r4 + 2],
+                                       acc[i][j][4 * r4 + 3]);
+          if (m < a.M) store4(a, z, m, n, v);
+        }
+    }
+    m0 = m1; n0 = n1; kbeg = kb1; kend = ke1;
+  }
 }
 
 __global__ void splitk_reduce_kernel(GemmArgs a, int splits) {
@@ -252,14 +316,41 @@ __global__ __launch_bounds__(1024) void colsum_final_kernel(const float* part, i
   }
 }
 
-template <int BM, int BN>
-static void launch_tile(const GemmArgs& a, int ta, int tb, bool va, bool vb, int splits, hipStream_t s) {
-  dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM, splits);
+// blocks per CU the hardware admits for a kernel (cached per kernel), x CUs of the current device
+template <typename K>
+static int resident_blocks(K kernel) {
+  static int per_cu = -1;
+  static int cus[16] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 16) dev = 0;
+  if (per_cu < 0) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(kernel), NT, 0) != hipSuccess || n < 1)
+      n = 1;
+    per_cu = n;
+  }
+  if (cus[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1) n = 256;
+    cus[dev] = n;
+  }
+  return per_cu * cus[dev];
+}
+
+template <int BM, int BN, int BK>
+static void launch_tile(GemmArgs a, int ta, int tb, bool va, bool vb, int splits, hipStream_t s) {
+  a.tiles_n = (a.N + BN - 1) / BN;
+  a.tiles_mn = a.tiles_n * ((a.M + BM - 1) / BM);
+  a.ntiles = a.tiles_mn * splits;
   const int code = (ta << 3) | (tb << 2) | ((int)va << 1) | (int)vb;
   switch (code) {
-#define MRG_G(TA, TB, VA, VB) \
-    case (TA << 3) | (TB << 2) | (VA << 1) | VB: \
-      gemm_f32_kernel<BM, BN, TA, TB, (bool)VA, (bool)VB><<<grid, NT, 0, s>>>(a); break;
+#define MRG_G(TA, TB, VA, VB)                                                                    \
+    case (TA << 3) | (TB << 2) | (VA << 1) | VB: {                                               \
+      auto k = gemm_f32_kernel<BM, BN, BK, TA, TB, (bool)VA, (bool)VB>;                              \
+      const int grid = a.ntiles < resident_blocks(k) ? a.ntiles : resident_blocks(k);           \
+      k<<<grid, NT, 0, s>>>(a);                                                                  \
+    } break;
     MRG_G(0, 0, 0, 0) MRG_G(0, 0, 0, 1) MRG_G(0, 0, 1, 0) MRG_G(0, 0, 1, 1)
     MRG_G(0, 1, 0, 0) MRG_G(0, 1, 0, 1) MRG_G(0, 1, 1, 0) MRG_G(0, 1, 1, 1)
     MRG_G(1, 0, 0, 0) MRG_G(1, 0, 0, 1) MRG_G(1, 0, 1, 0) MRG_G(1, 0, 1, 1)
@@ -268,13 +359,14 @@ static void launch_tile(const GemmArgs& a, int ta, int tb, bool va, bool vb, int
   }
 }
 
-static int launch_gemm(const GemmArgs& a, int tile, int ta, int tb, bool va, bool vb, int splits,
+static int launch_gemm(const GemmArgs& a, int tile, int bk, int ta, int tb, bool va, bool vb, int splits,
                        hipStream_t s) {
   ta = ta ? 1 : 0;
   tb = tb ? 1 : 0;
-  if (tile == 0) launch_tile<128, 128>(a, ta, tb, va, vb, splits, s);
-  else if (tile == 1) launch_tile<128, 64>(a, ta, tb, va, vb, splits, s);
-  else launch_tile<64, 64>(a, ta, tb, va, vb, splits, s);
+  (void)bk;  // BK = 64 measured no faster on these shapes (short K): only BK = 32 is instantiated
+  if (tile == 0) launch_tile<128, 128, BK>(a, ta, tb, va, vb, splits, s);
+  else if (tile == 1) launch_tile<128, 64, BK>(a, ta, tb, va, vb, splits, s);
+  else launch_tile<64, 64, BK>(a, ta, tb, va, vb, splits, s);
   return 0;
 }
 
@@ -303,9 +395,10 @@ MRG_API int mrg_gemm_f32(int M, int N, int K, float alpha,
   a.A = A; a.amap = RowMap{lda, lda_hi, a_rdiv}; a.transA = transA;
   a.B = B; a.bmap = RowMap{ldb, ldb_hi, b_rdiv}; a.transB = transB;
   a.C = C; a.ldc = ldc; a.bias = bias; a.epi = epilogue; a.aux = aux; a.ldaux = ldaux;
+  const int bk = BK;
   int kc = (K + splits - 1) / splits;
-  kc = ((kc + BK - 1) / BK) * BK;
-  if (kc == 0) kc = BK;
+  kc = ((kc + bk - 1) / bk) * bk;
+  if (kc == 0) kc = bk;
   splits = (K + kc - 1) / kc;
   if (splits < 1) splits = 1;
   a.kchunk = kc;
@@ -315,11 +408,18 @@ MRG_API int mrg_gemm_f32(int M, int N, int K, float alpha,
     return ((uintptr_t)p & 15) == 0 && (m.ld_lo & 3) == 0 && (m.rdiv <= 0 || (m.ld_hi & 3) == 0);
   };
   const bool va = aligned(A, a.amap), vb = aligned(B, a.bmap);
+  a.vec = ((((uintptr_t)C | (uintptr_t)bias | (uintptr_t)aux | (uintptr_t)workspace) & 15) == 0 && (ldc & 3) == 0 &&
+           (!aux || (ldaux & 3) == 0) && (!a.ws || (N & 3) == 0)) ? 1 : 0;
   int tile;  // 0: 128x128, 1: 128x64, 2: 64x64
   if (M >= 2048 && N > 64) tile = ((long)((M + 127) / 128) * ((N + 127) / 128) * splits >= 400) ? 0 : 1;
   else if (M >= 2048) tile = 1;
   else tile = 2;
-  if (launch_gemm(a, tile, transA, transB, va, vb, splits, stream)) return 2;
+  static const int tile_override = [] {  // tuning only: MRG_GEMM_TILE=0|1|2 forces one tile shape
+    const char* e = getenv("MRG_GEMM_TILE");
+    return e ? atoi(e) : -1;
+  }();
+  if (tile_override >= 0 && tile_override <= 2) tile = tile_override;
+  if (launch_gemm(a, tile, bk, transA, transB, va, vb, splits, stream)) return 2;
   if (check_launch("gemm_f32_kernel")) return 1;
   if (splits > 1) {
     long total = (long)M * N;
