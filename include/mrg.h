@@ -41,6 +41,14 @@ int mrg_device_cu_count(int device, int* out);
  * 433-435,474,504, lstm_with_sample.py:92-130) and the x W_ih^T / weight-grad
  * GEMMs inside cuDNN's LSTM (mixer_block.py:237-252).                      */
 size_t mrg_gemm_workspace_bytes(int M, int N, int splits);
+/* Arithmetic of every GEMM: 1 (default) = fp32 via a three-plane bf16 split
+ * (v = v0 + v1 + v2, |residual| <= 2^-24 |v|; the six products with i+j <= 2
+ * accumulated in fp32 on the bf16 matrix cores, <= ~2^-22 |ab| per product);
+ * 0 = exact f32 MFMA (a k-ordered fmaf chain).  Env MRG_GEMM_EXACT=1 -> 0.  */
+int mrg_gemm_set_mode(int mode);
+int mrg_gemm_get_mode(void);
+/* Tuning only: force the tile shape (0: 128x128, 1: 128x64, 2: 64x64), -1 = heuristic. */
+int mrg_gemm_force_tile(int tile);
 int mrg_gemm_f32(int M, int N, int K, float alpha,
                  const float* A, int transA, long lda, long lda_hi, int a_rdiv,
                  const float* B, int transB, long ldb, long ldb_hi, int b_rdiv,

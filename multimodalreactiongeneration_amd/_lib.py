@@ -31,6 +31,9 @@ SIGNATURES = {
     "mrg_version": (c_int, []),
     "mrg_device_cu_count": (c_int, [c_int, PI]),
     "mrg_gemm_workspace_bytes": (c_size, [c_int, c_int, c_int]),
+    "mrg_gemm_set_mode": (c_int, [c_int]),
+    "mrg_gemm_get_mode": (c_int, []),
+    "mrg_gemm_force_tile": (c_int, [c_int]),
     "mrg_gemm_f32": (c_int, [c_int, c_int, c_int, c_float,
                              P, c_int, c_long, c_long, c_int,
                              P, c_int, c_long, c_long, c_int,

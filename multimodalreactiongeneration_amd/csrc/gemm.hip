@@ -258,6 +258,251 @@ __global__ __launch_bounds__(NT, (BK == 32 ? 3 : 2)) void gemm_f32_kernel(GemmAr
   }
 }
 
+// ----------------------------------------------------------------------------------------------
+// fp32 GEMM on the bf16 matrix cores: "x6" split.  Every fp32 operand is cut into three bf16
+// planes v = v0 + v1 + v2 + r (v0 = bf16(v), v1 = bf16(v - v0), v2 = bf16(v - v0 - v1),
+// |r| <= 2^-24 |v|: 24 significand bits, the fp32 width) while it is staged into LDS, and the
+// six products with i + j <= 2 (a0b0, a0b1, a1b0, a0b2, a1b1, a2b0) are accumulated in fp32 by
+// v_mfma_f32_32x32x16_bf16.  bf16 x bf16 products are exact in fp32; the dropped terms and
+// the residuals are <= ~2^-22 |a b| per product, the accuracy class of an fp32 fmaf chain
+// (2^-24 per op), at 6 x 32 = 192 MFMA cycles per 32x32x16 block instead of 8 x 64 = 512 on
+// v_mfma_f32_32x32x2_f32.  bf16 keeps the fp32 exponent range, so no scaling is needed.
+//
+// LDS image per plane: [x][32 k] bf16 (64-B rows), 16-B chunks c = k / 8.  Byte offset
+//   off(x, c) = 256 (x >> 2) + 64 ((x & 3) ^ g) + 16 (c ^ g),  g = (x >> 2) & 3
+// keeps the fragment reads (16 lanes = 16 consecutive rows, one chunk) and both staging
+// patterns (4 rows x 64 B per 32 lanes, or 4 rows spaced 4 apart) bank-conflict free.
+static constexpr int XBK = 32;
+
+__device__ __forceinline__ int x6_off(int x, int c) {
+  const int g = (x >> 2) & 3;
+  return ((x >> 2) << 8) + (((x & 3) ^ g) << 6) + ((c ^ g) << 4);
+}
+
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+// two floats -> packed bf16 pair (RNE), one v_cvt_pk_bf16_f32
+__device__ __forceinline__ unsigned pk_bf16(float a, float b) {
+  const f32x2 v = {a, b};
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2));
+}
+
+// two values -> three planes of 2 bf16: 3 cvt_pk + 2 x (and, shift, packed sub) per pair
+__device__ __forceinline__ void split2(float a, float b, unsigned& p0, unsigned& p1, unsigned& p2) {
+  p0 = pk_bf16(a, b);
+  a -= __uint_as_float(p0 << 16);
+  b -= __uint_as_float(p0 & 0xffff0000u);
+  p1 = pk_bf16(a, b);
+  a -= __uint_as_float(p1 << 16);
+  b -= __uint_as_float(p1 & 0xffff0000u);
+  p2 = pk_bf16(a, b);
+}
+
+// four consecutive-k values -> three planes of 4 bf16 (8 B each)
+__device__ __forceinline__ void split4(float v0, float v1, float v2, float v3, uint2& p0, uint2& p1, uint2& p2) {
+  split2(v0, v1, p0.x, p1.x, p2.x);
+  split2(v2, v3, p0.y, p1.y, p2.y);
+}
+
+// One operand tile (X rows of the MFMA M or N dimension x XBK) for the x6 kernel.
+//   TR = 0 : memory row = x, contiguous along k: thread loads float4 (x, 4 k), 8 threads per row
+//   TR = 1 : memory row = k, contiguous along x: thread loads a 4 k x 4 x block (4 float4) and
+//            transposes it in registers (kg = tid % 8 fastest, so 32 lanes write 4 rows 4 apart)
+template <int X, int TR, bool VEC>
+struct TileX6 {
+  static constexpr int NV = TR ? 4 : X * XBK / 4 / NT;
+  static constexpr int ACT = TR ? (X / 4) * (XBK / 4) : NT;  // active threads
+  float4 r[NV];
+
+  __device__ __forceinline__ void load(const float* base, const RowMap& map, int x0, int xlim, int k0, int kend) {
+    const int tid = threadIdx.x;
+    if (TR) {
+      if (tid >= ACT) return;
+      const int kg = tid & 7, mg = tid >> 3;
+      const int gx = x0 + 4 * mg;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int gk = k0 + 4 * kg + i;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (gk < kend) {
+          const float* p = base + map.off(gk) + gx;
+          if (VEC && gx + 3 < xlim) v = *reinterpret_cast<const float4*>(p);
+          else {
+            if (gx < xlim) v.x = p[0];
+            if (gx + 1 < xlim) v.y = p[1];
+            if (gx + 2 < xlim) v.z = p[2];
+            if (gx + 3 < xlim) v.w = p[3];
+          }
+        }
+        r[i] = v;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int e = tid + i * NT;
+        const int x = e >> 3, gk = k0 + 4 * (e & 7), gx = x0 + x;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (gx < xlim) {
+          const float* p = base + map.off(gx) + gk;
+          if (VEC && gk + 3 < kend) v = *reinterpret_cast<const float4*>(p);
+          else {
+            if (gk < kend) v.x = p[0];
+            if (gk + 1 < kend) v.y = p[1];
+            if (gk + 2 < kend) v.z = p[2];
+            if (gk + 3 < kend) v.w = p[3];
+          }
+        }
+        r[i] = v;
+      }
+    }
+  }
+
+  __device__ __forceinline__ void store(unsigned char* S0, unsigned char* S1, unsigned char* S2) const {
+    const int tid = threadIdx.x;
+    if (TR) {
+      if (tid >= ACT) return;
+      const int kg = tid & 7, mg = tid >> 3;
+      const float c0[4] = {r[0].x, r[0].y, r[0].z, r[0].w};
+      const float c1[4] = {r[1].x, r[1].y, r[1].z, r[1].w};
+      const float c2[4] = {r[2].x, r[2].y, r[2].z, r[2].w};
+      const float c3[4] = {r[3].x, r[3].y, r[3].z, r[3].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint2 p0, p1, p2;
+        split4(c0[j], c1[j], c2[j], c3[j], p0, p1, p2);
+        const int o = x6_off(4 * mg + j, kg >> 1) + 8 * (kg & 1);
+        *reinterpret_cast<uint2*>(S0 + o) = p0;
+        *reinterpret_cast<uint2*>(S1 + o) = p1;
+        *reinterpret_cast<uint2*>(S2 + o) = p2;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int e = tid + i * NT;
+        const int x = e >> 3, q = e & 7;
+        uint2 p0, p1, p2;
+        split4(r[i].x, r[i].y, r[i].z, r[i].w, p0, p1, p2);
+        const int o = x6_off(x, q >> 1) + 8 * (q & 1);
+        *reinterpret_cast<uint2*>(S0 + o) = p0;
+        *reinterpret_cast<uint2*>(S1 + o) = p1;
+        *reinterpret_cast<uint2*>(S2 + o) = p2;
+      }
+    }
+  }
+};
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+template <int BM, int BN, int TA, int TB, bool VA, bool VB>
+__global__ __launch_bounds__(NT, 2) void gemm_x6_kernel(GemmArgs a) {
+  using IA = TileX6<BM, TA, VA>;
+  using IB = TileX6<BN, !TB, VB>;  // B(k, n): memory row k when TB == 0 (contiguous along n)
+  constexpr int TM = BM / 64, TN = BN / 64;
+  __shared__ __attribute__((aligned(16))) unsigned char sA[3][BM * 64];
+  __shared__ __attribute__((aligned(16))) unsigned char sB[3][BN * 64];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wm = (wave >> 1) * (BM / 2);
+  const int wn = (wave & 1) * (BN / 2);
+  const int lr = lane & 31, lh = lane >> 5;
+
+  auto coords = [&](int t, int& m0, int& n0, int& kbeg, int& kend) {
+    const int z = t / a.tiles_mn, r = t - z * a.tiles_mn;
+    m0 = (r / a.tiles_n) * BM;
+    n0 = (r % a.tiles_n) * BN;
+    kbeg = z * a.kchunk;
+    kend = min(a.K, kbeg + a.kchunk);
+  };
+  IA ia;
+  IB ib;
+  int t = blockIdx.x;
+  int m0, n0, kbeg, kend;
+  if (t < a.ntiles) {
+    coords(t, m0, n0, kbeg, kend);
+    if (kbeg < kend) {
+      ia.load(a.A, a.amap, m0, a.M, kbeg, kend);
+      ib.load(a.B, a.bmap, n0, a.N, kbeg, kend);
+    }
+  }
+  for (; t < a.ntiles; t += gridDim.x) {
+    const int tn = t + gridDim.x;
+    int m1 = 0, n1 = 0, kb1 = 0, ke1 = 0;
+    if (tn < a.ntiles) coords(tn, m1, n1, kb1, ke1);
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+    for (int k0 = kbeg; k0 < kend; k0 += XBK) {
+      ia.store(sA[0], sA[1], sA[2]);
+      ib.store(sB[0], sB[1], sB[2]);
+      __syncthreads();
+      {
+        const bool more = k0 + XBK < kend;
+        const int lm = more ? m0 : m1, ln = more ? n0 : n1;
+        const int lk = more ? k0 + XBK : kb1, lke = more ? kend : ke1;
+        if (more || (tn < a.ntiles && kb1 < ke1)) {
+          ia.load(a.A, a.amap, lm, a.M, lk, lke);
+          ib.load(a.B, a.bmap, ln, a.N, lk, lke);
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < XBK / 16; ++s) {
+        bf16x8 fa[TM][3], fb[TN][3];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int o = x6_off(wm + i * 32 + lr, 2 * s + lh);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) fa[i][p] = *reinterpret_cast<const bf16x8*>(sA[p] + o);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int o = x6_off(wn + j * 32 + lr, 2 * s + lh);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) fb[j][p] = *reinterpret_cast<const bf16x8*>(sB[p] + o);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            // small terms first; the MFMA operand order (B, A) yields C^T per lane (epilogue below)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][2], fa[i][0], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][1], fa[i][1], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][0], fa[i][2], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][1], fa[i][0], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][0], fa[i][1], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][0], fa[i][0], acc[i][j], 0, 0, 0);
+          }
+      }
+      __syncthreads();
+    }
+
+    // epilogue: same C^T lane map as the f32 kernel (one row m, four consecutive n per r>>2)
+    const int z = t / a.tiles_mn;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wm + i * 32 + lr;
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) {
+          const int n = n0 + wn + j * 32 + 8 * r4 + 4 * lh;
+          const float4 v = make_float4(acc[i][j][4 * r4], acc[i][j][4 * r4 + 1], acc[i][j][4 * r4 + 2],
+                                       acc[i][j][4 * r4 + 3]);
+          if (m < a.M) store4(a, z, m, n, v);
+        }
+    }
+    m0 = m1; n0 = n1; kbeg = kb1; kend = ke1;
+  }
+}
+
 __global__ void splitk_reduce_kernel(GemmArgs a, int splits) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   long total = (long)a.M * a.N;
@@ -266,6 +511,40 @@ __global__ void splitk_reduce_kernel(GemmArgs a, int splits) {
   float s = 0.0f;
   for (int z = 0; z < splits; ++z) s += a.ws[(long)z * total + idx];
   a.C[(long)m * a.ldc + n] = apply_epi(a, s, m, n);
+}
+
+// Vector form (a.vec, N % 4 == 0): a thread owns four consecutive columns and keeps eight slab
+// loads in flight (four partial sums over z mod 4, combined in a fixed order: deterministic).
+__global__ __launch_bounds__(256) void splitk_reduce4_kernel(GemmArgs a, int splits) {
+  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)a.M * a.N;
+  const long idx = q * 4;
+  if (idx >= total) return;
+  const float4* ws = reinterpret_cast<const float4*>(a.ws) + q;
+  const long zs = total / 4;
+  float4 s[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) s[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  int z = 0;
+  for (; z + 8 <= splits; z += 8) {
+    float4 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = ws[(long)(z + i) * zs];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      s[i & 3].x += v[i].x; s[i & 3].y += v[i].y; s[i & 3].z += v[i].z; s[i & 3].w += v[i].w;
+    }
+  }
+  for (; z < splits; ++z) {
+    const float4 v = ws[(long)z * zs];
+    s[z & 3].x += v.x; s[z & 3].y += v.y; s[z & 3].z += v.z; s[z & 3].w += v.w;
+  }
+  const float4 r = make_float4((s[0].x + s[1].x) + (s[2].x + s[3].x), (s[0].y + s[1].y) + (s[2].y + s[3].y),
+                               (s[0].z + s[1].z) + (s[2].z + s[3].z), (s[0].w + s[1].w) + (s[2].w + s[3].w));
+  const int m = idx / a.N, n = idx % a.N;
+  GemmArgs b = a;
+  b.ws = nullptr;  // store4 writes C (with alpha / beta / bias / epilogue) instead of a slab
+  store4(b, 0, m, n, r);
 }
 
 // column sums, stage 1: part[s][n] = sum of X(row, n) over rows [s*rows_per, (s+1)*rows_per).
@@ -359,11 +638,46 @@ static void launch_tile(GemmArgs a, int ta, int tb, bool va, bool vb, int splits
   }
 }
 
+template <int BM, int BN>
+static void launch_tile_x6(GemmArgs a, int ta, int tb, bool va, bool vb, int splits, hipStream_t s) {
+  a.tiles_n = (a.N + BN - 1) / BN;
+  a.tiles_mn = a.tiles_n * ((a.M + BM - 1) / BM);
+  a.ntiles = a.tiles_mn * splits;
+  const int code = (ta << 3) | (tb << 2) | ((int)va << 1) | (int)vb;
+  switch (code) {
+#define MRG_G(TA, TB, VA, VB)                                                                    \
+    case (TA << 3) | (TB << 2) | (VA << 1) | VB: {                                               \
+      auto k = gemm_x6_kernel<BM, BN, TA, TB, (bool)VA, (bool)VB>;                                \
+      const int grid = a.ntiles < resident_blocks(k) ? a.ntiles : resident_blocks(k);           \
+      k<<<grid, NT, 0, s>>>(a);                                                                  \
+    } break;
+    MRG_G(0, 0, 0, 0) MRG_G(0, 0, 0, 1) MRG_G(0, 0, 1, 0) MRG_G(0, 0, 1, 1)
+    MRG_G(0, 1, 0, 0) MRG_G(0, 1, 0, 1) MRG_G(0, 1, 1, 0) MRG_G(0, 1, 1, 1)
+    MRG_G(1, 0, 0, 0) MRG_G(1, 0, 0, 1) MRG_G(1, 0, 1, 0) MRG_G(1, 0, 1, 1)
+    MRG_G(1, 1, 0, 0) MRG_G(1, 1, 0, 1) MRG_G(1, 1, 1, 0) MRG_G(1, 1, 1, 1)
+#undef MRG_G
+  }
+}
+
+static int g_tile_override = -1;
+
+// GEMM arithmetic: 1 = x6 bf16 split on the bf16 matrix cores (default), 0 = exact f32 MFMA
+static int g_gemm_mode = [] {
+  const char* e = getenv("MRG_GEMM_EXACT");
+  return (e && atoi(e) != 0) ? 0 : 1;
+}();
+
 static int launch_gemm(const GemmArgs& a, int tile, int bk, int ta, int tb, bool va, bool vb, int splits,
                        hipStream_t s) {
   ta = ta ? 1 : 0;
   tb = tb ? 1 : 0;
   (void)bk;  // BK = 64 measured no faster on these shapes (short K): only BK = 32 is instantiated
+  if (g_gemm_mode == 1) {
+    if (tile == 0) launch_tile_x6<128, 128>(a, ta, tb, va, vb, splits, s);
+    else if (tile == 1) launch_tile_x6<128, 64>(a, ta, tb, va, vb, splits, s);
+    else launch_tile_x6<64, 64>(a, ta, tb, va, vb, splits, s);
+    return 0;
+  }
   if (tile == 0) launch_tile<128, 128, BK>(a, ta, tb, va, vb, splits, s);
   else if (tile == 1) launch_tile<128, 64, BK>(a, ta, tb, va, vb, splits, s);
   else launch_tile<64, 64, BK>(a, ta, tb, va, vb, splits, s);
@@ -373,6 +687,22 @@ static int launch_gemm(const GemmArgs& a, int tile, int bk, int ta, int tb, bool
 }  // namespace mrg
 
 using namespace mrg;
+
+// GEMM arithmetic mode: 1 = fp32 via the x6 bf16 split (default), 0 = exact f32 MFMA
+// (v_mfma_f32_32x32x2_f32, a k-ordered fmaf chain).  Env MRG_GEMM_EXACT=1 selects 0 at load.
+MRG_API int mrg_gemm_set_mode(int mode) {
+  MRG_REQUIRE(mode == 0 || mode == 1, "mrg_gemm_set_mode: mode must be 0 or 1");
+  g_gemm_mode = mode;
+  return 0;
+}
+MRG_API int mrg_gemm_get_mode(void) { return g_gemm_mode; }
+
+// Tuning only: force one tile shape (0: 128x128, 1: 128x64, 2: 64x64; -1 = heuristic).
+MRG_API int mrg_gemm_force_tile(int tile) {
+  MRG_REQUIRE(tile >= -1 && tile <= 2, "mrg_gemm_force_tile: tile must be -1..2");
+  g_tile_override = tile;
+  return 0;
+}
 
 MRG_API size_t mrg_gemm_workspace_bytes(int M, int N, int splits) {
   return splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;
@@ -411,19 +741,32 @@ MRG_API int mrg_gemm_f32(int M, int N, int K, float alpha,
   a.vec = ((((uintptr_t)C | (uintptr_t)bias | (uintptr_t)aux | (uintptr_t)workspace) & 15) == 0 && (ldc & 3) == 0 &&
            (!aux || (ldaux & 3) == 0) && (!a.ws || (N & 3) == 0)) ? 1 : 0;
   int tile;  // 0: 128x128, 1: 128x64, 2: 64x64
-  if (M >= 2048 && N > 64) tile = ((long)((M + 127) / 128) * ((N + 127) / 128) * splits >= 400) ? 0 : 1;
-  else if (M >= 2048) tile = 1;
-  else tile = 2;
-  static const int tile_override = [] {  // tuning only: MRG_GEMM_TILE=0|1|2 forces one tile shape
-    const char* e = getenv("MRG_GEMM_TILE");
-    return e ? atoi(e) : -1;
-  }();
-  if (tile_override >= 0 && tile_override <= 2) tile = tile_override;
+  if (g_gemm_mode == 1) {
+    // x6 (measured on the step's shapes, tools_gemm_sweep.py): 128x128 for split-K weight
+    // gradients and wide/deep products; 64x64 for narrow ones (N <= 128, or N = 256 at K <= 512
+    // with K-contiguous B); small problems take the tile that gives the most workgroups
+    const long t0 = (long)((M + 127) / 128) * ((N + 127) / 128) * splits;
+    if (splits > 1) tile = 0;
+    else if (t0 < 256) tile = 2;
+    else if (N >= 512 || K >= 1024) tile = 0;
+    else if (N <= 128) tile = 2;
+    else tile = transB ? 2 : 0;
+  } else if (M >= 2048 && N > 64) {
+    tile = ((long)((M + 127) / 128) * ((N + 127) / 128) * splits >= 400) ? 0 : 1;
+  } else if (M >= 2048) {
+    tile = 1;
+  } else {
+    tile = 2;
+  }
+  if (g_tile_override >= 0 && g_tile_override <= 2) tile = g_tile_override;
   if (launch_gemm(a, tile, bk, transA, transB, va, vb, splits, stream)) return 2;
   if (check_launch("gemm_f32_kernel")) return 1;
   if (splits > 1) {
     long total = (long)M * N;
-    splitk_reduce_kernel<<<(unsigned)((total + 255) / 256), 256, 0, stream>>>(a, splits);
+    if (a.vec && (N & 3) == 0)
+      splitk_reduce4_kernel<<<(unsigned)((total / 4 + 255) / 256), 256, 0, stream>>>(a, splits);
+    else
+      splitk_reduce_kernel<<<(unsigned)((total + 255) / 256), 256, 0, stream>>>(a, splits);
     if (check_launch("splitk_reduce_kernel")) return 1;
   }
   return 0;

@@ -127,7 +127,15 @@ def gemm(M, N, K, A, transA, lda, B, transB, ldb, C, ldc, *, alpha=1.0, beta=0.0
 
 
 def wgrad_splits(M, N, K):
-    """split-K factor for weight-gradient GEMMs (small M x N output, long B*T reduction)."""
+    """split-K factor for weight-gradient GEMMs (small M x N output, long B*T reduction).
+
+    About 512 workgroups: 128x128 tiles under the x6 arithmetic (chunks of >= 128 rows),
+    64x64 tiles under exact f32 (chunks of >= 256 rows); tools_gemm_sweep.py measured both.
+    """
+    if _lib.load().mrg_gemm_get_mode() == 1:
+        tiles = ((M + 127) // 128) * ((N + 127) // 128)
+        s = max(1, 512 // max(1, tiles))
+        return int(max(1, min(s, K // 128, 128)))
     tiles = ((M + 63) // 64) * ((N + 63) // 64)
     s = max(1, 512 // max(1, tiles))
     return int(max(1, min(s, K // 256, 64)))

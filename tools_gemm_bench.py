@@ -33,6 +33,11 @@ PROBES = [
     ("square TN 4096^3", 4096, 4096, 4096, 1, 0, 0, False),
     ("4096x4096 K=256 NT", 4096, 4096, 256, 0, 1, 0, False),
     ("19200x1024 K=1024 NT", R, 1024, 1024, 0, 1, 0, False),
+    ("odd NN 1000x70x45", 1000, 70, 45, 0, 0, 0, False),
+    ("odd NT 333x129x97", 333, 129, 97, 0, 1, 0, False),
+    ("odd TN 130x66x1001", 130, 66, 1001, 1, 0, 0, False),
+    ("odd TT 77x200x33", 77, 200, 33, 1, 1, 0, False),
+    ("odd wgrad 1024x6x19200", 6, 1024, R, 1, 0, 0, True),
 ]
 
 
@@ -48,7 +53,11 @@ def run_shape(M, N, K, ta, tb, wgrad, iters=20):
     def go():
         Fn.gemm(M, N, K, Fn._ptr(A), ta, lda, Fn._ptr(B), tb, ldb, Fn._ptr(C), N,
                 beta=1.0 if wgrad else 0.0, splits=splits, device=A.device)
-    for _ in range(3):
+    go()
+    torch.cuda.synchronize()
+    ref = ((A.t() if ta else A).double() @ (B.t() if tb else B).double())
+    err = ((C.double() - ref).abs().max() / ref.abs().max()).item()
+    for _ in range(2):
         go()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -58,16 +67,19 @@ def run_shape(M, N, K, ta, tb, wgrad, iters=20):
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / iters
-    # check one shape's numerics against torch fp32 (different summation order: loose)
-    ref = (A.t() if ta else A) @ (B.t() if tb else B)
-    if not wgrad:
-        err = (C - ref).abs().max().item() / ref.abs().max().item()
-    else:
-        err = float("nan")
     return ms, splits, err
 
 
 def main():
+    from multimodalreactiongeneration_amd import _lib
+    modes = [int(m) for m in sys.argv[1].split(",")] if len(sys.argv) > 1 else [1, 0]
+    for mode in modes:
+        _lib.check(_lib.load().mrg_gemm_set_mode(mode), "mode")
+        print(f"=== GEMM mode {mode} ({'x6 bf16 split' if mode == 1 else 'exact f32 MFMA'})")
+        one_mode()
+
+
+def one_mode():
     tot_ms = tot_fl = 0.0
     for name, M, N, K, ta, tb, calls, wgrad in SHAPES:
         ms, splits, err = run_shape(M, N, K, ta, tb, wgrad)
@@ -79,7 +91,7 @@ def main():
               f"{tf:6.1f} TF/s ({tf/157.3*100:5.1f}%)  x{calls}/step  err={err:.1e}")
     print(f"step-weighted: {tot_ms:.2f} ms/step, {tot_fl/(tot_ms/1e3)/1e12:.1f} TF/s")
     for name, M, N, K, ta, tb, calls, wgrad in PROBES:
-        ms, splits, err = run_shape(M, N, K, ta, tb, wgrad, iters=5)
+        ms, splits, err = run_shape(M, N, K, ta, tb, wgrad, iters=5)  # noqa
         tf = 2.0 * M * N * K / (ms / 1e3) / 1e12
         print(f"{name:20s} {ms*1e3:8.1f} us  {tf:6.1f} TF/s ({tf/157.3*100:5.1f}%)  err={err:.1e}")
 

@@ -8,7 +8,7 @@ cd /tmp
 P1="SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA"
 P2="SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"
 i=0
-for shape in "19200 1024 256 0 1" "4096 4096 4096 0 1"; do
+for shape in ${GPMC_SHAPES:-"19200 1024 256 0 1"}; do
   for P in "$P1" "$P2"; do
     i=$((i+1))
     timeout -k 10 200 rocprofv3 --pmc $P -d $R/gpurun_out/gpmc/p$i -o p --output-format csv -- python3 $R/tools_gemm_one.py $shape 5 > $R/gpurun_out/gpmc/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $R/gpurun_out/gpmc/p$i.log; exit 1; }
