@@ -25,6 +25,36 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "training frames/sec/GPU, lstmformer T=300 B=64; 1→8 GPU scaling"
 FP32_MFMA_PEAK_TF = 157.3   # MI355X_MICROARCH.md chip table (f32 matrix, dense)
 HBM_PEAK_GBS = 8000.0
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
+
+# probe name (functional._probe) -> kernels it brackets; FLOPs are algorithmic
+FAMILIES = {
+    "gemm": "gemm_x6_kernel (+ splitk_reduce4_kernel): every GEMM of the step, 2MNK FLOP per launch",
+    "lstm_fwd": "lstm_fwd_kernel<256,8,BS>: persistent recurrence, 8H^2 FLOP per (b, t) per layer",
+    "lstm_bwd": "lstm_bwd_kernel<256,8,BS>: persistent reverse recurrence, 8H^2 FLOP per (b, t) per layer",
+    "attn_fwd": "attn_fwd_kernel<64>: block-causal flash attention, 4D FLOP per visible (q, k) pair per head",
+    "attn_bwd": "attn_bwd_dq_kernel<64> + attn_bwd_dkv_kernel<64>: 10D FLOP per visible pair per head",
+}
+PEAK_NOTES = {
+    "gemm": "peak = f32 dense matrix peak (the dtype's); the GEMMs compute fp32 as a three-plane bf16 split "
+            "(6 bf16 MFMAs per product, fp32-class error), whose own MFMA ceiling is 2500/6 = 416.7 TFLOP/s",
+    "lstm_fwd": "latency-bound (one cross-CU hand-off per time step); VALU v_pk_fma_f32 peak = 157.3",
+    "lstm_bwd": "latency-bound (one cross-CU hand-off per time step); VALU v_pk_fma_f32 peak = 157.3",
+}
+# rocprofv3 kernel-name prefix of each family in the PMC summary (tools_pmc_summary.py)
+PMC_KEYS = {"gemm": "gemm_x6_kernel", "lstm_fwd": "lstm_fwd_kernel", "lstm_bwd": "lstm_bwd_kernel",
+            "attn_fwd": "attn_fwd_kernel", "attn_bwd": "attn_bwd"}
+
+
+def pmc_traffic(family):
+    """HBM bytes per launch of a family from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            doc = json.load(f)
+        fam = doc["families"].get(PMC_KEYS[family])
+        return None if fam is None else round(fam["hbm_bytes_per_launch"])
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def parse():
@@ -39,7 +69,6 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--probe", default="lstm_fwd", help="kernel family for the live roofline")
     ap.add_argument("--lstm-group", type=int, default=0, help="workgroups per LSTM row group at H=256 (8|16; 0 = library default)")
     return ap.parse_args()
 
@@ -68,6 +97,7 @@ def cpu_baseline(args, mc, oc):
     from multimodalreactiongeneration_amd.model import Metaformer
     from multimodalreactiongeneration_amd.synthetic import make_batch, clone_batch
     torch.set_num_threads(args.cpu_threads)
+    O.ATEN_LSTM = True   # the oneDNN LSTM op the reference's nn.LSTM runs on CPU, not the parity loop
     torch.manual_seed(0)
     sd = {k: v.detach().clone() for k, v in Metaformer(mc, oc, {"use_centroid": True, "use_angle": True,
                                                                    "delta_order": 0}).state_dict().items()}
@@ -80,9 +110,10 @@ def cpu_baseline(args, mc, oc):
     t = sorted(times[1:])[len(times[1:]) // 2]
     return {"value": round(args.batch * args.seq / t, 2), "unit": "frames/s", "cores": torch.get_num_threads(),
             "kind": "port",
-            "sample": f"oracle/mrg_oracle.py lstmformer train step (fwd+loss+bwd+AdamW) B={args.batch} "
-                      f"T={args.seq} r={args.ratio}, median of {args.cpu_steps} steps after 1 warm-up, "
-                      f"{torch.get_num_threads()} threads, {time.strftime('%Y-%m-%d')}"}
+            "sample": f"oracle/mrg_oracle.py lstmformer train step (fwd+loss+bwd+AdamW; LSTMs on the "
+                      f"fused ATen op nn.LSTM uses on CPU) B={args.batch} T={args.seq} r={args.ratio}, median of "
+                      f"{args.cpu_steps} steps after 1 warm-up, {torch.get_num_threads()} threads, "
+                      f"{time.strftime('%Y-%m-%d')}"}
 
 
 def main():
@@ -168,31 +199,37 @@ def main():
     frames = args.batch * args.seq * world
     value = frames * args.steps / elapsed
 
-    # live per-kernel timing of the dominant kernel family: eager steps with HIP events on the launch stream
-    roof = None
+    # live per-family kernel timing: HIP events recorded on the launch stream around every library
+    # call of two eager steps right after the timed region (a graph replay cannot be bracketed);
+    # each launch carries its algorithmic FLOPs (functional._probe), so achieved = FLOPs / time
+    fams = tuple(FAMILIES)
     if rank == 0:
-        Fn.probe_start(args.probe)
+        Fn.probe_start(*fams)
     for _ in range(2):      # every rank steps (the all-reduce is collective); rank 0 records
         step()
-    per = Fn.probe_stop().get(args.probe, []) if rank == 0 else []
+    per = Fn.probe_stop(with_work=True) if rank == 0 else {}
+    kernels, roof = {}, None
     if rank == 0:
-        H, B, T = mc.hidden_size, args.batch, args.seq
-        if per and args.probe == "lstm_fwd":
-            # launches per step: block0 layer0 (3 problems, or 2+1 at r>1), 4 more encoder layers (2),
-            # 4 main-stream layers (1): algorithmic FLOPs = recurrent h W_hh^T GEMV + gates
-            per_step = sum(per) / 2
-            launches = len(per) // 2
-            rec_layers = 3 + 2 * (mc.encoder_num_layer - 1) + (mc.num_block - 1)
-            flop = 2.0 * B * 4 * H * H * T * rec_layers * (1.0 if args.ratio == 1 else 1.0)
-            if args.ratio != 1:
-                flop = 2.0 * B * 4 * H * H * T * (1 + (mc.num_block - 1) + mc.encoder_num_layer) \
-                    + 2.0 * B * 4 * H * H * T * args.ratio * mc.encoder_num_layer
-            achieved = flop / (per_step / 1000.0) / 1e12
-            roof = {"kernel": "lstm_fwd_kernel<256,8,BS> (persistent recurrence, all fwd launches of a step)",
-                    "bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_MFMA_PEAK_TF,
-                    "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TF, 4), "traffic": None,
-                    "avg_launch_ms": round(per_step / launches, 4), "launches_per_step": launches,
-                    "algorithmic_flop_per_step": flop}
+        for f in fams:
+            v = per.get(f, [])
+            if not v:
+                continue
+            fms = sum(t for t, _ in v) / 2.0
+            work = sum(w for _, w in v) / 2.0
+            n = len(v) / 2.0
+            tf = work / (fms / 1e3) / 1e12
+            kernels[f] = {"kernel": FAMILIES[f], "ms_per_step": round(fms, 3), "launches_per_step": n,
+                          "avg_launch_ms": round(fms / n, 4), "algorithmic_flop_per_launch": work / n,
+                          "achieved_tflops": round(tf, 2), "frac_of_fp32_peak": round(tf / FP32_MFMA_PEAK_TF, 4)}
+        if kernels:
+            dom = max(kernels, key=lambda f: kernels[f]["ms_per_step"])
+            k = kernels[dom]
+            roof = {"kernel": k["kernel"], "family": dom, "bound": "mfma", "achieved": k["achieved_tflops"],
+                    "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s", "frac": k["frac_of_fp32_peak"],
+                    "traffic": pmc_traffic(dom), "avg_launch_ms": k["avg_launch_ms"],
+                    "launches_per_step": k["launches_per_step"],
+                    "algorithmic_flop_per_launch": k["algorithmic_flop_per_launch"],
+                    "peak_note": PEAK_NOTES.get(dom, "")}
     step_flop = (model_flops_per_frame(mc, args.ratio) + attn_flops_per_frame(mc, args.ratio, args.seq)) \
         * args.batch * args.seq
     out = {
@@ -208,6 +245,7 @@ def main():
                                 "peak": FP32_MFMA_PEAK_TF,
                                 "frac": round(step_flop / (ms / 1000.0) / 1e12 / FP32_MFMA_PEAK_TF, 4)},
         "roofline": roof,
+        "kernels": kernels,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and args.cpu_baseline:

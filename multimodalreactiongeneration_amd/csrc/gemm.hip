@@ -41,6 +41,13 @@ struct GemmArgs {
   int kchunk;
   int tiles_n, tiles_mn, ntiles;  // output tiles (x splits), walked by a persistent grid
   int vec;                        // C / bias / aux / slab rows 16-B aligned: vector epilogue
+  // fused row sums of op(A) (bias gradients of a weight-gradient GEMM, TA = 1, x6 path):
+  // per-(split, m) partials in asum [splits][M], reduced in a fixed order into
+  // asum_out[m] = asum_beta * asum_out[m] + sum (and asum_out2, nullable)
+  float* asum;
+  float* asum_out;
+  float* asum_out2;
+  float asum_beta;
 };
 
 static constexpr int BK = 32;  // K tile (64 measured no faster here: 2 blocks/CU instead of 3)
@@ -359,6 +366,16 @@ struct TileX6 {
     }
   }
 
+  // TR = 1: add this thread's 4 k-rows into per-x sums (column j = x offset 4 mg + j)
+  __device__ __forceinline__ void accum(float (&cs)[4]) const {
+    if (TR && (int)threadIdx.x < ACT) {
+      cs[0] += (r[0].x + r[1].x) + (r[2].x + r[3].x);
+      cs[1] += (r[0].y + r[1].y) + (r[2].y + r[3].y);
+      cs[2] += (r[0].z + r[1].z) + (r[2].z + r[3].z);
+      cs[3] += (r[0].w + r[1].w) + (r[2].w + r[3].w);
+    }
+  }
+
   __device__ __forceinline__ void store(unsigned char* S0, unsigned char* S1, unsigned char* S2) const {
     const int tid = threadIdx.x;
     if (TR) {
@@ -439,8 +456,11 @@ __global__ __launch_bounds__(NT, 2) void gemm_x6_kernel(GemmArgs a) {
       for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+    const bool do_asum = TA && a.asum && n0 == 0;
+    float cs[4] = {0.f, 0.f, 0.f, 0.f};
 
     for (int k0 = kbeg; k0 < kend; k0 += XBK) {
+      if (do_asum) ia.accum(cs);
       ia.store(sA[0], sA[1], sA[2]);
       ib.store(sB[0], sB[1], sB[2]);
       __syncthreads();
@@ -486,6 +506,22 @@ __global__ __launch_bounds__(NT, 2) void gemm_x6_kernel(GemmArgs a) {
 
     // epilogue: same C^T lane map as the f32 kernel (one row m, four consecutive n per r>>2)
     const int z = t / a.tiles_mn;
+    if (do_asum) {  // the 8 k-group lanes of an m-group sum their partials; lane kg = 0 writes
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        cs[j] += __shfl_xor(cs[j], 1, 64);
+        cs[j] += __shfl_xor(cs[j], 2, 64);
+        cs[j] += __shfl_xor(cs[j], 4, 64);
+      }
+      const int mg = threadIdx.x >> 3;
+      if ((threadIdx.x & 7) == 0 && (int)threadIdx.x < IA::ACT) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int m = m0 + 4 * mg + j;
+          if (m < a.M) a.asum[(long)z * a.M + m] = cs[j];
+        }
+      }
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int m = m0 + wm + i * 32 + lr;
@@ -513,38 +549,72 @@ __global__ void splitk_reduce_kernel(GemmArgs a, int splits) {
   a.C[(long)m * a.ldc + n] = apply_epi(a, s, m, n);
 }
 
-// Vector form (a.vec, N % 4 == 0): a thread owns four consecutive columns and keeps eight slab
-// loads in flight (four partial sums over z mod 4, combined in a fixed order: deterministic).
+// Split-K slab reduce.  A block = 32 outputs x 8 z-groups: thread (o, g) sums slabs
+// z = g, g + 8, ... (two loads in flight), then group 0 adds the 8 partials from LDS in a
+// fixed order (deterministic).  Vector outputs (float4 of C) when a.vec and N % 4 == 0; the
+// fused row sums of A (a.asum, [splits][M]) ride in trailing blocks of scalar outputs.
+static constexpr int RZG = 8;   // z-groups per output
+static constexpr int RPB = 32;  // outputs per block
+
+template <typename V>
+__device__ __forceinline__ V zsum(const V* base, long zs, int splits, int g) {
+  V s0 = V{}, s1 = V{};
+  int z = g;
+  for (; z + RZG < splits; z += 2 * RZG) {
+    const V v0 = base[(long)z * zs], v1 = base[(long)(z + RZG) * zs];
+    s0 += v0;
+    s1 += v1;
+  }
+  if (z < splits) s0 += base[(long)z * zs];
+  return s0 + s1;
+}
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+// row sums of A for RPB rows per block (fused bias gradients)
+__device__ __forceinline__ void asum_block(const GemmArgs& a, int splits, long blk) {
+  __shared__ float rs[RZG][RPB];
+  const int o = threadIdx.x % RPB, g = threadIdx.x / RPB;
+  const long m = blk * RPB + o;
+  rs[g][o] = m < a.M ? zsum(a.asum + m, (long)a.M, splits, g) : 0.0f;
+  __syncthreads();
+  if (g == 0 && m < a.M) {
+    float r = rs[0][o];
+#pragma unroll
+    for (int i = 1; i < RZG; ++i) r += rs[i][o];
+    a.asum_out[m] = (a.asum_beta != 0.0f ? a.asum_beta * a.asum_out[m] : 0.0f) + r;
+    if (a.asum_out2) a.asum_out2[m] = (a.asum_beta != 0.0f ? a.asum_beta * a.asum_out2[m] : 0.0f) + r;
+  }
+}
+
+__global__ __launch_bounds__(256) void asum_reduce_kernel(GemmArgs a, int splits) {
+  asum_block(a, splits, blockIdx.x);
+}
+
 __global__ __launch_bounds__(256) void splitk_reduce4_kernel(GemmArgs a, int splits) {
-  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ f32x4v red[RZG][RPB];
+  const int o = threadIdx.x % RPB, g = threadIdx.x / RPB;
   const long total = (long)a.M * a.N;
-  const long idx = q * 4;
-  if (idx >= total) return;
-  const float4* ws = reinterpret_cast<const float4*>(a.ws) + q;
-  const long zs = total / 4;
-  float4 s[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) s[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  int z = 0;
-  for (; z + 8 <= splits; z += 8) {
-    float4 v[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = ws[(long)(z + i) * zs];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      s[i & 3].x += v[i].x; s[i & 3].y += v[i].y; s[i & 3].z += v[i].z; s[i & 3].w += v[i].w;
-    }
+  const long cblocks = (total / 4 + RPB - 1) / RPB;
+  if ((long)blockIdx.x >= cblocks) {  // trailing blocks: the fused bias-gradient sums
+    asum_block(a, splits, (long)blockIdx.x - cblocks);
+    return;
   }
-  for (; z < splits; ++z) {
-    const float4 v = ws[(long)z * zs];
-    s[z & 3].x += v.x; s[z & 3].y += v.y; s[z & 3].z += v.z; s[z & 3].w += v.w;
+  const long q = (long)blockIdx.x * RPB + o;  // float4 index into C
+  f32x4v s = f32x4v{0.f, 0.f, 0.f, 0.f};
+  if (q * 4 < total) s = zsum(reinterpret_cast<const f32x4v*>(a.ws) + q, total / 4, splits, g);
+  red[g][o] = s;
+  __syncthreads();
+  if (g == 0 && q * 4 < total) {
+    f32x4v r = red[0][o];
+#pragma unroll
+    for (int i = 1; i < RZG; ++i) r += red[i][o];
+    const long idx = q * 4;
+    const int m = idx / a.N, n = idx % a.N;
+    GemmArgs b = a;
+    b.ws = nullptr;  // store4 writes C (alpha / beta / bias / epilogue) instead of a slab
+    store4(b, 0, m, n, make_float4(r.x, r.y, r.z, r.w));
   }
-  const float4 r = make_float4((s[0].x + s[1].x) + (s[2].x + s[3].x), (s[0].y + s[1].y) + (s[2].y + s[3].y),
-                               (s[0].z + s[1].z) + (s[2].z + s[3].z), (s[0].w + s[1].w) + (s[2].w + s[3].w));
-  const int m = idx / a.N, n = idx % a.N;
-  GemmArgs b = a;
-  b.ws = nullptr;  // store4 writes C (with alpha / beta / bias / epilogue) instead of a slab
-  store4(b, 0, m, n, r);
 }
 
 // column sums, stage 1: part[s][n] = sum of X(row, n) over rows [s*rows_per, (s+1)*rows_per).
@@ -704,16 +774,26 @@ MRG_API int mrg_gemm_force_tile(int tile) {
   return 0;
 }
 
+// split-K slabs [splits][M][N] (splits > 1), then room for the fused row sums of A
+// ([splits][M]) or, on the unfused path, the column-sum kernels' partials
 MRG_API size_t mrg_gemm_workspace_bytes(int M, int N, int splits) {
-  return splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;
+  const size_t slabs = splits > 1 ? (size_t)splits * M * N : 0;
+  const size_t rs = (size_t)(splits > 1 ? splits : 1) * M;
+  const size_t cs = (size_t)512 * M;  // colsum_splits(K) <= 512 partial rows of M
+  return (slabs + (rs > cs ? rs : cs)) * sizeof(float);
 }
 
-MRG_API int mrg_gemm_f32(int M, int N, int K, float alpha,
-                         const float* A, int transA, long lda, long lda_hi, int a_rdiv,
-                         const float* B, int transB, long ldb, long ldb_hi, int b_rdiv,
-                         float beta, float* C, long ldc, const float* bias, int epilogue,
-                         const float* aux, long ldaux, float* workspace, int splits,
-                         hipStream_t stream) {
+MRG_API int mrg_colsum_f32(int rows, int N, const float* X, long ld, long ld_hi, int rdiv,
+                           float beta, float* out, float* out2, float* workspace,
+                           hipStream_t stream);
+
+MRG_API int mrg_gemm_f32_ex(int M, int N, int K, float alpha,
+                            const float* A, int transA, long lda, long lda_hi, int a_rdiv,
+                            const float* B, int transB, long ldb, long ldb_hi, int b_rdiv,
+                            float beta, float* C, long ldc, const float* bias, int epilogue,
+                            const float* aux, long ldaux, float* workspace, int splits,
+                            float* asum_out, float* asum_out2, float asum_beta,
+                            hipStream_t stream) {
   MRG_REQUIRE(M >= 0 && N >= 0 && K >= 0, "mrg_gemm_f32: negative size");
   MRG_REQUIRE(epilogue >= 0 && epilogue <= 2, "mrg_gemm_f32: bad epilogue %d", epilogue);
   MRG_REQUIRE(epilogue != 2 || aux, "mrg_gemm_f32: epilogue 2 needs aux");
@@ -733,6 +813,10 @@ MRG_API int mrg_gemm_f32(int M, int N, int K, float alpha,
   if (splits < 1) splits = 1;
   a.kchunk = kc;
   a.ws = splits > 1 ? workspace : nullptr;
+  a.asum = nullptr; a.asum_out = asum_out; a.asum_out2 = asum_out2; a.asum_beta = asum_beta;
+  // fused bias-gradient row sums: x6 path with A = (memory rows k, contiguous along m)
+  const bool fuse_asum = asum_out && g_gemm_mode == 1 && transA && workspace;
+  if (fuse_asum) a.asum = workspace + (splits > 1 ? (long)splits * M * N : 0);
   // vector (float4) global loads need 16-B aligned rows along the contiguous index
   auto aligned = [](const float* p, const RowMap& m) {
     return ((uintptr_t)p & 15) == 0 && (m.ld_lo & 3) == 0 && (m.rdiv <= 0 || (m.ld_hi & 3) == 0);
@@ -761,15 +845,43 @@ MRG_API int mrg_gemm_f32(int M, int N, int K, float alpha,
   if (g_tile_override >= 0 && g_tile_override <= 2) tile = g_tile_override;
   if (launch_gemm(a, tile, bk, transA, transB, va, vb, splits, stream)) return 2;
   if (check_launch("gemm_f32_kernel")) return 1;
+  bool asum_done = false;
   if (splits > 1) {
     long total = (long)M * N;
-    if (a.vec && (N & 3) == 0)
-      splitk_reduce4_kernel<<<(unsigned)((total / 4 + 255) / 256), 256, 0, stream>>>(a, splits);
-    else
+    if (a.vec && (N & 3) == 0) {
+      const long cb = (total / 4 + RPB - 1) / RPB, ab = a.asum ? (M + RPB - 1) / RPB : 0;
+      splitk_reduce4_kernel<<<(unsigned)(cb + ab), 256, 0, stream>>>(a, splits);
+      asum_done = a.asum != nullptr;
+    } else {
       splitk_reduce_kernel<<<(unsigned)((total + 255) / 256), 256, 0, stream>>>(a, splits);
+    }
     if (check_launch("splitk_reduce_kernel")) return 1;
   }
+  if (a.asum && !asum_done) {
+    asum_reduce_kernel<<<(unsigned)((M + RPB - 1) / RPB), 256, 0, stream>>>(a, splits);
+    if (check_launch("asum_reduce_kernel")) return 1;
+  } else if (asum_out && !a.asum) {
+    // not fusable here (exact-f32 mode or A not k-major): the two-pass column-sum kernels
+    MRG_REQUIRE(workspace, "mrg_gemm_f32_ex: row sums need the workspace");
+    float* cws = workspace + (splits > 1 ? (long)splits * M * N : 0);
+    if (transA) {
+      if (int e = mrg_colsum_f32(K, M, A, lda, lda_hi, a_rdiv, asum_beta, asum_out, asum_out2, cws, stream))
+        return e;
+    } else {
+      MRG_REQUIRE(false, "mrg_gemm_f32_ex: row sums need transA = 1");
+    }
+  }
   return 0;
+}
+
+MRG_API int mrg_gemm_f32(int M, int N, int K, float alpha,
+                         const float* A, int transA, long lda, long lda_hi, int a_rdiv,
+                         const float* B, int transB, long ldb, long ldb_hi, int b_rdiv,
+                         float beta, float* C, long ldc, const float* bias, int epilogue,
+                         const float* aux, long ldaux, float* workspace, int splits,
+                         hipStream_t stream) {
+  return mrg_gemm_f32_ex(M, N, K, alpha, A, transA, lda, lda_hi, a_rdiv, B, transB, ldb, ldb_hi, b_rdiv, beta, C,
+                         ldc, bias, epilogue, aux, ldaux, workspace, splits, nullptr, nullptr, 0.0f, stream);
 }
 
 static int colsum_splits(int rows) {

@@ -35,12 +35,15 @@ _PROBES = {}
 
 
 class _probe:
-    """Bracket one library launch with timing events when ``name`` is being probed."""
-    __slots__ = ("name", "e0")
+    """Bracket one library launch with timing events when ``name`` is being probed.
 
-    def __init__(self, name):
+    ``work``: the launch's algorithmic FLOPs (or bytes), kept with its time for rooflines."""
+    __slots__ = ("name", "e0", "work")
+
+    def __init__(self, name, work=0.0):
         self.name = name
         self.e0 = None
+        self.work = work
 
     def __enter__(self):
         if self.name in _PROBE_ON:
@@ -52,7 +55,7 @@ class _probe:
         if self.e0 is not None:
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record()
-            _PROBES.setdefault(self.name, []).append((self.e0, e1))
+            _PROBES.setdefault(self.name, []).append((self.e0, e1, self.work))
         return False
 
 
@@ -62,11 +65,14 @@ def probe_start(*names):
     _PROBES.clear()
 
 
-def probe_stop():
-    """Stop probing; returns {name: [ms per launch]} (synchronises)."""
+def probe_stop(with_work=False):
+    """Stop probing; returns {name: [ms per launch]} or, with_work, {name: [(ms, work)]} (synchronises)."""
     _PROBE_ON.clear()
     torch.cuda.synchronize()
-    out = {k: [a.elapsed_time(b) for a, b in v] for k, v in _PROBES.items()}
+    if with_work:
+        out = {k: [(a.elapsed_time(b), w) for a, b, w in v] for k, v in _PROBES.items()}
+    else:
+        out = {k: [a.elapsed_time(b) for a, b, _ in v] for k, v in _PROBES.items()}
     _PROBES.clear()
     return out
 
@@ -112,17 +118,22 @@ def _gbuf(p: torch.Tensor) -> Optional[torch.Tensor]:
 
 
 def gemm(M, N, K, A, transA, lda, B, transB, ldb, C, ldc, *, alpha=1.0, beta=0.0, bias=None,
-         epi=0, aux=None, ldaux=0, a_hi=0, a_div=0, b_hi=0, b_div=0, splits=1, device=None):
-    """C = epi(alpha op(A) op(B) + beta C + bias); A/B/C/bias/aux are ctypes pointers."""
+         epi=0, aux=None, ldaux=0, a_hi=0, a_div=0, b_hi=0, b_div=0, splits=1, device=None,
+         asum_out=None, asum_out2=None, asum_beta=1.0):
+    """C = epi(alpha op(A) op(B) + beta C + bias); A/B/C/bias/aux are ctypes pointers.
+
+    asum_out (optional ctypes pointer): += row sums of op(A) over k, i.e. the bias gradient of a
+    weight-gradient GEMM dY^T X, fused into the GEMM (mrg_gemm_f32_ex)."""
     if M == 0 or N == 0:
         return
     lib = _lib.load()
     ws = None
-    if splits > 1:
+    if splits > 1 or asum_out is not None:
         ws = _ws(lib.mrg_gemm_workspace_bytes(M, N, splits), device)
-    with _probe("gemm"):
-        rc = lib.mrg_gemm_f32(M, N, K, alpha, A, transA, lda, a_hi, a_div, B, transB, ldb, b_hi, b_div,
-                              beta, C, ldc, bias, epi, aux, ldaux, _ptr(ws), splits, _stream())
+    with _probe("gemm", 2.0 * M * N * K):
+        rc = lib.mrg_gemm_f32_ex(M, N, K, alpha, A, transA, lda, a_hi, a_div, B, transB, ldb, b_hi, b_div,
+                                 beta, C, ldc, bias, epi, aux, ldaux, _ptr(ws), splits, asum_out, asum_out2,
+                                 asum_beta, _stream())
     _lib.check(rc, "gemm")
 
 
@@ -150,10 +161,16 @@ def colsum(rows, N, X, ld, out, *, out2=None, beta=1.0, ld_hi=0, rdiv=0, device=
                "colsum")
 
 
-def _wgrad(dY, ldy, X, ldx, rows, Nout, Nin, gw, device, *, dy_hi=0, dy_div=0, x_hi=0, x_div=0):
-    """gw[Nout, Nin] += sum_rows dY[row, :]^T X[row, :]."""
+def _wgrad(dY, ldy, X, ldx, rows, Nout, Nin, gw, device, *, dy_hi=0, dy_div=0, x_hi=0, x_div=0, gb=None,
+           gb2=None):
+    """gw[Nout, Nin] += sum_rows dY[row, :]^T X[row, :]; gb (and gb2) += sum_rows dY[row, :] (fused)."""
+    if gw is None:
+        if gb is not None:
+            colsum(rows, Nout, dY, ldy, _ptr(gb), out2=_ptr(gb2), ld_hi=dy_hi, rdiv=dy_div, device=device)
+        return
     gemm(Nout, Nin, rows, dY, 1, ldy, X, 0, ldx, _ptr(gw), Nin, beta=1.0, a_hi=dy_hi, a_div=dy_div,
-         b_hi=x_hi, b_div=x_div, splits=wgrad_splits(Nout, Nin, rows), device=device)
+         b_hi=x_hi, b_div=x_div, splits=wgrad_splits(Nout, Nin, rows), device=device,
+         asum_out=_ptr(gb), asum_out2=_ptr(gb2))
 
 
 # ------------------------------------------------------------------ Linear
@@ -177,12 +194,7 @@ class _LinearFn(Function):
         dy2 = dy.reshape(-1, N).contiguous()
         M = dy2.shape[0]
         dev = dy.device
-        gw = _gbuf(w)
-        if gw is not None:
-            _wgrad(_ptr(dy2), N, _ptr(x2), In, M, N, In, gw, dev)
-        gb = _gbuf(b)
-        if gb is not None:
-            colsum(M, N, _ptr(dy2), N, _ptr(gb), device=dev)
+        _wgrad(_ptr(dy2), N, _ptr(x2), In, M, N, In, _gbuf(w), dev, gb=_gbuf(b))
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(M, In, device=dev, dtype=torch.float32)
@@ -224,18 +236,8 @@ class _FFNFn(Function):
         dh = torch.empty(M, Hb, device=dev, dtype=torch.float32)
         gemm(M, Hb, N, _ptr(dz2), 0, N, _ptr(w2), 0, Hb, _ptr(dh), Hb, epi=2, aux=_ptr(h), ldaux=Hb,
              device=dev)
-        g = _gbuf(w2)
-        if g is not None:
-            _wgrad(_ptr(dz2), N, _ptr(h), Hb, M, N, Hb, g, dev)
-        g = _gbuf(b2)
-        if g is not None:
-            colsum(M, N, _ptr(dz2), N, _ptr(g), device=dev)
-        g = _gbuf(w1)
-        if g is not None:
-            _wgrad(_ptr(dh), Hb, _ptr(x2), In, M, Hb, In, g, dev)
-        g = _gbuf(b1)
-        if g is not None:
-            colsum(M, Hb, _ptr(dh), Hb, _ptr(g), device=dev)
+        _wgrad(_ptr(dz2), N, _ptr(h), Hb, M, N, Hb, _gbuf(w2), dev, gb=_gbuf(b2))
+        _wgrad(_ptr(dh), Hb, _ptr(x2), In, M, Hb, In, _gbuf(w1), dev, gb=_gbuf(b1))
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(M, In, device=dev, dtype=torch.float32)
@@ -349,7 +351,7 @@ class _LSTMFn(Function):
         def arr(ctype, vals):
             return (ctype * nprob)(*vals)
         VP = ctypes.c_void_p
-        pr = _probe("lstm_fwd").__enter__()
+        pr = _probe("lstm_fwd", 8.0 * H * H * B * T * nprob).__enter__()  # recurrent h W_hh^T FLOPs
         rc = lib.mrg_lstm_fwd(
             nprob, B, T, H,
             arr(VP, [_ptr(g) for g in gxs]), arr(ctypes.c_long, [T * 4 * H] * nprob),
@@ -423,7 +425,7 @@ class _LSTMFn(Function):
         def arr(ctype, vals):
             return (ctype * nprob)(*vals)
         VP = ctypes.c_void_p
-        pr = _probe("lstm_bwd").__enter__()
+        pr = _probe("lstm_bwd", 8.0 * H * H * B * T * nprob).__enter__()  # dG W_hh FLOPs
         rc = lib.mrg_lstm_bwd(
             nprob, B, T, H,
             arr(VP, [_ptr(p[2]) for p in per]), arr(VP, [_ptr(p[5]) for p in per]),
@@ -457,14 +459,10 @@ class _LSTMFn(Function):
                 t0 = T - 1 if reverse[i] else 0
                 gemm(4 * H, H, B, _ptr(g, t0 * 4 * H), 1, T * 4 * H, _ptr(h0), 0, H, _ptr(gw), H,
                      beta=1.0, device=dev)
-            gw = _gbuf(w_ih)
-            if gw is not None:
-                _wgrad(_ptr(g), 4 * H, _ptr(x), In, rows, 4 * H, In, gw, dev)
             gbi, gbh = _gbuf(b_ih), _gbuf(b_hh)
-            if gbi is not None or gbh is not None:
-                first = gbi if gbi is not None else gbh
-                second = gbh if gbi is not None else None
-                colsum(rows, 4 * H, _ptr(g), 4 * H, _ptr(first), out2=_ptr(second), device=dev)
+            first = gbi if gbi is not None else gbh
+            second = gbh if gbi is not None else None
+            _wgrad(_ptr(g), 4 * H, _ptr(x), In, rows, 4 * H, In, _gbuf(w_ih), dev, gb=first, gb2=second)
             dx = None
             if need[1 + 7 * i]:
                 if ctx.shared_x[i] and dx_first is not None:
@@ -511,6 +509,17 @@ def lstm_bidirectional_layer(x, fw, bw, h0=None, c0=None, force_bs=0):
 
 
 # ------------------------------------------------------------------ multi-head attention
+def visible_pairs(Tq, Tk, causal):
+    """(query, key) pairs the block-causal rule admits per (sample, head) (gen_attention_mask rules)."""
+    if not causal:
+        return Tq * Tk
+    if Tk >= Tq:
+        r = Tk // Tq
+        return sum(min((i + 1) * r, Tk) for i in range(Tq))
+    r = Tq // Tk
+    return sum(min(i // r + 1, Tk) for i in range(Tq))
+
+
 class _MHAFn(Function):
     @staticmethod
     def forward(ctx, spec, q_in, kv_in, in_w, in_b, out_w, out_b, qpad, kpad):
@@ -531,7 +540,7 @@ class _MHAFn(Function):
         lse = torch.empty(B, heads, Tq, device=dev, dtype=torch.float32)
         scale = 1.0 / math.sqrt(D)
         lib = _lib.load()
-        with _probe("attn_fwd"):
+        with _probe("attn_fwd", 4.0 * D * B * heads * visible_pairs(Tq, Tk, causal)):
             rc = lib.mrg_attention_fwd(B, heads, Tq, Tk, D, _ptr(Q), Tq * E, E, _ptr(KV), Tk * 2 * E,
                                          2 * E, _ptr(KV, E), Tk * 2 * E, 2 * E, _ptr(O), Tq * E, E,
                                        _ptr(lse), _ptr(qpad), _ptr(kpad), int(causal), scale,
@@ -555,30 +564,22 @@ class _MHAFn(Function):
         do2 = dout.contiguous()
         dO = torch.empty(B, Tq, E, device=dev, dtype=torch.float32)
         gemm(B * Tq, E, E, _ptr(do2), 0, E, _ptr(out_w), 0, E, _ptr(dO), E, device=dev)
-        g = _gbuf(out_w)
-        if g is not None:
-            _wgrad(_ptr(do2), E, _ptr(O), E, B * Tq, E, E, g, dev)
-        g = _gbuf(out_b)
-        if g is not None:
-            colsum(B * Tq, E, _ptr(do2), E, _ptr(g), device=dev)
+        _wgrad(_ptr(do2), E, _ptr(O), E, B * Tq, E, E, _gbuf(out_w), dev, gb=_gbuf(out_b))
         dQ = torch.empty(B, Tq, E, device=dev, dtype=torch.float32)
         dKV = torch.empty(B, Tk, 2 * E, device=dev, dtype=torch.float32)
         ws = _ws(lib.mrg_attention_bwd_workspace_bytes(B, heads, Tq), dev)
-        with _probe("attn_bwd"):
+        with _probe("attn_bwd", 10.0 * D * B * heads * visible_pairs(Tq, Tk, causal)):
             rc = lib.mrg_attention_bwd(
             B, heads, Tq, Tk, D, _ptr(Q), Tq * E, E, _ptr(KV), Tk * 2 * E, 2 * E, _ptr(KV, E), Tk * 2 * E,
             2 * E, _ptr(O), Tq * E, E, _ptr(lse), _ptr(qpad), _ptr(kpad), int(causal), scale,
             _ptr(dO), Tq * E, E, _ptr(dQ), Tq * E, E, _ptr(dKV), Tk * 2 * E, 2 * E, _ptr(dKV, E),
             Tk * 2 * E, 2 * E, _ptr(ws), _stream())
         _lib.check(rc, "attention bwd")
-        gw = _gbuf(in_w)
-        if gw is not None:
-            _wgrad(_ptr(dQ), E, _ptr(q2), E, B * Tq, E, E, gw[:E], dev)
-            _wgrad(_ptr(dKV), 2 * E, _ptr(kv2), E, B * Tk, 2 * E, E, gw[E:], dev)
-        gb = _gbuf(in_b)
-        if gb is not None:
-            colsum(B * Tq, E, _ptr(dQ), E, _ptr(gb), device=dev)
-            colsum(B * Tk, 2 * E, _ptr(dKV), 2 * E, _ptr(gb, E), device=dev)
+        gw, gb = _gbuf(in_w), _gbuf(in_b)
+        _wgrad(_ptr(dQ), E, _ptr(q2), E, B * Tq, E, E, None if gw is None else gw[:E], dev,
+               gb=None if gb is None else gb[:E])
+        _wgrad(_ptr(dKV), 2 * E, _ptr(kv2), E, B * Tk, 2 * E, E, None if gw is None else gw[E:], dev,
+               gb=None if gb is None else gb[E:])
         dq_in = dkv_in = None
         if ctx.needs_input_grad[1]:
             dq_in = torch.empty(B, Tq, E, device=dev, dtype=torch.float32)

@@ -23,6 +23,9 @@ import torch
 import torch.nn.functional as F
 
 PADDING_VALUE = -100.0
+# False (default): the explicit per-step restatement below (parity checks).  True: the fused ATen
+# LSTM op the reference's nn.LSTM runs on CPU (bench.py times the CPU baseline with it).
+ATEN_LSTM = False
 Tensor = torch.Tensor
 SD = Dict[str, Tensor]
 
@@ -48,6 +51,14 @@ def lstm_layer(x: Tensor, w_ih: Tensor, w_hh: Tensor, b_ih: Tensor, b_hh: Tensor
     """
     B, T, _ = x.shape
     H = w_hh.shape[1]
+    if ATEN_LSTM and T > 0:
+        # the fused ATen LSTM op nn.LSTM itself dispatches to on CPU (oneDNN); same math as the
+        # loop below, used only to time the reference's own CPU path (bench.py cpu_baseline)
+        h = x.new_zeros(1, B, H) if h0 is None else h0.unsqueeze(0)
+        c = x.new_zeros(1, B, H) if c0 is None else c0.unsqueeze(0)
+        xi = x.flip(1) if reverse else x
+        y, hT, cT = torch.lstm(xi, (h, c), [w_ih, w_hh, b_ih, b_hh], True, 1, 0.0, True, False, True)
+        return (y.flip(1) if reverse else y), hT[0], cT[0]
     gx = F.linear(x, w_ih, b_ih)
     h = x.new_zeros(B, H) if h0 is None else h0
     c = x.new_zeros(B, H) if c0 is None else c0

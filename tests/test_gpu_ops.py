@@ -33,8 +33,19 @@ def _param(t):
     return torch.nn.Parameter(t.clone().to(DEV))
 
 
+@pytest.fixture(params=[1, 0], ids=["x6", "exact_f32"])
+def gemm_mode(request):
+    """Both GEMM arithmetics: the x6 bf16 split (default) and the exact f32 MFMA."""
+    from multimodalreactiongeneration_amd import _lib as L
+    lib = L.load()
+    old = lib.mrg_gemm_get_mode()
+    L.check(lib.mrg_gemm_set_mode(request.param), "mode")
+    yield request.param
+    L.check(lib.mrg_gemm_set_mode(old), "mode")
+
+
 @pytest.mark.parametrize("M,N,K", [(19200, 1024, 256), (600, 6, 64), (37, 45, 53), (2048, 256, 512)])
-def test_linear_fwd_bwd_vs_torch_fp32(M, N, K):
+def test_linear_fwd_bwd_vs_torch_fp32(M, N, K, gemm_mode):
     from multimodalreactiongeneration_amd import functional as Fn
     g = torch.Generator().manual_seed(M + N)
     x = torch.randn(M, K, generator=g)
@@ -54,6 +65,43 @@ def test_linear_fwd_bwd_vs_torch_fp32(M, N, K):
     assert rel_err(xd.grad, xr.grad) < TOL
     assert rel_err(wd.grad, wr.grad) < TOL
     assert rel_err(bd.grad, br.grad) < TOL
+
+
+@pytest.mark.parametrize("rows,N,In,splits,time_shift", [
+    (19200, 1024, 256, 32, False), (19200, 256, 256, 120, False), (1000, 70, 45, 1, False),
+    (777, 130, 33, 5, False), (64 * 299, 1024, 256, 16, True)])
+def test_weight_grad_with_fused_bias_sums(rows, N, In, splits, time_shift, gemm_mode):
+    """gw += dY^T X and gb (+ gb2) += colsum(dY) in one mrg_gemm_f32_ex call, incl. a RowMap'd
+    (time-shifted, [:, 1:] of [64, 300, F]) operand pair as the LSTM's dW_hh uses."""
+    from multimodalreactiongeneration_amd import functional as Fn
+    g = torch.Generator().manual_seed(rows + N)
+    if time_shift:
+        T = 300
+        dYf = torch.randn(64, T, N, generator=g)
+        Xf = torch.randn(64, T, In, generator=g)
+        dY, X = dYf[:, 1:].reshape(-1, N), Xf[:, :-1].reshape(-1, In)
+        dYd, Xd = dYf.to(DEV), Xf.to(DEV)
+        kw = dict(dy_hi=T * N, dy_div=T - 1, x_hi=T * In, x_div=T - 1)
+        dy_ptr, x_ptr = Fn._ptr(dYd, N), Fn._ptr(Xd)
+    else:
+        dY, X = torch.randn(rows, N, generator=g), torch.randn(rows, In, generator=g)
+        dYd, Xd = dY.to(DEV), X.to(DEV)
+        kw = {}
+        dy_ptr, x_ptr = Fn._ptr(dYd), Fn._ptr(Xd)
+    gw0, gb0 = torch.randn(N, In, generator=g), torch.randn(N, generator=g)
+    gw, gb, gb2 = gw0.to(DEV), gb0.to(DEV), gb0.to(DEV) * 2
+    orig = Fn.wgrad_splits
+    Fn.wgrad_splits = lambda *a: splits
+    try:
+        Fn._wgrad(dy_ptr, N, x_ptr, In, dY.shape[0], N, In, gw, torch.device(DEV), gb=gb, gb2=gb2, **kw)
+    finally:
+        Fn.wgrad_splits = orig
+    torch.cuda.synchronize()
+    ref_w = gw0.double() + dY.double().t() @ X.double()
+    ref_b = gb0.double() + dY.double().sum(0)
+    assert rel_err(gw, ref_w) < TOL
+    assert rel_err(gb, ref_b) < TOL
+    assert rel_err(gb2, gb0.double() * 2 + dY.double().sum(0)) < TOL
 
 
 def test_ffn_relu_fused_vs_torch():

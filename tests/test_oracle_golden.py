@@ -183,3 +183,26 @@ def test_simple_lstm_train_step():
         assert rel_err(O.simple_lstm_forward(sd, cfg["model"], a, m), d["y"]) < TOL
     loss, y, grads, after = O.run_train_step(O.simple_lstm_training_loss, sd, cfg["optim"], cfg["model"], a, m, t)
     _check_train(d, loss, y, grads, after, check_y=False)
+
+
+@pytest.mark.parametrize("reverse", [False, True])
+def test_aten_lstm_timing_path_equals_restatement(reverse):
+    """The fused ATen LSTM (what bench.py's CPU baseline times) == the oracle's per-step loop."""
+    g = torch.Generator().manual_seed(3)
+    B, T, In, H = 3, 17, 12, 8
+    x = torch.randn(B, T, In, generator=g, requires_grad=True)
+    ws = [torch.randn(4 * H, In, generator=g) * 0.3, torch.randn(4 * H, H, generator=g) * 0.3,
+          torch.randn(4 * H, generator=g) * 0.1, torch.randn(4 * H, generator=g) * 0.1]
+    h0, c0 = torch.randn(B, H, generator=g), torch.randn(B, H, generator=g)
+    outs = []
+    for aten in (False, True):
+        O.ATEN_LSTM = aten
+        try:
+            xx = x.detach().clone().requires_grad_(True)
+            y, hT, cT = O.lstm_layer(xx, *ws, h0, c0, reverse=reverse)
+            (y.square().sum() + hT.sum() + cT.sum()).backward()
+            outs.append((y.detach(), hT.detach(), cT.detach(), xx.grad))
+        finally:
+            O.ATEN_LSTM = False
+    for a, b in zip(*outs):
+        assert rel_err(a, b) < 1e-5

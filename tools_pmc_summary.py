@@ -56,7 +56,7 @@ def fam_total(prefix):
 
 doc = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) over "
                  "`bench.py --graph 0 --cpu-baseline 0 --steps 1 --warmup 1`; FETCH_SIZE x2 (gfx950 correction)",
-       "families": {p: fam_total(p) for p in ("lstm_fwd_kernel", "lstm_bwd_kernel", "gemm_f32_kernel",
+       "families": {p: fam_total(p) for p in ("lstm_fwd_kernel", "lstm_bwd_kernel", "gemm_x6_kernel", "gemm_f32_kernel", "splitk_reduce",
                                               "attn_fwd_kernel", "attn_bwd", "resln", "adamw_kernel")},
        "kernels": summary}
 txt = json.dumps(doc, indent=1)
