@@ -35,7 +35,8 @@ int mrg_device_cu_count(int device, int* out);
 
 /* ---------------------------------------------------------------- GEMM
  * C = epi(alpha * op(A) op(B) + beta * C + bias[n]); epi 0 none, 1 relu,
- * 2 multiply by (aux[m, n] > 0) (relu backward).  split-K > 1 writes fp32
+ * 2 multiply by (aux[m, n] > 0) (relu backward), 3 add aux[m, n] (the residual
+ * branch of LN(f(x) + x): dx = g W + g without a separate add).  split-K > 1 writes fp32
  * slabs to `workspace` and reduces them in a fixed order (deterministic).
  * Replaces nn.Linear / addmm (mixer_block.py:63-74, multi_modal_metaformer.py:
  * 433-435,474,504, lstm_with_sample.py:92-130) and the x W_ih^T / weight-grad

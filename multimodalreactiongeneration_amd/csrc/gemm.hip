@@ -34,7 +34,7 @@ struct GemmArgs {
   float* C;
   long ldc;
   const float* bias;
-  int epi;  // 0 none, 1 relu, 2 multiply by (aux > 0)
+  int epi;  // 0 none, 1 relu, 2 multiply by (aux > 0), 3 add aux (residual gradient)
   const float* aux;
   long ldaux;
   float* ws;  // split-K slabs [splits][M][N] (nullptr when splits == 1)
@@ -59,6 +59,7 @@ __device__ __forceinline__ float apply_epi(const GemmArgs& a, float v, int m, in
   if (a.bias) v += a.bias[n];
   if (a.epi == 1) v = fmaxf(v, 0.0f);
   else if (a.epi == 2) v = (a.aux[(long)m * a.ldaux + n] > 0.0f) ? v : 0.0f;
+  else if (a.epi == 3) v += a.aux[(long)m * a.ldaux + n];
   return v;
 }
 
@@ -89,6 +90,9 @@ __device__ __forceinline__ void store4(const GemmArgs& a, int z, int m, int n, f
       const float4 x = *reinterpret_cast<const float4*>(a.aux + (long)m * a.ldaux + n);
       o.x = x.x > 0.0f ? o.x : 0.0f; o.y = x.y > 0.0f ? o.y : 0.0f;
       o.z = x.z > 0.0f ? o.z : 0.0f; o.w = x.w > 0.0f ? o.w : 0.0f;
+    } else if (a.epi == 3) {
+      const float4 x = *reinterpret_cast<const float4*>(a.aux + (long)m * a.ldaux + n);
+      o.x += x.x; o.y += x.y; o.z += x.z; o.w += x.w;
     }
     *reinterpret_cast<float4*>(pc) = o;
     return;
@@ -795,8 +799,8 @@ MRG_API int mrg_gemm_f32_ex(int M, int N, int K, float alpha,
                             float* asum_out, float* asum_out2, float asum_beta,
                             hipStream_t stream) {
   MRG_REQUIRE(M >= 0 && N >= 0 && K >= 0, "mrg_gemm_f32: negative size");
-  MRG_REQUIRE(epilogue >= 0 && epilogue <= 2, "mrg_gemm_f32: bad epilogue %d", epilogue);
-  MRG_REQUIRE(epilogue != 2 || aux, "mrg_gemm_f32: epilogue 2 needs aux");
+  MRG_REQUIRE(epilogue >= 0 && epilogue <= 3, "mrg_gemm_f32: bad epilogue %d", epilogue);
+  MRG_REQUIRE(epilogue < 2 || aux, "mrg_gemm_f32: epilogue %d needs aux", epilogue);
   if (M == 0 || N == 0) return 0;
   if (splits < 1) splits = 1;
   MRG_REQUIRE(splits == 1 || workspace, "mrg_gemm_f32: split-K needs workspace");

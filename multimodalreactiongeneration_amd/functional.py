@@ -296,6 +296,116 @@ def residual_layernorm(y, x, gamma, beta, eps=1e-5):
     return _ResLNFn.apply(y, x, gamma, beta, eps)
 
 
+def _resln_fwd(a2, b2, gamma, beta, eps):
+    """u = LN(a + b) over [rows, E] (both contiguous); returns (u, mean, rstd)."""
+    rows, E = a2.shape
+    dev = a2.device
+    y = torch.empty_like(a2)
+    mean = torch.empty(rows, device=dev, dtype=torch.float32)
+    rstd = torch.empty(rows, device=dev, dtype=torch.float32)
+    _lib.check(_lib.load().mrg_residual_layernorm_fwd(rows, E, _ptr(a2), _ptr(b2), _ptr(gamma), _ptr(beta), eps,
+                                                      _ptr(y), _ptr(mean), _ptr(rstd), _stream()), "layernorm fwd")
+    return y, mean, rstd
+
+
+def _resln_bwd(dy2, a2, b2, gamma, beta, mean, rstd):
+    """g = dL/d(a + b) of u = LN(a + b); dgamma / dbeta accumulate into the parameters' grads."""
+    rows, E = a2.shape
+    dev = a2.device
+    g = torch.empty_like(a2)
+    lib = _lib.load()
+    ws = _ws(lib.mrg_residual_layernorm_bwd_workspace_bytes(rows, E), dev)
+    gg, gb = _gbuf(gamma), _gbuf(beta)
+    scratch = None
+    if gg is None or gb is None:
+        scratch = torch.empty(2, E, device=dev, dtype=torch.float32)
+    _lib.check(lib.mrg_residual_layernorm_bwd(
+        rows, E, _ptr(dy2), _ptr(a2), _ptr(b2), _ptr(gamma), _ptr(mean), _ptr(rstd), _ptr(g),
+        _ptr(gg if gg is not None else scratch[0]), _ptr(gb if gb is not None else scratch[1]),
+        1, _ptr(ws), _stream()), "layernorm bwd")
+    return g
+
+
+# ------------------------------------------------------------------ Linear / FFN + residual LayerNorm
+# LN(f(x) + x) with f's input-gradient GEMM taking the residual branch in its epilogue
+# (dx = g W + g, epilogue 3): the add autograd would run for the two uses of x disappears.
+class _LinResLNFn(Function):
+    """LN(x W^T + b + x): FeedForward(nonlinearity none, residual, LN) (mixer_block.py:63-83)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, gamma, beta, eps):
+        _lib.require_device(x)
+        E = w.shape[0]
+        x2 = x.reshape(-1, E).contiguous()
+        M = x2.shape[0]
+        z = torch.empty(M, E, device=x.device, dtype=torch.float32)
+        gemm(M, E, E, _ptr(x2), 0, E, _ptr(w), 1, E, _ptr(z), E, bias=_ptr(b), device=x.device)
+        y, mean, rstd = _resln_fwd(z, x2, gamma, beta, eps)
+        ctx.save_for_backward(x2, w, b, z, gamma, beta, mean, rstd)
+        ctx.xshape = x.shape
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, b, z, gamma, beta, mean, rstd = ctx.saved_tensors
+        M, E = x2.shape
+        dev = dy.device
+        g = _resln_bwd(dy.reshape(M, E).contiguous(), z, x2, gamma, beta, mean, rstd)
+        _wgrad(_ptr(g), E, _ptr(x2), E, M, E, E, _gbuf(w), dev, gb=_gbuf(b))
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(M, E, device=dev, dtype=torch.float32)
+            gemm(M, E, E, _ptr(g), 0, E, _ptr(w), 0, E, _ptr(dx), E, epi=3, aux=_ptr(g), ldaux=E, device=dev)
+            dx = dx.view(ctx.xshape)
+        return dx, None, None, None, None, None
+
+
+def linear_residual_layernorm(x, weight, bias, gamma, beta, eps=1e-5):
+    return _LinResLNFn.apply(x, weight, bias, gamma, beta, eps)
+
+
+class _FFNResLNFn(Function):
+    """LN(W2 relu(W1 x + b1) + b2 + x): the metaformer block FeedForward (multi_modal_metaformer.py:328)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, gamma, beta, eps):
+        _lib.require_device(x)
+        Hb, E = w1.shape
+        x2 = x.reshape(-1, E).contiguous()
+        M = x2.shape[0]
+        dev = x.device
+        h = torch.empty(M, Hb, device=dev, dtype=torch.float32)
+        gemm(M, Hb, E, _ptr(x2), 0, E, _ptr(w1), 1, E, _ptr(h), Hb, bias=_ptr(b1), epi=1, device=dev)
+        z = torch.empty(M, E, device=dev, dtype=torch.float32)
+        gemm(M, E, Hb, _ptr(h), 0, Hb, _ptr(w2), 1, Hb, _ptr(z), E, bias=_ptr(b2), device=dev)
+        y, mean, rstd = _resln_fwd(z, x2, gamma, beta, eps)
+        ctx.save_for_backward(x2, h, z, w1, b1, w2, b2, gamma, beta, mean, rstd)
+        ctx.xshape = x.shape
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, h, z, w1, b1, w2, b2, gamma, beta, mean, rstd = ctx.saved_tensors
+        Hb, E = w1.shape
+        M = x2.shape[0]
+        dev = dy.device
+        g = _resln_bwd(dy.reshape(M, E).contiguous(), z, x2, gamma, beta, mean, rstd)
+        dh = torch.empty(M, Hb, device=dev, dtype=torch.float32)
+        gemm(M, Hb, E, _ptr(g), 0, E, _ptr(w2), 0, Hb, _ptr(dh), Hb, epi=2, aux=_ptr(h), ldaux=Hb, device=dev)
+        _wgrad(_ptr(g), E, _ptr(h), Hb, M, E, Hb, _gbuf(w2), dev, gb=_gbuf(b2))
+        _wgrad(_ptr(dh), Hb, _ptr(x2), E, M, Hb, E, _gbuf(w1), dev, gb=_gbuf(b1))
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(M, E, device=dev, dtype=torch.float32)
+            gemm(M, E, Hb, _ptr(dh), 0, Hb, _ptr(w1), 0, E, _ptr(dx), E, epi=3, aux=_ptr(g), ldaux=E, device=dev)
+            dx = dx.view(ctx.xshape)
+        return dx, None, None, None, None, None, None, None
+
+
+def ffn_residual_layernorm(x, w1, b1, w2, b2, gamma, beta, eps=1e-5):
+    return _FFNResLNFn.apply(x, w1, b1, w2, b2, gamma, beta, eps)
+
+
 # ------------------------------------------------------------------ LSTM
 class _LSTMFn(Function):
     """``nprob`` same-shape single-layer LSTM directions in one persistent launch.
@@ -308,8 +418,10 @@ class _LSTMFn(Function):
 
     @staticmethod
     def forward(ctx, spec, *tensors):
-        nprob, concat, reverse, force_bs = spec
-        probs = [tensors[7 * i:7 * i + 7] for i in range(nprob)]
+        nprob, concat, reverse, force_bs, eps = spec
+        resln = eps is not None  # per problem LN(y + x) (ResidualConnection around LSTMMixer)
+        K = 9 if resln else 7
+        probs = [tensors[K * i:K * i + K] for i in range(nprob)]
         x0 = probs[0][0]
         _lib.require_device(x0)
         dev = x0.device
@@ -366,33 +478,48 @@ class _LSTMFn(Function):
             _lib.cu_count(dev.index or 0), force_bs, _stream())
         pr.__exit__()
         _lib.check(rc, "lstm fwd")
-        ctx.spec = (nprob, concat, tuple(reverse), force_bs, B, T, H)
+        ctx.spec = (nprob, concat, tuple(reverse), force_bs, B, T, H, resln)
         ctx.has_h0 = [h is not None for h in h0]
         ctx.has_c0 = [c is not None for c in c0]
         ctx.y_layout = (y_bs, y_ts)
         yout = [ycat] if concat else ys
         save = []
+        uout = []
         for i, p in enumerate(probs):
             save += [xs[i], p[1], p[2], p[3], p[4], gates[i], cs[i], h0[i], c0[i]]
+            if resln:
+                u, mean, rstd = _resln_fwd(ys[i].view(B * T, H), xs[i].view(B * T, H), p[7], p[8], eps)
+                uout.append(u.view(B, T, H))
+                save += [p[7], p[8], mean, rstd]
         save += yout
         ctx.save_for_backward(*save)
         ctx.shared_x = [any(probs[i][0] is probs[k][0] for k in range(i)) for i in range(nprob)]
-        outs = list(yout)
+        outs = list(uout if resln else yout)
         for i in range(nprob):
             outs += [hT[i], cT[i]]
         return tuple(outs)
 
     @staticmethod
     def backward(ctx, *grads):
-        nprob, concat, reverse, force_bs, B, T, H = ctx.spec
+        nprob, concat, reverse, force_bs, B, T, H, resln = ctx.spec
         saved = ctx.saved_tensors
-        per = [saved[9 * i:9 * i + 9] for i in range(nprob)]
-        yout = saved[9 * nprob:]
+        S = 13 if resln else 9
+        per = [saved[S * i:S * i + S] for i in range(nprob)]
+        yout = saved[S * nprob:]
         dev = yout[0].device
         lib = _lib.load()
         ny = 1 if concat else nprob
         gy = list(grads[:ny])
         gstate = grads[ny:]
+        res = [None] * nprob  # residual-branch gradient g_i of LN(y_i + x_i), added by the dX GEMM
+        if resln:
+            for i in range(nprob):
+                if gy[i] is None:
+                    continue
+                gamma, beta, mean, rstd = per[i][9:13]
+                res[i] = _resln_bwd(gy[i].reshape(B * T, H).contiguous(), yout[i].view(B * T, H),
+                                    per[i][0].view(B * T, H), gamma, beta, mean, rstd)
+                gy[i] = res[i].view(B, T, H)
         y_bs, y_ts = ctx.y_layout
         dy_ptr, dy_bs, dy_ts = [], [], []
         for i in range(nprob):
@@ -415,10 +542,11 @@ class _LSTMFn(Function):
         dcT = [None if gstate[2 * i + 1] is None else gstate[2 * i + 1].contiguous() for i in range(nprob)]
         dG = [torch.empty(B, T, 4 * H, device=dev, dtype=torch.float32) for _ in range(nprob)]
         need = ctx.needs_input_grad  # index 0 is spec
+        K = 9 if resln else 7
         dh0 = [torch.empty(B, H, device=dev, dtype=torch.float32)
-               if ctx.has_h0[i] and need[1 + 7 * i + 5] else None for i in range(nprob)]
+               if ctx.has_h0[i] and need[1 + K * i + 5] else None for i in range(nprob)]
         dc0 = [torch.empty(B, H, device=dev, dtype=torch.float32)
-               if ctx.has_c0[i] and need[1 + 7 * i + 6] else None for i in range(nprob)]
+               if ctx.has_c0[i] and need[1 + K * i + 6] else None for i in range(nprob)]
         xb_elems = lib.mrg_lstm_bwd_xbuf_bytes(B, H) // 8
         xbuf = torch.zeros(nprob, xb_elems, dtype=torch.int64, device=dev)
 
@@ -442,7 +570,7 @@ class _LSTMFn(Function):
         out = [None]
         dx_first = None
         for i in range(nprob):
-            x, w_ih, w_hh, b_ih, b_hh, _g, _c, h0, _c0 = per[i]
+            x, w_ih, w_hh, b_ih, b_hh, _g, _c, h0, _c0 = per[i][:9]
             In = x.shape[2]
             g = dG[i]
             rows = B * T
@@ -464,23 +592,36 @@ class _LSTMFn(Function):
             second = gbh if gbi is not None else None
             _wgrad(_ptr(g), 4 * H, _ptr(x), In, rows, 4 * H, In, _gbuf(w_ih), dev, gb=first, gb2=second)
             dx = None
-            if need[1 + 7 * i]:
+            if need[1 + K * i]:
                 if ctx.shared_x[i] and dx_first is not None:
                     gemm(rows, In, 4 * H, _ptr(g), 0, 4 * H, _ptr(w_ih), 0, In, _ptr(dx_first), In,
                          beta=1.0, device=dev)
                 else:
                     dx = torch.empty(B, T, In, device=dev, dtype=torch.float32)
-                    gemm(rows, In, 4 * H, _ptr(g), 0, 4 * H, _ptr(w_ih), 0, In, _ptr(dx), In, device=dev)
+                    if res[i] is not None:  # dx = dG W_ih + g (residual branch in the epilogue)
+                        gemm(rows, In, 4 * H, _ptr(g), 0, 4 * H, _ptr(w_ih), 0, In, _ptr(dx), In, epi=3,
+                             aux=_ptr(res[i]), ldaux=In, device=dev)
+                    else:
+                        gemm(rows, In, 4 * H, _ptr(g), 0, 4 * H, _ptr(w_ih), 0, In, _ptr(dx), In, device=dev)
                     if dx_first is None:
                         dx_first = dx
-            out += [dx, None, None, None, None, dh0[i], dc0[i]]
+            out += [dx, None, None, None, None, dh0[i], dc0[i]] + ([None, None] if resln else [])
         return tuple(out)
 
 
 def lstm_layer(x, w_ih, w_hh, b_ih, b_hh, h0=None, c0=None, reverse=False, force_bs=0):
     """One direction of one nn.LSTM layer (batch_first).  Returns (y, hT, cT)."""
-    y, hT, cT = _LSTMFn.apply((1, False, (reverse,), force_bs), x, w_ih, w_hh, b_ih, b_hh, h0, c0)
+    y, hT, cT = _LSTMFn.apply((1, False, (reverse,), force_bs, None), x, w_ih, w_hh, b_ih, b_hh, h0, c0)
     return y, hT, cT
+
+
+def lstm_residual_layernorm(x, w_ih, w_hh, b_ih, b_hh, gamma, beta, eps=1e-5, h0=None, c0=None,
+                            force_bs=0):
+    """LN(LSTM(x) + x) for one unidirectional layer (ResidualConnection(LSTMMixer), mixer_block.py:
+    479-507); the LSTM's dX GEMM takes the residual gradient in its epilogue.  Returns (u, hT, cT)."""
+    u, hT, cT = _LSTMFn.apply((1, False, (False,), force_bs, float(eps)), x, w_ih, w_hh, b_ih, b_hh, h0, c0,
+                              gamma, beta)
+    return u, hT, cT
 
 
 def lstm_layers_batched(problems: Sequence[Sequence], force_bs=0):
@@ -489,10 +630,17 @@ def lstm_layers_batched(problems: Sequence[Sequence], force_bs=0):
     problems: [(x, w_ih, w_hh, b_ih, b_hh)] -> [y_i]; zero initial state.
     """
     flat = []
-    for x, w_ih, w_hh, b_ih, b_hh in problems:
+    eps = None
+    for p in problems:
+        x, w_ih, w_hh, b_ih, b_hh = p[:5]
         flat += [x, w_ih, w_hh, b_ih, b_hh, None, None]
+        if len(p) > 5:  # (.., gamma, beta, eps): LN(LSTM(x) + x) per problem
+            flat += [p[5], p[6]]
+            eps = float(p[7])
+    if eps is not None and any(len(p) <= 5 for p in problems):
+        raise ValueError("lstm_layers_batched: residual LayerNorm must be given for every problem or none")
     n = len(problems)
-    outs = _LSTMFn.apply((n, False, (False,) * n, force_bs), *flat)
+    outs = _LSTMFn.apply((n, False, (False,) * n, force_bs, eps), *flat)
     return list(outs[:n])
 
 
@@ -503,7 +651,7 @@ def lstm_bidirectional_layer(x, fw, bw, h0=None, c0=None, force_bs=0):
         h0f, h0b = h0[0], h0[1]
     if c0 is not None:
         c0f, c0b = c0[0], c0[1]
-    outs = _LSTMFn.apply((2, True, (False, True), force_bs), x, *fw, h0f, c0f, x, *bw, h0b, c0b)
+    outs = _LSTMFn.apply((2, True, (False, True), force_bs, None), x, *fw, h0f, c0f, x, *bw, h0b, c0b)
     y, hTf, cTf, hTb, cTb = outs
     return y, torch.stack([hTf, hTb]), torch.stack([cTf, cTb])
 
@@ -522,8 +670,8 @@ def visible_pairs(Tq, Tk, causal):
 
 class _MHAFn(Function):
     @staticmethod
-    def forward(ctx, spec, q_in, kv_in, in_w, in_b, out_w, out_b, qpad, kpad):
-        heads, causal = spec
+    def forward(ctx, spec, q_in, kv_in, in_w, in_b, out_w, out_b, qpad, kpad, gamma=None, beta=None):
+        heads, causal, eps = spec  # eps not None: return LN(attn + q) (ResidualConnection(MHAMixer))
         _lib.require_device(q_in)
         dev = q_in.device
         B, Tq, E = q_in.shape
@@ -548,20 +696,34 @@ class _MHAFn(Function):
         _lib.check(rc, "attention fwd")
         out = torch.empty(B, Tq, E, device=dev, dtype=torch.float32)
         gemm(B * Tq, E, E, _ptr(O), 0, E, _ptr(out_w), 1, E, _ptr(out), E, bias=_ptr(out_b), device=dev)
-        ctx.save_for_backward(q2, kv2, Q, KV, O, lse, in_w, in_b, out_w, out_b, qpad, kpad)
-        ctx.spec = (heads, causal, scale)
-        return out
+        extra = []
+        res = out
+        if eps is not None:
+            u, mean, rstd = _resln_fwd(out.view(B * Tq, E), q2.view(B * Tq, E), gamma, beta, eps)
+            res = u.view(B, Tq, E)
+            extra = [out, gamma, beta, mean, rstd]
+        ctx.save_for_backward(q2, kv2, Q, KV, O, lse, in_w, in_b, out_w, out_b, qpad, kpad, *extra)
+        ctx.spec = (heads, causal, scale, eps is not None)
+        return res
 
     @staticmethod
     def backward(ctx, dout):
-        q2, kv2, Q, KV, O, lse, in_w, in_b, out_w, out_b, qpad, kpad = ctx.saved_tensors
-        heads, causal, scale = ctx.spec
+        saved = ctx.saved_tensors
+        q2, kv2, Q, KV, O, lse, in_w, in_b, out_w, out_b, qpad, kpad = saved[:12]
+        heads, causal, scale, resln = ctx.spec
         B, Tq, E = q2.shape
         Tk = kv2.shape[1]
         D = E // heads
         dev = dout.device
         lib = _lib.load()
-        do2 = dout.contiguous()
+        g = None  # residual-branch gradient of LN(attn + q), added by the dq GEMM's epilogue
+        if resln:
+            out, gamma, beta, mean, rstd = saved[12:]
+            g = _resln_bwd(dout.reshape(B * Tq, E).contiguous(), out.view(B * Tq, E), q2.view(B * Tq, E),
+                           gamma, beta, mean, rstd)
+            do2 = g.view(B, Tq, E)
+        else:
+            do2 = dout.contiguous()
         dO = torch.empty(B, Tq, E, device=dev, dtype=torch.float32)
         gemm(B * Tq, E, E, _ptr(do2), 0, E, _ptr(out_w), 0, E, _ptr(dO), E, device=dev)
         _wgrad(_ptr(do2), E, _ptr(O), E, B * Tq, E, E, _gbuf(out_w), dev, gb=_gbuf(out_b))
@@ -583,12 +745,18 @@ class _MHAFn(Function):
         dq_in = dkv_in = None
         if ctx.needs_input_grad[1]:
             dq_in = torch.empty(B, Tq, E, device=dev, dtype=torch.float32)
-            gemm(B * Tq, E, E, _ptr(dQ), 0, E, _ptr(in_w), 0, E, _ptr(dq_in), E, device=dev)
+            if g is not None:
+                gemm(B * Tq, E, E, _ptr(dQ), 0, E, _ptr(in_w), 0, E, _ptr(dq_in), E, epi=3, aux=_ptr(g), ldaux=E,
+                     device=dev)
+            else:
+                gemm(B * Tq, E, E, _ptr(dQ), 0, E, _ptr(in_w), 0, E, _ptr(dq_in), E, device=dev)
+        elif g is not None:
+            dq_in = None
         if ctx.needs_input_grad[2]:
             dkv_in = torch.empty(B, Tk, E, device=dev, dtype=torch.float32)
             gemm(B * Tk, E, 2 * E, _ptr(dKV), 0, 2 * E, _ptr(in_w, E * E), 0, E, _ptr(dkv_in), E,
                  device=dev)
-        return None, dq_in, dkv_in, None, None, None, None, None, None
+        return None, dq_in, dkv_in, None, None, None, None, None, None, None, None
 
 
 def mha(q, kv, in_proj_weight, in_proj_bias, out_weight, out_bias, heads, causal=False,
@@ -596,8 +764,18 @@ def mha(q, kv, in_proj_weight, in_proj_bias, out_weight, out_bias, heads, causal
     """nn.MultiheadAttention(batch_first, kdim=vdim=E)(q, kv, kv) with the reference mask rules."""
     if in_proj_weight.shape[0] != 3 * q.shape[-1]:
         raise ValueError("in_proj_weight must be [3E, E]")
-    return _MHAFn.apply((heads, bool(causal)), q, kv, in_proj_weight, in_proj_bias, out_weight,
+    return _MHAFn.apply((heads, bool(causal), None), q, kv, in_proj_weight, in_proj_bias, out_weight,
                         out_bias, qpad, kpad)
+
+
+def mha_residual_layernorm(q, kv, in_proj_weight, in_proj_bias, out_weight, out_bias, heads, gamma, beta,
+                           eps=1e-5, causal=False, qpad=None, kpad=None):
+    """LN(MHA(q, kv, kv) + q): ResidualConnection(MHAMixer) (mixer_block.py:567-603); the query
+    projection's input-gradient GEMM takes the residual gradient in its epilogue."""
+    if in_proj_weight.shape[0] != 3 * q.shape[-1]:
+        raise ValueError("in_proj_weight must be [3E, E]")
+    return _MHAFn.apply((heads, bool(causal), float(eps)), q, kv, in_proj_weight, in_proj_bias, out_weight,
+                        out_bias, qpad, kpad, gamma, beta)
 
 
 def padding_flags(x: torch.Tensor, padding_value: float = -100.0) -> torch.Tensor:

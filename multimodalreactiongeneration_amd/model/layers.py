@@ -92,6 +92,13 @@ class ResidualConnection(nn.Module):
         _unsupported("residual without LayerNorm")
 
     def forward(self, x, *args, **kwargs):
+        # modules that can run LN(module(x) + x) as one fused op (the residual branch's gradient is
+        # added by their input-gradient GEMM) expose fused_residual_ln; None = not eligible here
+        fused = getattr(self.module, "fused_residual_ln", None)
+        if fused is not None and self.layer_norm is not None:
+            out = fused(self.layer_norm, x, *args, **kwargs)
+            if out is not None:
+                return out
         y = self.module(x, *args, **kwargs)
         rest = None
         if isinstance(y, (tuple, list)):
@@ -125,6 +132,13 @@ class FeedForward(nn.Module):
     def forward(self, x):
         ff = self.feed_forward
         if isinstance(ff, ResidualConnection):
+            ln = ff.layer_norm
+            mods = list(ff.module.children())
+            if ln is not None and len(mods) == 1 and isinstance(mods[0], nn.Linear):
+                return Fn.linear_residual_layernorm(x, mods[0].weight, mods[0].bias, ln.weight, ln.bias, ln.eps)
+            if ln is not None and len(mods) == 3 and isinstance(mods[1], nn.ReLU):
+                return Fn.ffn_residual_layernorm(x, mods[0].weight, mods[0].bias, mods[2].weight, mods[2].bias,
+                                                 ln.weight, ln.bias, ln.eps)
             return ff.combine(run_sequential_ffn(ff.module, x), x)
         return run_sequential_ffn(ff, x)
 

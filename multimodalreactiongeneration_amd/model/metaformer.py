@@ -219,9 +219,14 @@ class MultiModalMetaformer(nn.Module):
                 # 512 resident workgroups; three would need batch tiles of 4 (longer GEMV per step)
                 for start in range(0, len(idxs), 2):
                     part = idxs[start:start + 2]
-                    ys = Fn.lstm_layers_batched([(xs[i], *chains[i][layer].lstm_params()) for i in part])
-                    for i, y in zip(part, ys):
-                        xs[i] = _lstm_block_tail(chains[i][layer], y, xs[i])
+                    # LN(LSTM(x) + x) fused per problem, then each block's FeedForward (fused too)
+                    probs = []
+                    for i in part:
+                        ln = chains[i][layer].mixer.layer_norm
+                        probs.append((xs[i], *chains[i][layer].lstm_params(), ln.weight, ln.bias, ln.eps))
+                    us = Fn.lstm_layers_batched(probs)
+                    for i, u in zip(part, us):
+                        xs[i] = chains[i][layer].feed_forward(u)
         return xs
 
     def _fast_eligible(self) -> bool:

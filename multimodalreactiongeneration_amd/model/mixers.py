@@ -14,6 +14,7 @@ from typing import Any, List, Tuple
 import torch
 from torch import nn
 
+from .. import functional as Fn
 from .layers import LSTM, MHAforSequentail, ResidualConnection, FeedForward
 
 
@@ -59,6 +60,14 @@ class LSTMMixer(Mixer):
     def forward(self, x, hn=None):
         return self.mixer(x, hn)
 
+    def fused_residual_ln(self, ln, x, hn=None):
+        """LN(LSTM(x) + x) in one op when the LSTM is one unidirectional layer from a zero state."""
+        m = self.mixer
+        if hn is not None or m.num_layers != 1 or m.bidirectional or not isinstance(x, torch.Tensor):
+            return None
+        u, hT, cT = Fn.lstm_residual_layernorm(x, *m.direction_params(0), ln.weight, ln.bias, ln.eps)
+        return u, (hT.unsqueeze(0), cT.unsqueeze(0))
+
 
 class MHAMixer(Mixer):
     """Stack of MultiheadAttention layers; returns the last output tensor (mixer_block.py:255-305)."""
@@ -74,6 +83,23 @@ class MHAMixer(Mixer):
             MHAforSequentail(input_size, num_heads, dropout, bias, add_bias_kv, add_zero_attn, kdim, vdim,
                              batch_first, nonlinearity, device=device, dtype=dtype)
             for _ in range(num_layers)])
+
+    def fused_residual_ln(self, ln, q, k, v, attn_mask=None):
+        """LN(MHA(q, k, v) + q) in one op (single layer, batch_first, k is v, reference mask)."""
+        from .masks import BlockCausalMask
+        if len(self.mixer) != 1 or k is not v:
+            return None
+        mha = self.mixer[0].mha
+        if not mha.batch_first or (mha.dropout and mha.training):
+            return None
+        if attn_mask is not None and not isinstance(attn_mask, BlockCausalMask):
+            return None
+        causal, qpad, kpad = False, None, None
+        if attn_mask is not None:
+            causal, qpad, kpad = True, attn_mask.main_pad, attn_mask.other_pad
+        return Fn.mha_residual_layernorm(q, k, mha.in_proj_weight, mha.in_proj_bias, mha.out_proj.weight,
+                                         mha.out_proj.bias, mha.num_heads, ln.weight, ln.bias, ln.eps,
+                                         causal, qpad, kpad)
 
     def forward(self, q, k, v, attn_mask=None):
         if len(self.mixer) > 1:
