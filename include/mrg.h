@@ -50,6 +50,10 @@ int mrg_gemm_set_mode(int mode);
 int mrg_gemm_get_mode(void);
 /* Tuning only: force the tile shape (0: 128x128, 1: 128x64, 2: 64x64), -1 = heuristic. */
 int mrg_gemm_force_tile(int tile);
+/* Tuning only: structural variants of the x6 kernel (0 product, 1 split + one MFMA, 2 plane-0 +
+ * six MFMAs, 3 plane-0 + one MFMA) on C = A B^T, A [M][K], B [N][K]; var != 0 gives no valid C. */
+int mrg_gemm_x6_variant(int var, int M, int N, int K, const float* A, const float* B, float* C,
+                        hipStream_t stream);
 int mrg_gemm_f32(int M, int N, int K, float alpha,
                  const float* A, int transA, long lda, long lda_hi, int a_rdiv,
                  const float* B, int transB, long ldb, long ldb_hi, int b_rdiv,

@@ -321,7 +321,7 @@ __device__ __forceinline__ void split4(float v0, float v1, float v2, float v3, u
 //   TR = 0 : memory row = x, contiguous along k: thread loads float4 (x, 4 k), 8 threads per row
 //   TR = 1 : memory row = k, contiguous along x: thread loads a 4 k x 4 x block (4 float4) and
 //            transposes it in registers (kg = tid % 8 fastest, so 32 lanes write 4 rows 4 apart)
-template <int X, int TR, bool VEC>
+template <int X, int TR, bool VEC, bool P0ONLY = false>
 struct TileX6 {
   static constexpr int NV = TR ? 4 : X * XBK / 4 / NT;
   static constexpr int ACT = TR ? (X / 4) * (XBK / 4) : NT;  // active threads
@@ -391,9 +391,13 @@ struct TileX6 {
       const float c3[4] = {r[3].x, r[3].y, r[3].z, r[3].w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
+        const int o = x6_off(4 * mg + j, kg >> 1) + 8 * (kg & 1);
+        if (P0ONLY) {
+          *reinterpret_cast<uint2*>(S0 + o) = make_uint2(pk_bf16(c0[j], c1[j]), pk_bf16(c2[j], c3[j]));
+          continue;
+        }
         uint2 p0, p1, p2;
         split4(c0[j], c1[j], c2[j], c3[j], p0, p1, p2);
-        const int o = x6_off(4 * mg + j, kg >> 1) + 8 * (kg & 1);
         *reinterpret_cast<uint2*>(S0 + o) = p0;
         *reinterpret_cast<uint2*>(S1 + o) = p1;
         *reinterpret_cast<uint2*>(S2 + o) = p2;
@@ -403,9 +407,13 @@ struct TileX6 {
       for (int i = 0; i < NV; ++i) {
         const int e = tid + i * NT;
         const int x = e >> 3, q = e & 7;
+        const int o = x6_off(x, q >> 1) + 8 * (q & 1);
+        if (P0ONLY) {
+          *reinterpret_cast<uint2*>(S0 + o) = make_uint2(pk_bf16(r[i].x, r[i].y), pk_bf16(r[i].z, r[i].w));
+          continue;
+        }
         uint2 p0, p1, p2;
         split4(r[i].x, r[i].y, r[i].z, r[i].w, p0, p1, p2);
-        const int o = x6_off(x, q >> 1) + 8 * (q & 1);
         *reinterpret_cast<uint2*>(S0 + o) = p0;
         *reinterpret_cast<uint2*>(S1 + o) = p1;
         *reinterpret_cast<uint2*>(S2 + o) = p2;
@@ -416,10 +424,13 @@ struct TileX6 {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-template <int BM, int BN, int TA, int TB, bool VA, bool VB>
+// VAR (tuning experiments only, mrg_gemm_x6_variant): 0 = the product kernel; 1 = split but one
+// MFMA (a0 b0) per block; 2 = plane 0 only (no residual split) with six MFMAs; 3 = plane 0 and one
+// MFMA (a plain bf16 GEMM on the same structure)
+template <int BM, int BN, int TA, int TB, bool VA, bool VB, int VAR = 0>
 __global__ __launch_bounds__(NT, 2) void gemm_x6_kernel(GemmArgs a) {
-  using IA = TileX6<BM, TA, VA>;
-  using IB = TileX6<BN, !TB, VB>;  // B(k, n): memory row k when TB == 0 (contiguous along n)
+  using IA = TileX6<BM, TA, VA, (VAR >= 2)>;
+  using IB = TileX6<BN, !TB, VB, (VAR >= 2)>;  // B(k, n): memory row k when TB == 0 (contiguous along n)
   constexpr int TM = BM / 64, TN = BN / 64;
   __shared__ __attribute__((aligned(16))) unsigned char sA[3][BM * 64];
   __shared__ __attribute__((aligned(16))) unsigned char sB[3][BN * 64];
@@ -497,6 +508,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_x6_kernel(GemmArgs a) {
 #pragma unroll
           for (int j = 0; j < TN; ++j) {
             // small terms first; the MFMA operand order (B, A) yields C^T per lane (epilogue below)
+            if (VAR == 1 || VAR == 3) {
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][0], fa[i][0], acc[i][j], 0, 0, 0);
+              continue;
+            }
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][2], fa[i][0], acc[i][j], 0, 0, 0);
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][1], fa[i][1], acc[i][j], 0, 0, 0);
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][0], fa[i][2], acc[i][j], 0, 0, 0);
@@ -770,6 +785,32 @@ MRG_API int mrg_gemm_set_mode(int mode) {
   return 0;
 }
 MRG_API int mrg_gemm_get_mode(void) { return g_gemm_mode; }
+
+// Tuning only: the x6 kernel's structural variants (see gemm_x6_kernel VAR) on C = A B^T,
+// A [M][K], B [N][K] row-major, 128x128 tiles, no split-K.  Results are NOT C for var != 0.
+MRG_API int mrg_gemm_x6_variant(int var, int M, int N, int K, const float* A, const float* B, float* C,
+                                hipStream_t stream) {
+  GemmArgs a;
+  memset(&a, 0, sizeof(a));
+  a.M = M; a.N = N; a.K = K; a.alpha = 1.0f;
+  a.A = A; a.amap = RowMap{K, 0, 0}; a.B = B; a.bmap = RowMap{K, 0, 0}; a.transB = 1;
+  a.C = C; a.ldc = N; a.kchunk = ((K + 31) / 32) * 32; a.vec = 1;
+  a.tiles_n = (N + 127) / 128;
+  a.tiles_mn = a.tiles_n * ((M + 127) / 128);
+  a.ntiles = a.tiles_mn;
+  switch (var) {
+#define MRG_V(V)                                                                            \
+    case V: {                                                                               \
+      auto k = gemm_x6_kernel<128, 128, 0, 1, true, true, V>;                               \
+      const int grid = a.ntiles < resident_blocks(k) ? a.ntiles : resident_blocks(k);      \
+      k<<<grid, NT, 0, stream>>>(a);                                                        \
+    } break;
+    MRG_V(0) MRG_V(1) MRG_V(2) MRG_V(3)
+#undef MRG_V
+    default: MRG_REQUIRE(false, "mrg_gemm_x6_variant: var 0..3");
+  }
+  return check_launch("gemm_x6_variant");
+}
 
 // Tuning only: force one tile shape (0: 128x128, 1: 128x64, 2: 64x64; -1 = heuristic).
 MRG_API int mrg_gemm_force_tile(int tile) {

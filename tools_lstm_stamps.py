@@ -59,5 +59,6 @@ if __name__ == "__main__":
     for grp in [int(g) for g in os.environ.get("GROUPS", "8").split(",")]:
         _lib.check(lib.mrg_lstm_config(grp), "config")
         print(f"== group256 = {grp}")
-        for nprob, bs in [(1, 0), (2, 0), (3, 0), (1, 2), (1, 4), (2, 4), (4, 4), (1, 8)]:
+        cfgs = os.environ.get("STAMP_CFGS", "1:0,2:0,3:0,1:2,1:4,2:4,4:4,1:8")
+        for nprob, bs in [tuple(int(v) for v in c.split(":")) for c in cfgs.split(",")]:
             run(nprob, bs)
