@@ -432,8 +432,11 @@ __global__ __launch_bounds__(NT, 2) void gemm_x6_kernel(GemmArgs a) {
   using IA = TileX6<BM, TA, VA, (VAR >= 2)>;
   using IB = TileX6<BN, !TB, VB, (VAR >= 2)>;  // B(k, n): memory row k when TB == 0 (contiguous along n)
   constexpr int TM = BM / 64, TN = BN / 64;
-  __shared__ __attribute__((aligned(16))) unsigned char sA[3][BM * 64];
-  __shared__ __attribute__((aligned(16))) unsigned char sB[3][BN * 64];
+  // one LDS array: the three bf16 planes of the A and B tiles, reused by the epilogue to
+  // turn the accumulators into whole-row stores
+  __shared__ __attribute__((aligned(16))) unsigned char lds[3 * (BM + BN) * 64];
+  unsigned char* const sA[3] = {lds, lds + BM * 64, lds + 2 * BM * 64};
+  unsigned char* const sB[3] = {lds + 3 * BM * 64, lds + 3 * BM * 64 + BN * 64, lds + 3 * BM * 64 + 2 * BN * 64};
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -541,18 +544,48 @@ __global__ __launch_bounds__(NT, 2) void gemm_x6_kernel(GemmArgs a) {
         }
       }
     }
+    // Each wave stages one 32-row slab of its accumulators in LDS (C^T lane map: lane = row,
+    // four consecutive n per register quad) and reads it back row-major, so every store
+    // instruction writes whole 128-256-B row segments instead of 32 B in each of 32 rows.
+    // (64-column tiles keep the direct per-lane stores: measured faster there)
+    if constexpr (BN >= 128) {
+      constexpr int WC = TN * 32, PITCH = WC + 4, C4 = WC / 4;
+      float* stg = reinterpret_cast<float*>(lds) + wave * 32 * PITCH;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int m = m0 + wm + i * 32 + lr;
+      for (int i = 0; i < TM; ++i) {
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
+        for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int r4 = 0; r4 < 4; ++r4) {
-          const int n = n0 + wn + j * 32 + 8 * r4 + 4 * lh;
-          const float4 v = make_float4(acc[i][j][4 * r4], acc[i][j][4 * r4 + 1], acc[i][j][4 * r4 + 2],
-                                       acc[i][j][4 * r4 + 3]);
-          if (m < a.M) store4(a, z, m, n, v);
+          for (int r4 = 0; r4 < 4; ++r4)
+            *reinterpret_cast<float4*>(stg + lr * PITCH + j * 32 + 8 * r4 + 4 * lh) =
+                make_float4(acc[i][j][4 * r4], acc[i][j][4 * r4 + 1], acc[i][j][4 * r4 + 2], acc[i][j][4 * r4 + 3]);
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int it = 0; it < 32 * C4 / 64; ++it) {
+          const int q = lane + 64 * it, row = q / C4, c4 = q % C4;
+          const float4 v = *reinterpret_cast<const float4*>(stg + row * PITCH + 4 * c4);
+          const int m = m0 + wm + i * 32 + row;
+          if (m < a.M) store4(a, z, m, n0 + wn + 4 * c4, v);
         }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+      __syncthreads();  // the staging area is the next tile's A/B planes
+    } else {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = m0 + wm + i * 32 + lr;
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r4 = 0; r4 < 4; ++r4) {
+            const int n = n0 + wn + j * 32 + 8 * r4 + 4 * lh;
+            const float4 v = make_float4(acc[i][j][4 * r4], acc[i][j][4 * r4 + 1], acc[i][j][4 * r4 + 2],
+                                         acc[i][j][4 * r4 + 3]);
+            if (m < a.M) store4(a, z, m, n, v);
+          }
+      }
     }
     m0 = m1; n0 = n1; kbeg = kb1; kend = ke1;
   }
