@@ -69,7 +69,12 @@ struct AttnCfg {
   static constexpr int DT = (D + 15) / 16;  // 16-wide d tiles of the output
   static constexpr int DP = DT * 16;
   static constexpr int KS = D / 4;          // k-steps over d
-  static constexpr int SA = DP + 2;         // row stride for [row = lane&15][4s + lane>>4] reads
+  // VEC (D >= 32): lane group lg takes the contiguous contraction indices d = KS*lg + s and the
+  // output columns d = DT*i + dt, so LDS operands are read as float4 / float2 (4x fewer LDS
+  // instructions than one ds_read_b32 per MFMA) and outputs are stored as contiguous runs; the
+  // sums are the same, in a different order.  D < 32 keeps the interleaved map (d = 4s + lg).
+  static constexpr bool VEC = D >= 32;
+  static constexpr int SA = VEC ? DP + 4 : DP + 2;  // row stride for the [row = lane&15][d] operand reads
   static constexpr int SV = DP + 4;         // row stride for [row = 4(lane>>4)+s][16dt + lane&15] reads
   static constexpr int NV = TT * (D / 4) / 256;  // float4 per thread per tile (0 at D = 8: half the threads load)
   static constexpr int NVR = NV > 0 ? NV : 1;
@@ -109,18 +114,59 @@ struct TileRegs {
   }
 };
 
+// contraction index d of k-step s for lane group lg (same map for every operand of a product)
+template <int D>
+__device__ __forceinline__ int dmap(int lg, int s) {
+  return AttnCfg<D>::VEC ? AttnCfg<D>::KS * lg + s : 4 * s + lg;
+}
+// output d of accumulator register (dt, r) held by lane group lg
+template <int D>
+__device__ __forceinline__ int dout(int lg, int dt, int r) {
+  return AttnCfg<D>::VEC ? AttnCfg<D>::DT * (4 * lg + r) + dt : dt * 16 + lg * 4 + r;
+}
+// the KS contraction operands of LDS row `row` for this lane: v[s] = S[row * STR + dmap(lg, s)]
+template <int D, int STR>
+__device__ __forceinline__ void row_operands(const float* S, int row, int lg, float (&v)[AttnCfg<D>::KS]) {
+  using C = AttnCfg<D>;
+  if constexpr (C::VEC) {
+#pragma unroll
+    for (int i = 0; i < C::KS; i += 4) {
+      const float4 t = *reinterpret_cast<const float4*>(S + row * STR + C::KS * lg + i);
+      v[i] = t.x; v[i + 1] = t.y; v[i + 2] = t.z; v[i + 3] = t.w;
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) v[s] = S[row * STR + 4 * s + lg];
+  }
+}
+// the DT output-side operands of LDS row `row` (A = X^T, MFMA row i = lane&15): v[dt] = X[row][col(i, dt)]
+template <int D, int STR>
+__device__ __forceinline__ void col_operands(const float* S, int row, int l16, float (&v)[AttnCfg<D>::DT]) {
+  using C = AttnCfg<D>;
+  if constexpr (C::VEC && C::DT == 4) {
+    const float4 t = *reinterpret_cast<const float4*>(S + row * STR + 4 * l16);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  } else if constexpr (C::VEC && C::DT == 2) {
+    const float2 t = *reinterpret_cast<const float2*>(S + row * STR + 2 * l16);
+    v[0] = t.x; v[1] = t.y;
+  } else {
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt) v[dt] = S[row * STR + dt * 16 + l16];
+  }
+}
+
 // S^T tile (16 keys x 16 queries) = K rows [kr..kr+15] . Q^T, two accumulation chains
 template <int D>
 __device__ __forceinline__ f32x4 qk16(const float* Ks, int rowbase, const float (&qreg)[AttnCfg<D>::KS], int lq,
                                       int lg) {
   using C = AttnCfg<D>;
   f32x4 s0 = f32x4{0.f, 0.f, 0.f, 0.f}, s1 = f32x4{0.f, 0.f, 0.f, 0.f};
+  float kv[C::KS];
+  row_operands<D, C::SA>(Ks, rowbase + lq, lg, kv);
 #pragma unroll
   for (int s = 0; s < C::KS; s += 2) {
-    s0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ks[(rowbase + lq) * C::SA + 4 * s + lg], qreg[s], s0, 0, 0, 0);
-    if (s + 1 < C::KS)
-      s1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ks[(rowbase + lq) * C::SA + 4 * (s + 1) + lg], qreg[s + 1], s1, 0,
-                                                0, 0);
+    s0 = __builtin_amdgcn_mfma_f32_16x16x4f32(kv[s], qreg[s], s0, 0, 0, 0);
+    if (s + 1 < C::KS) s1 = __builtin_amdgcn_mfma_f32_16x16x4f32(kv[s + 1], qreg[s + 1], s1, 0, 0, 0);
   }
   return s0 + s1;
 }
@@ -145,7 +191,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   float qreg[C::KS];
 #pragma unroll
   for (int s = 0; s < C::KS; ++s)
-    qreg[s] = qi < a.Tq ? a.q[(long)b * a.q_bs + (long)qi * a.q_ts + hoff + 4 * s + lg] * a.scale : 0.0f;
+    qreg[s] = qi < a.Tq ? a.q[(long)b * a.q_bs + (long)qi * a.q_ts + hoff + dmap<D>(lg, s)] * a.scale : 0.0f;
 
   f32x4 o[C::DT];
 #pragma unroll
@@ -205,11 +251,12 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
       for (int dt = 0; dt < C::DT; ++dt) o[dt] *= alpha;
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
+      for (int s = 0; s < 4; ++s) {
+        float vv[C::DT];
+        col_operands<D, C::SV>(Vs, sub * 16 + 4 * lg + s, lq, vv);
 #pragma unroll
-        for (int dt = 0; dt < C::DT; ++dt)
-          o[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Vs[(sub * 16 + 4 * lg + s) * C::SV + dt * 16 + lq], p[s],
-                                                       o[dt], 0, 0, 0);
+        for (int dt = 0; dt < C::DT; ++dt) o[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[dt], p[s], o[dt], 0, 0, 0);
+      }
     }
   }
   if (qi < a.Tq) {
@@ -219,7 +266,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
     for (int dt = 0; dt < C::DT; ++dt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int d = dt * 16 + lg * 4 + r;
+        const int d = dout<D>(lg, dt, r);
         if (d < D) op[d] = (l == 0.0f) ? NAN : o[dt][r] * inv;
       }
     if (lg == 0) a.lse[((long)b * a.Hh + h) * a.Tq + qi] = (l == 0.0f) ? NAN : m + __logf(l);
@@ -249,7 +296,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
   float dsum = 0.0f;
 #pragma unroll
   for (int s = 0; s < C::KS; ++s) {
-    const int d = 4 * s + lg;
+    const int d = dmap<D>(lg, s);
     qreg[s] = qv ? a.q[(long)b * a.q_bs + (long)qi * a.q_ts + hoff + d] * a.scale : 0.0f;
     dreg[s] = qv ? a.dout[(long)b * a.do_bs + (long)qi * a.do_ts + hoff + d] : 0.0f;
     const float ov = qv ? a.o[(long)b * a.o_bs + (long)qi * a.o_ts + hoff + d] : 0.0f;
@@ -286,10 +333,15 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
       if (kb >= klim) break;
       f32x4 s4 = f32x4{0.f, 0.f, 0.f, 0.f};
       f32x4 dp4 = f32x4{0.f, 0.f, 0.f, 0.f};
+      {
+        float kk[C::KS], vv[C::KS];
+        row_operands<D, C::SA>(Ks, sub * 16 + lq, lg, kk);
+        row_operands<D, C::SA>(Vs, sub * 16 + lq, lg, vv);
 #pragma unroll
-      for (int s = 0; s < C::KS; ++s) {
-        s4 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ks[(sub * 16 + lq) * C::SA + 4 * s + lg], qreg[s], s4, 0, 0, 0);
-        dp4 = __builtin_amdgcn_mfma_f32_16x16x4f32(Vs[(sub * 16 + lq) * C::SA + 4 * s + lg], dreg[s], dp4, 0, 0, 0);
+        for (int s = 0; s < C::KS; ++s) {
+          s4 = __builtin_amdgcn_mfma_f32_16x16x4f32(kk[s], qreg[s], s4, 0, 0, 0);
+          dp4 = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[s], dreg[s], dp4, 0, 0, 0);
+        }
       }
       const bool full = !pad && kb + 16 <= wmin;
       float ds[4];
@@ -301,11 +353,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
         ds[r] = p * (dp4[r] - dl);
       }
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
+      for (int s = 0; s < 4; ++s) {
+        float kk[C::DT];
+        col_operands<D, C::SA>(Ks, sub * 16 + 4 * lg + s, lq, kk);
 #pragma unroll
-        for (int dt = 0; dt < C::DT; ++dt)
-          dq[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ks[(sub * 16 + 4 * lg + s) * C::SA + dt * 16 + lq], ds[s],
-                                                        dq[dt], 0, 0, 0);
+        for (int dt = 0; dt < C::DT; ++dt) dq[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(kk[dt], ds[s], dq[dt], 0, 0, 0);
+      }
     }
   }
   if (qv) {
@@ -314,7 +367,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
     for (int dt = 0; dt < C::DT; ++dt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int d = dt * 16 + lg * 4 + r;
+        const int d = dout<D>(lg, dt, r);
         if (d < D) op[d] = dq[dt][r] * a.scale;
       }
   }
@@ -343,8 +396,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
   float kreg[C::KS], vreg[C::KS];
 #pragma unroll
   for (int s = 0; s < C::KS; ++s) {
-    kreg[s] = kv ? a.k[(long)b * a.k_bs + (long)kj * a.k_ts + hoff + 4 * s + lg] : 0.0f;
-    vreg[s] = kv ? a.v[(long)b * a.v_bs + (long)kj * a.v_ts + hoff + 4 * s + lg] : 0.0f;
+    kreg[s] = kv ? a.k[(long)b * a.k_bs + (long)kj * a.k_ts + hoff + dmap<D>(lg, s)] : 0.0f;
+    vreg[s] = kv ? a.v[(long)b * a.v_bs + (long)kj * a.v_ts + hoff + dmap<D>(lg, s)] : 0.0f;
   }
   f32x4 dkT[C::DT], dvT[C::DT];
 #pragma unroll
@@ -382,10 +435,15 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
       if (qb >= a.Tq) break;
       f32x4 s4 = f32x4{0.f, 0.f, 0.f, 0.f};
       f32x4 dp4 = f32x4{0.f, 0.f, 0.f, 0.f};
+      {
+        float qq[C::KS], dd[C::KS];
+        row_operands<D, C::SA>(Qs, sub * 16 + lk, lg, qq);
+        row_operands<D, C::SA>(Ds, sub * 16 + lk, lg, dd);
 #pragma unroll
-      for (int s = 0; s < C::KS; ++s) {
-        s4 = __builtin_amdgcn_mfma_f32_16x16x4f32(Qs[(sub * 16 + lk) * C::SA + 4 * s + lg], kreg[s], s4, 0, 0, 0);
-        dp4 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ds[(sub * 16 + lk) * C::SA + 4 * s + lg], vreg[s], dp4, 0, 0, 0);
+        for (int s = 0; s < C::KS; ++s) {
+          s4 = __builtin_amdgcn_mfma_f32_16x16x4f32(qq[s], kreg[s], s4, 0, 0, 0);
+          dp4 = __builtin_amdgcn_mfma_f32_16x16x4f32(dd[s], vreg[s], dp4, 0, 0, 0);
+        }
       }
       // every key of the wave is seen by all 16 queries of the sub-tile (all < Tq)
       const bool full = !pad && qb >= wmax && qb + 16 <= a.Tq;
@@ -399,13 +457,16 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
         ds[r] = p[r] * (dp4[r] - Dl[ql]);
       }
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
+      for (int s = 0; s < 4; ++s) {
+        float dd[C::DT], qq[C::DT];
+        col_operands<D, C::SA>(Ds, sub * 16 + 4 * lg + s, lk, dd);
+        col_operands<D, C::SA>(Qs, sub * 16 + 4 * lg + s, lk, qq);
 #pragma unroll
         for (int dt = 0; dt < C::DT; ++dt) {
-          const int row = (sub * 16 + 4 * lg + s) * C::SA + dt * 16 + lk;
-          dvT[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ds[row], p[s], dvT[dt], 0, 0, 0);
-          dkT[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Qs[row], ds[s], dkT[dt], 0, 0, 0);
+          dvT[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(dd[dt], p[s], dvT[dt], 0, 0, 0);
+          dkT[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(qq[dt], ds[s], dkT[dt], 0, 0, 0);
         }
+      }
     }
   }
   if (kv) {
@@ -415,7 +476,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
     for (int dt = 0; dt < C::DT; ++dt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int d = dt * 16 + lg * 4 + r;
+        const int d = dout<D>(lg, dt, r);
         if (d < D) {
           pk[d] = dkT[dt][r] * a.scale;
           pv[d] = dvT[dt][r];
