@@ -728,3 +728,76 @@ MRG_API int mrg_lstm_bwd(int nprob, int B, int T, int H,
   }
   return 2;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Single-step LSTM cell (T = 1): the per-frame decode of lstm_with_sampling's scheduled-sampling
+// training (LSTMSampler with carried state, LSTMLayerd restarted from zero each frame,
+// lstm_with_sample.py:410-433).  A persistent recurrence launch (W_hh into the VGPRs of 512
+// workgroups, a zeroed hand-off ring) for one step is pure overhead: the gate pre-activations
+// come from the GEMMs (x W_ih^T + b_ih, + h0 W_hh^T when there is a state) and these two
+// element-wise kernels do the rest.  Same gate order (i, f, g, o) and the same sigmoid / tanh
+// as the persistent kernels.
+namespace mrg {
+
+__global__ __launch_bounds__(256) void lstm_cell_fwd_kernel(int B, int H, const float* __restrict__ pre, long pre_ld,
+                                                            const float* __restrict__ b_hh,
+                                                            const float* __restrict__ c0, float* __restrict__ gates,
+                                                            float* __restrict__ c, float* __restrict__ h, long h_ld) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)B * H) return;
+  const int b = i / H, u = i % H;
+  const float* p = pre + (long)b * pre_ld;
+  const float zi = p[u] + b_hh[u], zf = p[H + u] + b_hh[H + u];
+  const float zg = p[2 * H + u] + b_hh[2 * H + u], zo = p[3 * H + u] + b_hh[3 * H + u];
+  const float ig = sigmoidf_(zi), fg = sigmoidf_(zf), gg = tanhf_(zg), og = sigmoidf_(zo);
+  const float cc = fg * (c0 ? c0[i] : 0.0f) + ig * gg;
+  float* gs = gates + (long)b * 4 * H + u;
+  gs[0] = ig; gs[H] = fg; gs[2 * H] = gg; gs[3 * H] = og;
+  c[i] = cc;
+  h[(long)b * h_ld + u] = og * tanhf_(cc);
+}
+
+__global__ __launch_bounds__(256) void lstm_cell_bwd_kernel(int B, int H, const float* __restrict__ gates,
+                                                            const float* __restrict__ c,
+                                                            const float* __restrict__ c0,
+                                                            const float* __restrict__ dh, long dh_ld,
+                                                            const float* __restrict__ dc, float* __restrict__ dG,
+                                                            float* __restrict__ dc0) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)B * H) return;
+  const int b = i / H, u = i % H;
+  const float* gs = gates + (long)b * 4 * H + u;
+  const float ig = gs[0], fg = gs[H], gg = gs[2 * H], og = gs[3 * H];
+  const float cc = c[i], cp = c0 ? c0[i] : 0.0f;
+  const float dhv = dh ? dh[(long)b * dh_ld + u] : 0.0f;
+  const float tc = tanhf_(cc);
+  const float dcc = dhv * og * (1.0f - tc * tc) + (dc ? dc[i] : 0.0f);
+  float* d = dG + (long)b * 4 * H + u;
+  d[0] = dcc * gg * ig * (1.0f - ig);
+  d[H] = dcc * cp * fg * (1.0f - fg);
+  d[2 * H] = dcc * ig * (1.0f - gg * gg);
+  d[3 * H] = dhv * tc * og * (1.0f - og);
+  if (dc0) dc0[i] = dcc * fg;
+}
+
+}  // namespace mrg
+
+// gates [B, 4H], c [B, H], h rows of stride h_ld; pre [B, 4H] rows of stride pre_ld (b_ih already in);
+// c0 nullable (zero state)
+MRG_API int mrg_lstm_cell_fwd(int B, int H, const float* pre, long pre_ld, const float* b_hh, const float* c0,
+                              float* gates, float* c, float* h, long h_ld, hipStream_t stream) {
+  if (B == 0 || H == 0) return 0;
+  const long n = (long)B * H;
+  lstm_cell_fwd_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(B, H, pre, pre_ld, b_hh, c0, gates, c, h,
+                                                                        h_ld);
+  return check_launch("lstm_cell_fwd_kernel");
+}
+
+// dG [B, 4H] = d(gate pre-activations); dh (rows of stride dh_ld), dc, c0, dc0 nullable
+MRG_API int mrg_lstm_cell_bwd(int B, int H, const float* gates, const float* c, const float* c0, const float* dh,
+                              long dh_ld, const float* dc, float* dG, float* dc0, hipStream_t stream) {
+  if (B == 0 || H == 0) return 0;
+  const long n = (long)B * H;
+  lstm_cell_bwd_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(B, H, gates, c, c0, dh, dh_ld, dc, dG, dc0);
+  return check_launch("lstm_cell_bwd_kernel");
+}

@@ -609,8 +609,74 @@ class _LSTMFn(Function):
         return tuple(out)
 
 
+class _LSTMCellFn(Function):
+    """One time step (T = 1) of one nn.LSTM direction: gate pre-activations by the GEMMs
+    (x W_ih^T + b_ih, + h0 W_hh^T with a state) and the element-wise cell kernels.  The per-frame
+    decode of lstm_with_sampling's scheduled sampling (lstm_with_sample.py:410-433) runs 300 of
+    these per training step; a persistent recurrence launch per frame would be pure overhead."""
+
+    @staticmethod
+    def forward(ctx, x, w_ih, w_hh, b_ih, b_hh, h0, c0):
+        _lib.require_device(x)
+        dev = x.device
+        B, _, In = x.shape
+        H = w_hh.shape[1]
+        lib = _lib.load()
+        x2 = x.reshape(B, In).contiguous()
+        pre = torch.empty(B, 4 * H, device=dev, dtype=torch.float32)
+        gemm(B, 4 * H, In, _ptr(x2), 0, In, _ptr(w_ih), 1, In, _ptr(pre), 4 * H, bias=_ptr(b_ih), device=dev)
+        h0c = None if h0 is None else h0.contiguous()
+        c0c = None if c0 is None else c0.contiguous()
+        if h0c is not None:
+            gemm(B, 4 * H, H, _ptr(h0c), 0, H, _ptr(w_hh), 1, H, _ptr(pre), 4 * H, beta=1.0, device=dev)
+        gates = torch.empty(B, 4 * H, device=dev, dtype=torch.float32)
+        c = torch.empty(B, H, device=dev, dtype=torch.float32)
+        h = torch.empty(B, H, device=dev, dtype=torch.float32)
+        _lib.check(lib.mrg_lstm_cell_fwd(B, H, _ptr(pre), 4 * H, _ptr(b_hh), _ptr(c0c), _ptr(gates), _ptr(c),
+                                         _ptr(h), H, _stream()), "lstm cell fwd")
+        ctx.save_for_backward(x2, w_ih, w_hh, b_ih, b_hh, h0c, c0c, gates, c)
+        return h.view(B, 1, H), h.clone(), c.clone()
+
+    @staticmethod
+    def backward(ctx, dy, dhT, dcT):
+        x2, w_ih, w_hh, b_ih, b_hh, h0c, c0c, gates, c = ctx.saved_tensors
+        B, In = x2.shape
+        H = w_hh.shape[1]
+        dev = x2.device
+        lib = _lib.load()
+        dh = None
+        if dy is not None:
+            dh = dy.reshape(B, H)
+        if dhT is not None:
+            dh = dhT if dh is None else dh + dhT
+        dh = None if dh is None else dh.contiguous()
+        dcT = None if dcT is None else dcT.contiguous()
+        dG = torch.empty(B, 4 * H, device=dev, dtype=torch.float32)
+        need = ctx.needs_input_grad
+        dc0 = torch.empty(B, H, device=dev, dtype=torch.float32) if (c0c is not None and need[6]) else None
+        _lib.check(lib.mrg_lstm_cell_bwd(B, H, _ptr(gates), _ptr(c), _ptr(c0c), _ptr(dh), H, _ptr(dcT), _ptr(dG),
+                                         _ptr(dc0), _stream()), "lstm cell bwd")
+        gbi, gbh = _gbuf(b_ih), _gbuf(b_hh)
+        first = gbi if gbi is not None else gbh
+        _wgrad(_ptr(dG), 4 * H, _ptr(x2), In, B, 4 * H, In, _gbuf(w_ih), dev, gb=first,
+               gb2=gbh if gbi is not None else None)
+        gw = _gbuf(w_hh)  # zero state: dW_hh = dG^T h0 = 0 (the buffer still exists, as with nn.LSTM)
+        if gw is not None and h0c is not None:
+            _wgrad(_ptr(dG), 4 * H, _ptr(h0c), H, B, 4 * H, H, gw, dev)
+        dx = dh0 = None
+        if need[0]:
+            dx = torch.empty(B, 1, In, device=dev, dtype=torch.float32)
+            gemm(B, In, 4 * H, _ptr(dG), 0, 4 * H, _ptr(w_ih), 0, In, _ptr(dx), In, device=dev)
+        if h0c is not None and need[5]:
+            dh0 = torch.empty(B, H, device=dev, dtype=torch.float32)
+            gemm(B, H, 4 * H, _ptr(dG), 0, 4 * H, _ptr(w_hh), 0, H, _ptr(dh0), H, device=dev)
+        return dx, None, None, None, None, dh0, dc0
+
+
 def lstm_layer(x, w_ih, w_hh, b_ih, b_hh, h0=None, c0=None, reverse=False, force_bs=0):
     """One direction of one nn.LSTM layer (batch_first).  Returns (y, hT, cT)."""
+    if x.shape[1] == 1 and force_bs == 0:
+        return _LSTMCellFn.apply(x, w_ih, w_hh, b_ih, b_hh, h0, c0)
     y, hT, cT = _LSTMFn.apply((1, False, (reverse,), force_bs, None), x, w_ih, w_hh, b_ih, b_hh, h0, c0)
     return y, hT, cT
 
@@ -619,6 +685,9 @@ def lstm_residual_layernorm(x, w_ih, w_hh, b_ih, b_hh, gamma, beta, eps=1e-5, h0
                             force_bs=0):
     """LN(LSTM(x) + x) for one unidirectional layer (ResidualConnection(LSTMMixer), mixer_block.py:
     479-507); the LSTM's dX GEMM takes the residual gradient in its epilogue.  Returns (u, hT, cT)."""
+    if x.shape[1] == 1 and force_bs == 0:
+        y, hT, cT = _LSTMCellFn.apply(x, w_ih, w_hh, b_ih, b_hh, h0, c0)
+        return residual_layernorm(y, x, gamma, beta, eps), hT, cT
     u, hT, cT = _LSTMFn.apply((1, False, (False,), force_bs, float(eps)), x, w_ih, w_hh, b_ih, b_hh, h0, c0,
                               gamma, beta)
     return u, hT, cT
@@ -640,6 +709,9 @@ def lstm_layers_batched(problems: Sequence[Sequence], force_bs=0):
     if eps is not None and any(len(p) <= 5 for p in problems):
         raise ValueError("lstm_layers_batched: residual LayerNorm must be given for every problem or none")
     n = len(problems)
+    if problems[0][0].shape[1] == 1 and force_bs == 0:
+        return [lstm_layer(*p[:5])[0] if len(p) <= 5 else lstm_residual_layernorm(*p[:5], p[5], p[6], p[7])[0]
+                for p in problems]
     outs = _LSTMFn.apply((n, False, (False,) * n, force_bs, eps), *flat)
     return list(outs[:n])
 

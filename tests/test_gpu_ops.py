@@ -241,6 +241,41 @@ def test_lstm_layer_vs_oracle(H, In, B, T, rev):
         assert rel_err(p.grad, r.grad) < TOL
 
 
+@pytest.mark.parametrize("H,In,B", [(256, 256, 64), (64, 40, 5), (16, 8, 3)])
+def test_lstm_single_step_chain_vs_oracle(H, In, B):
+    """T = 1 steps (the scheduled-sampling decode, lstm_with_sample.py:410-433) go through the cell
+    kernels; four chained steps carry (h, c) and their gradients from step to step."""
+    from multimodalreactiongeneration_amd import functional as Fn
+    from oracle import mrg_oracle as O
+    g = torch.Generator().manual_seed(H + In)
+    k = 1 / math.sqrt(H)
+    w = [(torch.rand(4 * H, n, generator=g) * 2 - 1) * k for n in (In, H)]
+    bb = [(torch.rand(4 * H, generator=g) * 2 - 1) * k for _ in range(2)]
+    xs = [torch.randn(B, 1, In, generator=g) for _ in range(4)]
+    dys = [torch.randn(B, 1, H, generator=g) for _ in range(4)]
+    ps = [_param(t) for t in (*w, *bb)]
+    rs = [t.clone().requires_grad_(True) for t in (*w, *bb)]
+    xd = [x.to(DEV).requires_grad_(True) for x in xs]
+    xr = [x.clone().requires_grad_(True) for x in xs]
+    h = c = hr = cr = None
+    loss = loss_r = 0
+    for i in range(4):
+        y, h, c = Fn.lstm_layer(xd[i], *ps, h, c)
+        yr, hr, cr = O.lstm_layer(xr[i], *rs, hr, cr)
+        assert y.shape == (B, 1, H)
+        assert rel_err(y, yr) < TOL
+        loss = loss + (y * dys[i].to(DEV)).sum()
+        loss_r = loss_r + (yr * dys[i]).sum()
+    (loss + c.sum()).backward()
+    (loss_r + cr.sum()).backward()
+    torch.cuda.synchronize()
+    assert rel_err(c, cr) < TOL
+    for a, r in zip(xd, xr):
+        assert rel_err(a.grad, r.grad) < TOL
+    for p, r in zip(ps, rs):
+        assert rel_err(p.grad, r.grad) < TOL
+
+
 @pytest.mark.parametrize("bs", [1, 2, 4, 8])
 def test_lstm_batched_problems_and_forced_tiling(bs):
     """3 independent recurrences in one launch, every batch-tile size, vs the oracle."""

@@ -1,0 +1,76 @@
+"""Step times of the other BASELINE configs (not the headline bench line): eager fwd+bwd+AdamW.
+
+    python tools_bench_models.py [steps]      (on a GPU box)
+
+  C2  simple_lstm, B=64, T=300 (fp32 arithmetic here; the BASELINE names bf16)
+  C3  lstm_with_sampling, scheduled-sampling autoregressive training, B=64, T=300, lead 12,
+      epoch 30/60 (sampling probability 0.5, mask from RandomState(7) as SURVEY §8d)
+  C3' lstm_with_sampling teacher-forced, B=64, T=300
+"""
+import json
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+from multimodalreactiongeneration_amd import configs as C  # noqa: E402
+from multimodalreactiongeneration_amd import functional as Fn  # noqa: E402
+from multimodalreactiongeneration_amd.model import LSTMwithSample, SimpleLSTM  # noqa: E402
+from multimodalreactiongeneration_amd.synthetic import make_batch, make_simple_batch, clone_batch  # noqa: E402
+
+DEV = "cuda:0"
+
+
+def timed(fn, steps, warm=2):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps * 1e3
+
+
+def main():
+    steps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    out = {}
+    torch.manual_seed(0)
+    mc, oc, me = C.simple_lstm_config()
+    m = SimpleLSTM(mc, oc, me).to(DEV)
+    opt = m.configure_optimizers()["optimizer"]
+    batch = make_simple_batch(B=64, T=300, device=DEV)
+
+    def step_simple():
+        opt.zero_grad()
+        m.training_step(batch)["loss"].backward()
+        opt.step()
+    ms = timed(step_simple, steps)
+    out["C2_simple_lstm_fp32_B64_T300"] = {"ms_per_step": round(ms, 2), "frames_per_s": round(64 * 300 / ms * 1e3)}
+    print(json.dumps(out), flush=True)
+
+    for ss in (False, True):
+        mc, oc, me = C.lstm_with_sampling_config(use_scheduled_sampling=ss)
+        torch.manual_seed(0)
+        m = LSTMwithSample(mc, oc, me).to(DEV)
+        m.current_epoch = 30
+        opt = m.configure_optimizers()["optimizer"]
+        batch = make_batch(B=64, T=300, lead=12 if ss else 0, seed=1234, device=DEV)
+        mask = torch.from_numpy(np.random.RandomState(7).rand(300) < 0.5)
+
+        def step_lws():
+            opt.zero_grad()
+            kw = {"sampling_mask": mask} if ss else {}
+            m.training_step(clone_batch(batch), **kw)["loss"].backward()
+            opt.step()
+        ms = timed(step_lws, steps)
+        key = "C3_lstm_with_sampling_scheduled_sampling" if ss else "C3tf_lstm_with_sampling_teacher_forced"
+        out[key] = {"ms_per_step": round(ms, 2), "frames_per_s": round(64 * 300 / ms * 1e3)}
+        print(json.dumps(out), flush=True)
+    Fn.check_errors()
+
+
+if __name__ == "__main__":
+    main()
