@@ -120,6 +120,7 @@ def main():
     args = parse()
     from multimodalreactiongeneration_amd import configs as C
     from multimodalreactiongeneration_amd import functional as Fn
+    from multimodalreactiongeneration_amd.graphs import capture
     from multimodalreactiongeneration_amd.ddp import init_from_env, broadcast_parameters, GradReducer
     from multimodalreactiongeneration_amd.model import Metaformer
     from multimodalreactiongeneration_amd.synthetic import make_batch
@@ -155,21 +156,12 @@ def main():
     if args.graph:
         # capture fwd+bwd(+AdamW at N=1) once; the RCCL all-reduce stays eager between replays at N>1
         captured = step if world == 1 else fwd_bwd
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(max(2, args.warmup)):
-                step()
-        torch.cuda.current_stream().wait_stream(s)
-        torch.cuda.synchronize()
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            captured()
+        replay = capture(captured, max(2, args.warmup))
         if world == 1:
-            run = graph.replay
+            run = replay
         else:
             def run():
-                graph.replay()
+                replay()
                 reducer.allreduce()
                 opt.step()
     else:

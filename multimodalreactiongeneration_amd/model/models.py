@@ -374,7 +374,8 @@ class LSTMwithSample(LightningSurface):
 
         The sampler state is carried across steps; the layered LSTM restarts
         from zero every step (Q2); teacher forcing feeds motion_s[step] (Q10).
-        ``sampling_mask`` overrides the global-RNG draw (tests pin it).
+        ``sampling_mask`` overrides the global-RNG draw (tests pin it); on the GPU it makes the
+        step graph-capturable (``graphs.capture``).
         """
         dev = self.device
         (fb, lf), (mp, lp), (ms, ls) = batch[0], batch[1], batch[2]
@@ -393,10 +394,16 @@ class LSTMwithSample(LightningSurface):
         y = ms[0]
         preds = []
         ones = torch.ones(B, dtype=torch.long)
+        # a device-resident mask selects on the GPU (same values and gradients as the host branch):
+        # no host read per frame, so the whole decode + backward can be captured in one HIP graph
+        on_device = torch.is_tensor(sampling_mask) and sampling_mask.device.type != "cpu"
         for step in range(T):
             y, _, cell = self.forward((fb[step], lf), (mp[step], lp), (y, ones), *empty[3:6], cell)
             preds.append(y)
-            y = y if bool(sampling_mask[step]) else ms[step]
+            if on_device:
+                y = torch.where(sampling_mask[step], y, ms[step])
+            else:
+                y = y if bool(sampling_mask[step]) else ms[step]
         return torch.cat(preds, dim=1), target
 
 

@@ -1,6 +1,9 @@
 """Step times of the other BASELINE configs (not the headline bench line): eager fwd+bwd+AdamW.
 
-    python tools_bench_models.py [steps]      (on a GPU box)
+    python tools_bench_models.py [steps] [C2|C3|C3tf] [graph]     (on a GPU box)
+
+  graph=1 replays each step as one HIP graph (graphs.capture); C3's sampling mask then lives in a
+  static device buffer refreshed from the host RNG draw before every replay.
 
   C2  simple_lstm, B=64, T=300 (fp32 arithmetic here; the BASELINE names bf16)
   C3  lstm_with_sampling, scheduled-sampling autoregressive training, B=64, T=300, lead 12,
@@ -23,7 +26,18 @@ from multimodalreactiongeneration_amd.synthetic import make_batch, make_simple_b
 DEV = "cuda:0"
 
 
-def timed(fn, steps, warm=2):
+GRAPH = False
+
+
+def timed(fn, steps, warm=2, pre=None):
+    if GRAPH:
+        from multimodalreactiongeneration_amd.graphs import capture
+        replay = capture(fn, warm)
+
+        def fn():
+            if pre is not None:
+                pre()
+            replay()
     for _ in range(warm):
         fn()
     torch.cuda.synchronize()
@@ -36,8 +50,13 @@ def timed(fn, steps, warm=2):
 
 def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    only = sys.argv[2] if len(sys.argv) > 2 and sys.argv[2] != "all" else ""
+    global GRAPH
+    GRAPH = len(sys.argv) > 3 and sys.argv[3] == "1"
     out = {}
     torch.manual_seed(0)
+    if only and only != "C2":
+        return main_lws(steps, only, out)
     mc, oc, me = C.simple_lstm_config()
     m = SimpleLSTM(mc, oc, me).to(DEV)
     opt = m.configure_optimizers()["optimizer"]
@@ -48,10 +67,16 @@ def main():
         m.training_step(batch)["loss"].backward()
         opt.step()
     ms = timed(step_simple, steps)
-    out["C2_simple_lstm_fp32_B64_T300"] = {"ms_per_step": round(ms, 2), "frames_per_s": round(64 * 300 / ms * 1e3)}
+    out["C2_simple_lstm_fp32_B64_T300" + ("_graph" if GRAPH else "")] = {"ms_per_step": round(ms, 2), "frames_per_s": round(64 * 300 / ms * 1e3)}
     print(json.dumps(out), flush=True)
+    if not only:
+        main_lws(steps, only, out)
 
+
+def main_lws(steps, only, out):
     for ss in (False, True):
+        if only and only != ("C3" if ss else "C3tf"):
+            continue
         mc, oc, me = C.lstm_with_sampling_config(use_scheduled_sampling=ss)
         torch.manual_seed(0)
         m = LSTMwithSample(mc, oc, me).to(DEV)
@@ -59,14 +84,21 @@ def main():
         opt = m.configure_optimizers()["optimizer"]
         batch = make_batch(B=64, T=300, lead=12 if ss else 0, seed=1234, device=DEV)
         mask = torch.from_numpy(np.random.RandomState(7).rand(300) < 0.5)
+        if GRAPH:
+            mask = mask.to(DEV)
+        rng = np.random.RandomState(7)
+
+        def refresh():  # the host draw of lstm_with_sample.py:389 into the static device mask
+            mask.copy_(torch.from_numpy(rng.rand(300) < 0.5))
 
         def step_lws():
             opt.zero_grad()
             kw = {"sampling_mask": mask} if ss else {}
-            m.training_step(clone_batch(batch), **kw)["loss"].backward()
+            m.training_step(batch if GRAPH else clone_batch(batch), **kw)["loss"].backward()
             opt.step()
-        ms = timed(step_lws, steps)
+        ms = timed(step_lws, steps, pre=refresh if ss else None)
         key = "C3_lstm_with_sampling_scheduled_sampling" if ss else "C3tf_lstm_with_sampling_teacher_forced"
+        key += "_graph" if GRAPH else ""
         out[key] = {"ms_per_step": round(ms, 2), "frames_per_s": round(64 * 300 / ms * 1e3)}
         print(json.dumps(out), flush=True)
     Fn.check_errors()
