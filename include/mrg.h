@@ -115,12 +115,15 @@ int mrg_lstm_bwd(int nprob, int B, int T, int H,
 int mrg_lstm_config(int group256);
 /* Single-step cell (T = 1), e.g. the per-frame decode of lstm_with_sampling's scheduled-sampling
  * training (lstm_with_sample.py:410-433): pre [B, 4H] = x W_ih^T + b_ih (+ h0 W_hh^T) from the
- * GEMMs; fwd adds b_hh and writes gates [B, 4H], c [B, H], h (row stride h_ld); bwd writes dG and
- * dc0 (nullable).  c0 / dh / dc nullable (zero).                                              */
+ * GEMMs; fwd adds b_hh and writes gates [B, 4H], c [B, H], h (row stride h_ld) and a dense copy
+ * h2 [B, H] (nullable; the step's output and its final state); bwd takes the h gradient as
+ * dh (row stride dh_ld) + dh2 (dense) and writes dG and dc0 (nullable).  c0 / dh / dh2 / dc
+ * nullable (zero).                                                                            */
 int mrg_lstm_cell_fwd(int B, int H, const float* pre, long pre_ld, const float* b_hh, const float* c0,
-                      float* gates, float* c, float* h, long h_ld, hipStream_t stream);
+                      float* gates, float* c, float* h, long h_ld, float* h2, hipStream_t stream);
 int mrg_lstm_cell_bwd(int B, int H, const float* gates, const float* c, const float* c0, const float* dh,
-                      long dh_ld, const float* dc, float* dG, float* dc0, hipStream_t stream);
+                      long dh_ld, const float* dh2, const float* dc, float* dG, float* dc0,
+                      hipStream_t stream);
 
 /* Diagnostics only: record per-step phase clocks (s_memtime) of block 0 of the next
  * LSTM launches into buf ([T][8] u64); null disables.  Never in timed runs. */

@@ -540,7 +540,14 @@ __global__ __launch_bounds__(NT, 2) void gemm_x6_kernel(GemmArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int m = m0 + 4 * mg + j;
-          if (m < a.M) a.asum[(long)z * a.M + m] = cs[j];
+          if (m >= a.M) continue;
+          if (a.ws) {
+            a.asum[(long)z * a.M + m] = cs[j];
+          } else {  // no split: this tile holds the whole sum of row m; finish it here
+            a.asum_out[m] = (a.asum_beta != 0.0f ? a.asum_beta * a.asum_out[m] : 0.0f) + cs[j];
+            if (a.asum_out2)
+              a.asum_out2[m] = (a.asum_beta != 0.0f ? a.asum_beta * a.asum_out2[m] : 0.0f) + cs[j];
+          }
         }
       }
     }
@@ -908,7 +915,7 @@ MRG_API int mrg_gemm_f32_ex(int M, int N, int K, float alpha,
     // gradients and wide/deep products; 64x64 for narrow ones (N <= 128, or N = 256 at K <= 512
     // with K-contiguous B); small problems take the tile that gives the most workgroups
     const long t0 = (long)((M + 127) / 128) * ((N + 127) / 128) * splits;
-    if (splits > 1) tile = 0;
+    if (splits > 1) tile = transA ? 0 : 2;  // weight gradients / few-row activation products
     else if (t0 < 256) tile = 2;
     else if (N >= 512 || K >= 1024) tile = 0;
     else if (N <= 128) tile = 2;
@@ -923,7 +930,7 @@ MRG_API int mrg_gemm_f32_ex(int M, int N, int K, float alpha,
   if (g_tile_override >= 0 && g_tile_override <= 2) tile = g_tile_override;
   if (launch_gemm(a, tile, bk, transA, transB, va, vb, splits, stream)) return 2;
   if (check_launch("gemm_f32_kernel")) return 1;
-  bool asum_done = false;
+  bool asum_done = splits == 1;  // unsplit: the GEMM's n0 == 0 tiles wrote asum_out directly
   if (splits > 1) {
     long total = (long)M * N;
     if (a.vec && (N & 3) == 0) {

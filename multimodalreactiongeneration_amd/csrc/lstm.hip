@@ -742,7 +742,8 @@ namespace mrg {
 __global__ __launch_bounds__(256) void lstm_cell_fwd_kernel(int B, int H, const float* __restrict__ pre, long pre_ld,
                                                             const float* __restrict__ b_hh,
                                                             const float* __restrict__ c0, float* __restrict__ gates,
-                                                            float* __restrict__ c, float* __restrict__ h, long h_ld) {
+                                                            float* __restrict__ c, float* __restrict__ h, long h_ld,
+                                                            float* __restrict__ h2) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= (long)B * H) return;
   const int b = i / H, u = i % H;
@@ -754,13 +755,16 @@ __global__ __launch_bounds__(256) void lstm_cell_fwd_kernel(int B, int H, const 
   float* gs = gates + (long)b * 4 * H + u;
   gs[0] = ig; gs[H] = fg; gs[2 * H] = gg; gs[3 * H] = og;
   c[i] = cc;
-  h[(long)b * h_ld + u] = og * tanhf_(cc);
+  const float hv = og * tanhf_(cc);
+  h[(long)b * h_ld + u] = hv;
+  if (h2) h2[i] = hv;
 }
 
 __global__ __launch_bounds__(256) void lstm_cell_bwd_kernel(int B, int H, const float* __restrict__ gates,
                                                             const float* __restrict__ c,
                                                             const float* __restrict__ c0,
                                                             const float* __restrict__ dh, long dh_ld,
+                                                            const float* __restrict__ dh2,
                                                             const float* __restrict__ dc, float* __restrict__ dG,
                                                             float* __restrict__ dc0) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
@@ -769,7 +773,7 @@ __global__ __launch_bounds__(256) void lstm_cell_bwd_kernel(int B, int H, const 
   const float* gs = gates + (long)b * 4 * H + u;
   const float ig = gs[0], fg = gs[H], gg = gs[2 * H], og = gs[3 * H];
   const float cc = c[i], cp = c0 ? c0[i] : 0.0f;
-  const float dhv = dh ? dh[(long)b * dh_ld + u] : 0.0f;
+  const float dhv = (dh ? dh[(long)b * dh_ld + u] : 0.0f) + (dh2 ? dh2[i] : 0.0f);
   const float tc = tanhf_(cc);
   const float dcc = dhv * og * (1.0f - tc * tc) + (dc ? dc[i] : 0.0f);
   float* d = dG + (long)b * 4 * H + u;
@@ -782,22 +786,24 @@ __global__ __launch_bounds__(256) void lstm_cell_bwd_kernel(int B, int H, const 
 
 }  // namespace mrg
 
-// gates [B, 4H], c [B, H], h rows of stride h_ld; pre [B, 4H] rows of stride pre_ld (b_ih already in);
-// c0 nullable (zero state)
+// gates [B, 4H], c [B, H], h rows of stride h_ld (and a dense copy in h2, nullable); pre [B, 4H]
+// rows of stride pre_ld (b_ih already in); c0 nullable (zero state)
 MRG_API int mrg_lstm_cell_fwd(int B, int H, const float* pre, long pre_ld, const float* b_hh, const float* c0,
-                              float* gates, float* c, float* h, long h_ld, hipStream_t stream) {
+                              float* gates, float* c, float* h, long h_ld, float* h2, hipStream_t stream) {
   if (B == 0 || H == 0) return 0;
   const long n = (long)B * H;
   lstm_cell_fwd_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(B, H, pre, pre_ld, b_hh, c0, gates, c, h,
-                                                                        h_ld);
+                                                                        h_ld, h2);
   return check_launch("lstm_cell_fwd_kernel");
 }
 
-// dG [B, 4H] = d(gate pre-activations); dh (rows of stride dh_ld), dc, c0, dc0 nullable
+// dG [B, 4H] = d(gate pre-activations); the h gradient is dh (rows of stride dh_ld) + dh2 (dense);
+// dh, dh2, dc, c0, dc0 nullable
 MRG_API int mrg_lstm_cell_bwd(int B, int H, const float* gates, const float* c, const float* c0, const float* dh,
-                              long dh_ld, const float* dc, float* dG, float* dc0, hipStream_t stream) {
+                              long dh_ld, const float* dh2, const float* dc, float* dG, float* dc0,
+                              hipStream_t stream) {
   if (B == 0 || H == 0) return 0;
   const long n = (long)B * H;
-  lstm_cell_bwd_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(B, H, gates, c, c0, dh, dh_ld, dc, dG, dc0);
+  lstm_cell_bwd_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(B, H, gates, c, c0, dh, dh_ld, dh2, dc, dG, dc0);
   return check_launch("lstm_cell_bwd_kernel");
 }

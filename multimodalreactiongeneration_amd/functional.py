@@ -127,6 +127,8 @@ def gemm(M, N, K, A, transA, lda, B, transB, ldb, C, ldc, *, alpha=1.0, beta=0.0
     if M == 0 or N == 0:
         return
     lib = _lib.load()
+    if splits == 1 and not transA:
+        splits = act_splits(M, N, K)
     ws = None
     if splits > 1 or asum_out is not None:
         ws = _ws(lib.mrg_gemm_workspace_bytes(M, N, splits), device)
@@ -135,6 +137,15 @@ def gemm(M, N, K, A, transA, lda, B, transB, ldb, C, ldc, *, alpha=1.0, beta=0.0
                                  beta, C, ldc, bias, epi, aux, ldaux, _ptr(ws), splits, asum_out, asum_out2,
                                  asum_beta, _stream())
     _lib.check(rc, "gemm")
+
+
+def act_splits(M, N, K):
+    """split-K factor for few-row activation products (the T = 1 decode: M = batch rows):
+    a handful of 64x64 tiles walking K >= 512 is latency-bound, so spread K over the CUs."""
+    tiles = ((M + 63) // 64) * ((N + 63) // 64)
+    if tiles >= 64 or K < 512 or _lib.load().mrg_gemm_get_mode() != 1:
+        return 1
+    return int(max(1, min(K // 64, 128 // tiles)))
 
 
 def wgrad_splits(M, N, K):
@@ -631,11 +642,13 @@ class _LSTMCellFn(Function):
             gemm(B, 4 * H, H, _ptr(h0c), 0, H, _ptr(w_hh), 1, H, _ptr(pre), 4 * H, beta=1.0, device=dev)
         gates = torch.empty(B, 4 * H, device=dev, dtype=torch.float32)
         c = torch.empty(B, H, device=dev, dtype=torch.float32)
-        h = torch.empty(B, H, device=dev, dtype=torch.float32)
+        y = torch.empty(B, 1, H, device=dev, dtype=torch.float32)
+        hT = torch.empty(B, H, device=dev, dtype=torch.float32)
         _lib.check(lib.mrg_lstm_cell_fwd(B, H, _ptr(pre), 4 * H, _ptr(b_hh), _ptr(c0c), _ptr(gates), _ptr(c),
-                                         _ptr(h), H, _stream()), "lstm cell fwd")
+                                         _ptr(y), H, _ptr(hT), _stream()), "lstm cell fwd")
         ctx.save_for_backward(x2, w_ih, w_hh, b_ih, b_hh, h0c, c0c, gates, c)
-        return h.view(B, 1, H), h.clone(), c.clone()
+        ctx.set_materialize_grads(False)  # an unused final state costs no zero-filled gradient
+        return y, hT, c
 
     @staticmethod
     def backward(ctx, dy, dhT, dcT):
@@ -644,18 +657,14 @@ class _LSTMCellFn(Function):
         H = w_hh.shape[1]
         dev = x2.device
         lib = _lib.load()
-        dh = None
-        if dy is not None:
-            dh = dy.reshape(B, H)
-        if dhT is not None:
-            dh = dhT if dh is None else dh + dhT
-        dh = None if dh is None else dh.contiguous()
+        dy = None if dy is None else dy.contiguous()
+        dhT = None if dhT is None else dhT.contiguous()
         dcT = None if dcT is None else dcT.contiguous()
         dG = torch.empty(B, 4 * H, device=dev, dtype=torch.float32)
         need = ctx.needs_input_grad
         dc0 = torch.empty(B, H, device=dev, dtype=torch.float32) if (c0c is not None and need[6]) else None
-        _lib.check(lib.mrg_lstm_cell_bwd(B, H, _ptr(gates), _ptr(c), _ptr(c0c), _ptr(dh), H, _ptr(dcT), _ptr(dG),
-                                         _ptr(dc0), _stream()), "lstm cell bwd")
+        _lib.check(lib.mrg_lstm_cell_bwd(B, H, _ptr(gates), _ptr(c), _ptr(c0c), _ptr(dy), H, _ptr(dhT), _ptr(dcT),
+                                         _ptr(dG), _ptr(dc0), _stream()), "lstm cell bwd")
         gbi, gbh = _gbuf(b_ih), _gbuf(b_hh)
         first = gbi if gbi is not None else gbh
         _wgrad(_ptr(dG), 4 * H, _ptr(x2), In, B, 4 * H, In, _gbuf(w_ih), dev, gb=first,
