@@ -218,10 +218,10 @@ class Metaformer(LightningSurface):
         return Fn.masked_loss(y, target.to(y.device), lead, self.model.loss_type, self.huber_delta,
                               self.smoothl1_beta, True, self.delta_order, self.delta_loss_scale)
 
-    def training_step(self, batch: List, *args):
+    def training_step(self, batch: List, *args, sampling_mask=None):
         if self.use_scheduled_sampling:
             self.log("scheduled_sampling_rate", self.current_epoch / self.max_epochs, logger=True)
-            y, target = self.prediction(batch, use_scheduled_sampling=True)
+            y, target = self.prediction(batch, use_scheduled_sampling=True, sampling_mask=sampling_mask)
             loss = self._masked_loss(y, target, 0)
         else:
             lead = batch[4][0].shape[1]
@@ -249,11 +249,15 @@ class Metaformer(LightningSurface):
         return {"loss": loss}
 
     # ---------------- autoregressive generation (lstmformer.py:426-559)
-    def prediction(self, batch: List, use_scheduled_sampling: bool = False, full_generation: bool = False):
+    def prediction(self, batch: List, use_scheduled_sampling: bool = False, full_generation: bool = False,
+                   sampling_mask=None):
         """Stateless step-by-step generation (the reference never carries state, Q1).
 
         The reference multiplies target [B,T,F] by a [T,B,1,F] mask, which
         broadcasts (Q9); here the target is masked elementwise instead.
+        ``sampling_mask`` ([T] bool) overrides the mask drawn from the flags; on the GPU it
+        selects on the device, so the whole generation can be captured as one HIP graph
+        (``graphs.capture``).
         """
         dev = self.device
         (fb, lf), (mp, lp), (ms, ls) = batch[0], batch[1], batch[2]
@@ -269,17 +273,23 @@ class Metaformer(LightningSurface):
         target = target * (target != PADDING_VALUE).to(target.dtype)
         empty = [(torch.empty(x.shape[0], 0, x.shape[2], device=dev), n) for x, n in batch]
         _, cell = self.forward(*empty[:3], *batch[3:6], hxs=None)
-        if use_scheduled_sampling:
+        if sampling_mask is not None:
+            mask = sampling_mask
+        elif use_scheduled_sampling:
             mask = torch.rand(T) < (self.current_epoch / self.max_epochs)
         else:
             mask = torch.ones(T, dtype=torch.bool) if full_generation else torch.zeros(T, dtype=torch.bool)
+        on_device = mask.device.type != "cpu"
         y = ms[0]
         preds = []
         ones = torch.ones(B, dtype=torch.long)
         for step in range(T):
             y, cell = self.forward((fb[step], lf), (mp[step], lp), (y, ones), *empty[3:6], cell)
             preds.append(y)
-            y = y if bool(mask[step]) else ms[step]
+            if on_device:
+                y = torch.where(mask[step], y, ms[step])
+            else:
+                y = y if bool(mask[step]) else ms[step]
         return torch.cat(preds, dim=1), target
 
 

@@ -261,6 +261,36 @@ def metaformer_training_loss(sd: SD, cfg, batch) -> Tuple[Tensor, Tensor]:
     return loss, y
 
 
+def metaformer_prediction(sd: SD, cfg, batch, sampling_mask: Tensor) -> Tensor:
+    """Metaformer.prediction (lstmformer.py:426-547): stateless single-step generation.
+
+    form_generation_init (:523-547) zeroes the -100 padding of audio / partner / self
+    motion and cuts them into per-step slices ([B, r, F] audio, [B, 1, F] pose); each step
+    runs the full forward on that step with empty lead inputs (gen_dummy_input, :549-559)
+    and feeds back its own output (mask true) or motion_s[step] (teacher forcing, the
+    one-step lag of :492).  The warm-up forward (:461-464) only produces a state the
+    forward never reads, so it is not restated.  Returns the prediction [B, T, F].
+    """
+    (fb, lf), (mp, lp), (ms, ls) = batch[0], batch[1], batch[2]
+    T, B = mp.shape[1], mp.shape[0]
+    r = fb.shape[1] // T
+    fb = fb.reshape(B, T, r, fb.shape[-1]).transpose(0, 1)
+    mp = mp.transpose(0, 1).unsqueeze(2)
+    ms = ms.transpose(0, 1).unsqueeze(2)
+    fb = fb * (fb != PADDING_VALUE).int()
+    mp = mp * (mp != PADDING_VALUE).int()
+    ms = ms * (ms != PADDING_VALUE).int()
+    empty = [(x.new_zeros(x.shape[0], 0, x.shape[2]), n) for x, n in batch]
+    y = ms[0]
+    preds = []
+    ones = torch.ones(B, dtype=torch.long)
+    for step in range(T):
+        y = metaformer_forward(sd, cfg, [(fb[step], lf), (mp[step], lp), (y, ones)] + empty[3:6])
+        preds.append(y)
+        y = y if bool(sampling_mask[step]) else ms[step]
+    return torch.cat(preds, 1)
+
+
 # ---------------------------------------------------------- lstm_with_sampling
 def lstm_with_sample_forward(sd: SD, cfg, inputs, hx_sampler=None):
     """LSTMwithSample.forward (lstm_with_sample.py:151-232); returns (y, hx_sampler)."""

@@ -93,6 +93,44 @@ def metaformer_case(name, hidden, nb, enc, bn, B, T, lead, ratio, lengths=None, 
     print("wrote", name, "loss", out["loss"])
 
 
+def metaformer_generation_case(name, hidden, nb, enc, bn, B, T, lead, ratio, lengths=None, seed=0,
+                               epoch=30):
+    """Metaformer.prediction (lstmformer.py:426-547), eval + no_grad: full generation, teacher
+    forcing, and scheduled sampling with the global-RNG mask recorded (lstmformer.py:476)."""
+    model_cfg, optim, metrics = C.lstmformer_config(hidden=hidden, num_block=nb,
+                                                    encoder_num_layer=enc, bottleneck=bn,
+                                                    ratio=ratio, lr=1e-3)
+    torch.manual_seed(seed)
+    m = R.Metaformer(model_cfg, optim, metrics)
+    m.current_epoch = epoch
+    m.eval()
+    batch = make_batch(B=B, T=T, lead=lead, ratio=ratio, seed=1234 + seed, lengths=lengths)
+    out = {"meta/config": json.dumps(dict(model=model_cfg, optim=optim, metrics=metrics)),
+           "meta/epoch": np.int64(epoch)}
+    pack_batch(out, batch)
+    for k, v in m.state_dict().items():
+        out[f"param/{k}"] = _np(v)
+    with torch.no_grad():
+        out["pred/full"] = _np(m.prediction(clone_batch(batch), full_generation=True)[0])
+        out["pred/tf"] = _np(m.prediction(clone_batch(batch))[0])
+        rec = {}
+        orig = torch.rand
+
+        def _rand(*a, **k):
+            r = orig(*a, **k)
+            rec.setdefault("mask_rand", r.clone())
+            return r
+        torch.manual_seed(7)
+        torch.rand = _rand
+        try:
+            out["pred/ss"] = _np(m.prediction(clone_batch(batch), use_scheduled_sampling=True)[0])
+        finally:
+            torch.rand = orig
+        out["sampling_mask"] = (rec["mask_rand"] < epoch / model_cfg["max_epochs"]).numpy()
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    print("wrote", name, "ss mask", out["sampling_mask"].astype(int).tolist())
+
+
 def lstm_with_sample_case(name, hidden, sh, B, T, lead, ratio, scheduled=False, epoch=30,
                           seed=0, lengths=None):
     model_cfg, optim, metrics = C.lstm_with_sampling_config(
@@ -244,7 +282,16 @@ def state_dict_keys():
     print("wrote state_dict_keys", {k: len(v) for k, v in res.items()})
 
 
+def generation_cases():
+    metaformer_generation_case("metaformer_gen_r2_pad", 32, 2, 2, 16, B=3, T=6, lead=2, ratio=2,
+                               lengths=[6, 5, 4], seed=3)
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["generation"]:  # only the generation fixtures (the others stay as committed)
+        generation_cases()
+        sys.exit(0)
+    generation_cases()
     mask_cases()
     op_cases()
     state_dict_keys()

@@ -186,3 +186,67 @@ def test_metaformer_benchmark_width_vs_oracle(ratio, B, T):
     assert abs(loss.item() - ref_loss.item()) / abs(ref_loss.item()) < TOL
     worst = max(rel_err(p.grad, grads[k]) for k, p in m.named_parameters())
     assert worst < TOL, worst
+
+
+@pytest.mark.parametrize("mode", ["full", "tf", "ss"])
+def test_metaformer_generation_golden(mode):
+    """Metaformer.prediction (lstmformer.py:426-547) vs the reference's own output: T = 1 steps
+    through the LSTM cell kernels, ratio 2, ragged padding; all three sampling modes."""
+    from multimodalreactiongeneration_amd.model import Metaformer
+    d = load("metaformer_gen_r2_pad")
+    m, cfg = _build(Metaformer, d)
+    m.eval()
+    batch = batch_from(d, DEV)
+    T = batch[1][0].shape[1]
+    mask = {"full": torch.ones(T, dtype=torch.bool), "tf": torch.zeros(T, dtype=torch.bool),
+            "ss": torch.from_numpy(d["sampling_mask"])}[mode]
+    with torch.no_grad():
+        pred, _ = m.prediction(batch, sampling_mask=mask)
+    torch.cuda.synchronize()
+    assert rel_err(pred, d[f"pred/{mode}"]) < TOL
+
+
+def test_metaformer_generation_graph_replay():
+    """The same generation captured once as a HIP graph with the mask in a device buffer and
+    replayed for two different masks (graphs.capture)."""
+    from multimodalreactiongeneration_amd.graphs import capture
+    from multimodalreactiongeneration_amd.model import Metaformer
+    d = load("metaformer_gen_r2_pad")
+    m, cfg = _build(Metaformer, d)
+    m.eval()
+    batch = batch_from(d, DEV)
+    T = batch[1][0].shape[1]
+    mask = torch.zeros(T, dtype=torch.bool, device=DEV)
+    out = torch.zeros(batch[1][0].shape[0], T, 6, device=DEV)
+
+    def gen():
+        with torch.no_grad():
+            out.copy_(m.prediction(batch, sampling_mask=mask)[0])
+    replay = capture(gen, 1)
+    for mode in ("ss", "full"):
+        mask.copy_(torch.from_numpy(d["sampling_mask"]) if mode == "ss" else torch.ones(T, dtype=torch.bool))
+        replay()
+        torch.cuda.synchronize()
+        assert rel_err(out, d[f"pred/{mode}"]) < TOL, mode
+
+
+def test_metaformer_generation_benchmark_width_vs_oracle():
+    """Benchmark architecture (H=256, 5 blocks, 5 encoder layers, r=1) generating 40 frames,
+    scheduled-sampling mask RandomState(7) < 0.5, vs the CPU oracle restatement."""
+    from multimodalreactiongeneration_amd import configs as C
+    from multimodalreactiongeneration_amd.model import Metaformer
+    from multimodalreactiongeneration_amd.synthetic import make_batch, clone_batch
+    from oracle import mrg_oracle as O
+    mc, oc, me = C.lstmformer_config(ratio=1)
+    torch.manual_seed(0)
+    m = Metaformer(mc, oc, me).eval()
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.to(DEV)
+    T = 40
+    batch = make_batch(B=3, T=T, lead=4, seed=5)
+    mask = torch.from_numpy(np.random.RandomState(7).rand(T) < 0.5)
+    with torch.no_grad():
+        pred, _ = m.prediction(clone_batch(batch, DEV), sampling_mask=mask)
+        ref = O.metaformer_prediction(sd, mc, clone_batch(batch), mask)
+    torch.cuda.synchronize()
+    assert rel_err(pred, ref) < TOL

@@ -206,3 +206,19 @@ def test_aten_lstm_timing_path_equals_restatement(reverse):
             O.ATEN_LSTM = False
     for a, b in zip(*outs):
         assert rel_err(a, b) < 1e-5
+
+
+@pytest.mark.parametrize("mode", ["full", "tf", "ss"])
+def test_metaformer_generation(mode):
+    """Metaformer.prediction (lstmformer.py:426-547) at ratio 2 with ragged -100 padding:
+    full generation, teacher forcing and the recorded scheduled-sampling mask."""
+    d = load("metaformer_gen_r2_pad")
+    cfg = config(d)
+    sd = prefixed(d, "param/")
+    batch = batch_from(d)
+    T = batch[1][0].shape[1]
+    mask = {"full": torch.ones(T, dtype=torch.bool), "tf": torch.zeros(T, dtype=torch.bool),
+            "ss": torch.from_numpy(d["sampling_mask"])}[mode]
+    with torch.no_grad():
+        pred = O.metaformer_prediction(sd, cfg["model"], batch, mask)
+    assert rel_err(pred, d[f"pred/{mode}"]) < TOL

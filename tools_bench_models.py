@@ -1,6 +1,6 @@
 """Step times of the other BASELINE configs (not the headline bench line): eager fwd+bwd+AdamW.
 
-    python tools_bench_models.py [steps] [C2|C3|C3tf] [graph]     (on a GPU box)
+    python tools_bench_models.py [steps] [C2|C3|C3tf|gen|all] [graph]     (on a GPU box)
 
   graph=1 replays each step as one HIP graph (graphs.capture); C3's sampling mask then lives in a
   static device buffer refreshed from the host RNG draw before every replay.
@@ -55,6 +55,8 @@ def main():
     GRAPH = len(sys.argv) > 3 and sys.argv[3] == "1"
     out = {}
     torch.manual_seed(0)
+    if only == "gen":
+        return main_gen(steps, out)
     if only and only != "C2":
         return main_lws(steps, only, out)
     mc, oc, me = C.simple_lstm_config()
@@ -71,6 +73,28 @@ def main():
     print(json.dumps(out), flush=True)
     if not only:
         main_lws(steps, only, out)
+        main_gen(steps, out)
+
+
+def main_gen(steps, out):
+    """lstmformer autoregressive generation (Metaformer.prediction, full_generation, no grad):
+    SURVEY 8f rank 1; the reference logs this per clip in speed.log (visualize_metaformer.py)."""
+    from multimodalreactiongeneration_amd.model import Metaformer
+    mc, oc, me = C.lstmformer_config(ratio=1)
+    torch.manual_seed(0)
+    m = Metaformer(mc, oc, me).to(DEV).eval()
+    T = 300
+    batch = make_batch(B=64, T=T, lead=12, seed=1234, device=DEV)
+    mask = torch.ones(T, dtype=torch.bool, device=DEV) if GRAPH else None
+
+    def gen():
+        with torch.no_grad():
+            m.prediction(batch, full_generation=True, sampling_mask=mask)
+    ms = timed(gen, steps)
+    key = "lstmformer_generation_B64_T300" + ("_graph" if GRAPH else "")
+    out[key] = {"ms_per_clip_batch": round(ms, 2), "ms_per_frame": round(ms / T, 4),
+                "frames_per_s": round(64 * T / ms * 1e3)}
+    print(json.dumps(out), flush=True)
 
 
 def main_lws(steps, only, out):
