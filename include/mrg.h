@@ -65,14 +65,19 @@ int mrg_gemm_f32(int M, int N, int K, float alpha,
  * With transA = 1 (A stored k-major, e.g. dY of a weight gradient dY^T X) this
  * is the bias gradient of the same Linear, computed inside the GEMM's A-tile
  * staging instead of by a separate column-sum pass; needs `workspace`
- * (mrg_gemm_workspace_bytes).                                               */
+ * (mrg_gemm_workspace_bytes).
+ * counters (nullable): MRG_GEMM_COUNTERS u32 tickets, zero-filled once by the caller and kept
+ * across calls on one stream.  With it, a split-K GEMM with a small output lets the last K slice
+ * of each tile combine the slabs in the same launch (fixed z order, like the reduce kernel) and
+ * return the tickets to zero, instead of a separate reduce launch.                            */
+#define MRG_GEMM_COUNTERS 4096
 int mrg_gemm_f32_ex(int M, int N, int K, float alpha,
                     const float* A, int transA, long lda, long lda_hi, int a_rdiv,
                     const float* B, int transB, long ldb, long ldb_hi, int b_rdiv,
                     float beta, float* C, long ldc, const float* bias, int epilogue,
                     const float* aux, long ldaux, float* workspace, int splits,
                     float* asum_out, float* asum_out2, float asum_beta,
-                    hipStream_t stream);
+                    unsigned* counters, hipStream_t stream);
 
 /* out[n] = beta*out[n] + sum_rows X(row, n); out2 (nullable) receives the same
  * sum (b_ih and b_hh share one gradient).  Bias gradients of every Linear.  */

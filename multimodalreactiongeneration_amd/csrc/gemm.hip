@@ -40,6 +40,10 @@ struct GemmArgs {
   float* ws;  // split-K slabs [splits][M][N] (nullptr when splits == 1)
   int kchunk;
   int tiles_n, tiles_mn, ntiles;  // output tiles (x splits), walked by a persistent grid
+  int nsplit;                     // K slices per tile (ntiles / tiles_mn)
+  // in-launch split-K combine (x6 path, small outputs): per-tile tickets, zero between launches;
+  // null -> the slabs are reduced by splitk_reduce*_kernel
+  unsigned* cnt;
   int vec;                        // C / bias / aux / slab rows 16-B aligned: vector epilogue
   // fused row sums of op(A) (bias gradients of a weight-gradient GEMM, TA = 1, x6 path):
   // per-(split, m) partials in asum [splits][M], reduced in a fixed order into
@@ -49,6 +53,10 @@ struct GemmArgs {
   float* asum_out2;
   float asum_beta;
 };
+
+#ifndef MRG_GEMM_COUNTERS
+#define MRG_GEMM_COUNTERS 4096  // tickets the caller provides (include/mrg.h)
+#endif
 
 static constexpr int BK = 32;  // K tile (64 measured no faster here: 2 blocks/CU instead of 3)
 static constexpr int NT = 256;
@@ -424,6 +432,57 @@ struct TileX6 {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
+// In-launch split-K combine (cdna_hip_programming.md, "Projection GEMM at M = 256", item 2):
+// every K slice stores its fp32 slab and draws a ticket for its tile; the workgroup that draws
+// the last one sums the tile's slabs in z order (deterministic, the order splitk_reduce uses)
+// and runs the epilogue, then returns the ticket counter to 0 for the next launch.  Agent-scope
+// release before the ticket, acquire after it, so slices on different XCDs are seen.
+template <int BM, int BN>
+__device__ __forceinline__ void splitk_fixup(const GemmArgs& a, int tile, int m0, int n0, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab stores
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned old = __hip_atomic_fetch_add(a.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == (unsigned)(a.nsplit - 1);
+    if (last) {
+      __hip_atomic_store(a.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  const int last = *flag;
+  __syncthreads();  // the flag lives in the staging array the next tile overwrites
+  if (!last) return;
+  GemmArgs b = a;
+  b.ws = nullptr;  // store4 now writes C through the epilogue
+  const long slab = (long)a.M * a.N;
+  constexpr int C4 = BN / 4;
+  for (int e = threadIdx.x; e < BM * C4; e += NT) {
+    const int m = m0 + e / C4, n = n0 + 4 * (e % C4);
+    if (m >= a.M || n >= a.N) continue;
+    const float* p = a.ws + (long)m * a.N + n;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.vec && n + 3 < a.N) {
+      for (int z = 0; z < a.nsplit; ++z) {
+        const float4 v = *reinterpret_cast<const float4*>(p + z * slab);
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      }
+    } else {
+      for (int z = 0; z < a.nsplit; ++z) {
+        s.x += p[z * slab];
+        if (n + 1 < a.N) s.y += p[z * slab + 1];
+        if (n + 2 < a.N) s.z += p[z * slab + 2];
+        if (n + 3 < a.N) s.w += p[z * slab + 3];
+      }
+    }
+    store4(b, 0, m, n, s);
+  }
+}
+
 // VAR (tuning experiments only, mrg_gemm_x6_variant): 0 = the product kernel; 1 = split but one
 // MFMA (a0 b0) per block; 2 = plane 0 only (no residual split) with six MFMAs; 3 = plane 0 and one
 // MFMA (a plain bf16 GEMM on the same structure)
@@ -432,6 +491,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_x6_kernel(GemmArgs a) {
   using IA = TileX6<BM, TA, VA, (VAR >= 2)>;
   using IB = TileX6<BN, !TB, VB, (VAR >= 2)>;  // B(k, n): memory row k when TB == 0 (contiguous along n)
   constexpr int TM = BM / 64, TN = BN / 64;
+  // 64x64 tiles (small products) also finish unsplit bias sums and combine split-K slabs in-launch;
+  // kept out of the 128-wide kernels, whose register budget sets 3 waves per SIMD
+  constexpr bool SMALL = (BM == 64 && BN == 64);
   // one LDS array: the three bf16 planes of the A and B tiles, reused by the epilogue to
   // turn the accumulators into whole-row stores
   __shared__ __attribute__((aligned(16))) unsigned char lds[3 * (BM + BN) * 64];
@@ -541,9 +603,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_x6_kernel(GemmArgs a) {
         for (int j = 0; j < 4; ++j) {
           const int m = m0 + 4 * mg + j;
           if (m >= a.M) continue;
-          if (a.ws) {
+          if (!SMALL || a.ws) {
             a.asum[(long)z * a.M + m] = cs[j];
-          } else {  // no split: this tile holds the whole sum of row m; finish it here
+          } else {  // 64x64 tiles, no split: this tile holds the whole sum of row m; finish it here
             a.asum_out[m] = (a.asum_beta != 0.0f ? a.asum_beta * a.asum_out[m] : 0.0f) + cs[j];
             if (a.asum_out2)
               a.asum_out2[m] = (a.asum_beta != 0.0f ? a.asum_beta * a.asum_out2[m] : 0.0f) + cs[j];
@@ -593,6 +655,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_x6_kernel(GemmArgs a) {
             if (m < a.M) store4(a, z, m, n, v);
           }
       }
+    }
+    if constexpr (SMALL) {
+      if (a.cnt) splitk_fixup<BM, BN>(a, t - z * a.tiles_mn, m0, n0, reinterpret_cast<int*>(lds));
     }
     m0 = m1; n0 = n1; kbeg = kb1; kend = ke1;
   }
@@ -751,6 +816,7 @@ static void launch_tile(GemmArgs a, int ta, int tb, bool va, bool vb, int splits
   a.tiles_n = (a.N + BN - 1) / BN;
   a.tiles_mn = a.tiles_n * ((a.M + BM - 1) / BM);
   a.ntiles = a.tiles_mn * splits;
+  a.nsplit = splits;
   const int code = (ta << 3) | (tb << 2) | ((int)va << 1) | (int)vb;
   switch (code) {
 #define MRG_G(TA, TB, VA, VB)                                                                    \
@@ -772,6 +838,7 @@ static void launch_tile_x6(GemmArgs a, int ta, int tb, bool va, bool vb, int spl
   a.tiles_n = (a.N + BN - 1) / BN;
   a.tiles_mn = a.tiles_n * ((a.M + BM - 1) / BM);
   a.ntiles = a.tiles_mn * splits;
+  a.nsplit = splits;
   const int code = (ta << 3) | (tb << 2) | ((int)va << 1) | (int)vb;
   switch (code) {
 #define MRG_G(TA, TB, VA, VB)                                                                    \
@@ -785,6 +852,65 @@ static void launch_tile_x6(GemmArgs a, int ta, int tb, bool va, bool vb, int spl
     MRG_G(1, 0, 0, 0) MRG_G(1, 0, 0, 1) MRG_G(1, 0, 1, 0) MRG_G(1, 0, 1, 1)
     MRG_G(1, 1, 0, 0) MRG_G(1, 1, 0, 1) MRG_G(1, 1, 1, 0) MRG_G(1, 1, 1, 1)
 #undef MRG_G
+  }
+}
+
+
+// ----------------------------------------------------------------------------------------------
+// Few-row products (M <= 64: the batch rows of a T = 1 decode step, lstm_with_sample.py:410-433,
+// lstmformer.py:498-521).  Staging a 64x64 tile through LDS 32 k at a time leaves every k step
+// waiting on a global round trip, so these run as exact f32 MFMA (v_mfma_f32_16x16x4_f32) straight
+// from global/L2 into registers: a workgroup owns one 16 x 16 output block, its 4 waves take K
+// quarters and each wave's 4 lane groups contiguous sub-ranges of those (operands load as runs),
+// all loads of a chunk are in flight at once, and the 4 partial blocks are summed in LDS in a
+// fixed order before the epilogue.  Arithmetic: fp32 FMA chains (no bf16 split needed).
+template <int TB, int CH>
+__global__ __launch_bounds__(256) void gemm_rows_kernel(GemmArgs a) {
+  __shared__ float red[4][16][17];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, l16 = lane & 15;
+  const int m0 = blockIdx.y * 16, n0 = blockIdx.x * 16;
+  const int KQ = (a.K + 15) / 16;  // contiguous k per (wave, lane group)
+  const int kb = (wave * 4 + g) * KQ;
+  const int ke = min(a.K, kb + KQ);
+  const int m = m0 + l16, n = n0 + l16;
+  const bool mv = m < a.M, nv = n < a.N;
+  const float* ap = a.A + (mv ? a.amap.off(m) : 0);
+  const float* bp = a.B + (TB ? (nv ? a.bmap.off(n) : 0) : n);
+  f32x4v acc = f32x4v{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = kb; k0 < ke; k0 += CH) {
+    float av[CH], bv[CH];
+#pragma unroll
+    for (int s = 0; s < CH; ++s) {
+      const int k = k0 + s;
+      const bool ok = k < ke;
+      av[s] = (ok && mv) ? ap[k] : 0.0f;
+      bv[s] = (ok && nv) ? (TB ? bp[k] : bp[a.bmap.off(k)]) : 0.0f;
+    }
+#pragma unroll
+    for (int s = 0; s < CH; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[s], acc, 0, 0, 0);
+  }
+  // lane holds C[4g + i][l16] of this wave's partial block
+#pragma unroll
+  for (int i = 0; i < 4; ++i) red[wave][4 * g + i][l16] = acc[i];
+  __syncthreads();
+  const int r = threadIdx.x >> 4, c = threadIdx.x & 15;
+  const int mo = m0 + r, no = n0 + c;
+  if (mo < a.M && no < a.N) {
+    const float v = ((red[0][r][c] + red[1][r][c]) + red[2][r][c]) + red[3][r][c];
+    a.C[(long)mo * a.ldc + no] = apply_epi(a, v, mo, no);
+  }
+}
+
+static void launch_rows(const GemmArgs& a, hipStream_t s) {
+  const dim3 grid((a.N + 15) / 16, (a.M + 15) / 16);
+  const int kq = (a.K + 15) / 16;
+  if (a.transB) {
+    if (kq <= 16) gemm_rows_kernel<1, 16><<<grid, 256, 0, s>>>(a);
+    else gemm_rows_kernel<1, 64><<<grid, 256, 0, s>>>(a);
+  } else {
+    if (kq <= 16) gemm_rows_kernel<0, 16><<<grid, 256, 0, s>>>(a);
+    else gemm_rows_kernel<0, 64><<<grid, 256, 0, s>>>(a);
   }
 }
 
@@ -878,7 +1004,7 @@ MRG_API int mrg_gemm_f32_ex(int M, int N, int K, float alpha,
                             float beta, float* C, long ldc, const float* bias, int epilogue,
                             const float* aux, long ldaux, float* workspace, int splits,
                             float* asum_out, float* asum_out2, float asum_beta,
-                            hipStream_t stream) {
+                            unsigned* counters, hipStream_t stream) {
   MRG_REQUIRE(M >= 0 && N >= 0 && K >= 0, "mrg_gemm_f32: negative size");
   MRG_REQUIRE(epilogue >= 0 && epilogue <= 3, "mrg_gemm_f32: bad epilogue %d", epilogue);
   MRG_REQUIRE(epilogue < 2 || aux, "mrg_gemm_f32: epilogue %d needs aux", epilogue);
@@ -899,6 +1025,7 @@ MRG_API int mrg_gemm_f32_ex(int M, int N, int K, float alpha,
   a.kchunk = kc;
   a.ws = splits > 1 ? workspace : nullptr;
   a.asum = nullptr; a.asum_out = asum_out; a.asum_out2 = asum_out2; a.asum_beta = asum_beta;
+  a.cnt = nullptr; a.nsplit = splits;
   // fused bias-gradient row sums: x6 path with A = (memory rows k, contiguous along m)
   const bool fuse_asum = asum_out && g_gemm_mode == 1 && transA && workspace;
   if (fuse_asum) a.asum = workspace + (splits > 1 ? (long)splits * M * N : 0);
@@ -909,6 +1036,11 @@ MRG_API int mrg_gemm_f32_ex(int M, int N, int K, float alpha,
   const bool va = aligned(A, a.amap), vb = aligned(B, a.bmap);
   a.vec = ((((uintptr_t)C | (uintptr_t)bias | (uintptr_t)aux | (uintptr_t)workspace) & 15) == 0 && (ldc & 3) == 0 &&
            (!aux || (ldaux & 3) == 0) && (!a.ws || (N & 3) == 0)) ? 1 : 0;
+  // few-row products (x6 mode): exact f32 MFMA from registers, no split, no LDS staging
+  if (g_gemm_mode == 1 && !transA && M <= 64 && splits == 1 && !asum_out) {
+    launch_rows(a, stream);
+    return check_launch("gemm_rows_kernel");
+  }
   int tile;  // 0: 128x128, 1: 128x64, 2: 64x64
   if (g_gemm_mode == 1) {
     // x6 (measured on the step's shapes, tools_gemm_sweep.py): 128x128 for split-K weight
@@ -928,10 +1060,17 @@ MRG_API int mrg_gemm_f32_ex(int M, int N, int K, float alpha,
     tile = 2;
   }
   if (g_tile_override >= 0 && g_tile_override <= 2) tile = g_tile_override;
+  // small split outputs: the last K slice of each tile combines the slabs in-launch (no reduce
+  // kernel) when the slabs it must read stay small (<= 64 KB per tile)
+  if (splits > 1 && counters && g_gemm_mode == 1 && !a.asum && tile == 2) {
+    const long tiles = (long)((M + 63) / 64) * ((N + 63) / 64);
+    if (tiles <= MRG_GEMM_COUNTERS && (long)splits * 64 * 64 * 4 <= 65536) a.cnt = counters;
+  }
   if (launch_gemm(a, tile, bk, transA, transB, va, vb, splits, stream)) return 2;
   if (check_launch("gemm_f32_kernel")) return 1;
-  bool asum_done = splits == 1;  // unsplit: the GEMM's n0 == 0 tiles wrote asum_out directly
-  if (splits > 1) {
+  // unsplit 64x64-tile GEMM (x6): its n0 == 0 tiles wrote asum_out directly
+  bool asum_done = splits == 1 && tile == 2 && g_gemm_mode == 1;
+  if (splits > 1 && !a.cnt) {
     long total = (long)M * N;
     if (a.vec && (N & 3) == 0) {
       const long cb = (total / 4 + RPB - 1) / RPB, ab = a.asum ? (M + RPB - 1) / RPB : 0;
@@ -966,7 +1105,8 @@ MRG_API int mrg_gemm_f32(int M, int N, int K, float alpha,
                          const float* aux, long ldaux, float* workspace, int splits,
                          hipStream_t stream) {
   return mrg_gemm_f32_ex(M, N, K, alpha, A, transA, lda, lda_hi, a_rdiv, B, transB, ldb, ldb_hi, b_rdiv, beta, C,
-                         ldc, bias, epilogue, aux, ldaux, workspace, splits, nullptr, nullptr, 0.0f, stream);
+                         ldc, bias, epilogue, aux, ldaux, workspace, splits, nullptr, nullptr, 0.0f, nullptr,
+                         stream);
 }
 
 static int colsum_splits(int rows) {

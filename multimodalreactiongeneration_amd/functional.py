@@ -28,6 +28,7 @@ from . import _lib
 
 F32 = 4
 _ERR = {}
+_CNT = {}
 
 # --- optional live kernel timing (bench.py): HIP events recorded on the launch stream
 _PROBE_ON = set()
@@ -91,6 +92,15 @@ def _ws(nbytes: int, device) -> torch.Tensor:
     return torch.empty(max(1, (int(nbytes) + 3) // 4), dtype=torch.float32, device=device)
 
 
+def _counters(device) -> torch.Tensor:
+    """Split-K tickets of the in-launch slab combine (mrg_gemm_f32_ex): zeroed once, every launch
+    leaves them at zero again."""
+    key = torch.device(device).index or 0
+    if key not in _CNT:
+        _CNT[key] = torch.zeros(4096, dtype=torch.int32, device=device)  # MRG_GEMM_COUNTERS
+    return _CNT[key]
+
+
 def _err_flag(device) -> torch.Tensor:
     key = torch.device(device).index or 0
     if key not in _ERR:
@@ -135,17 +145,18 @@ def gemm(M, N, K, A, transA, lda, B, transB, ldb, C, ldc, *, alpha=1.0, beta=0.0
     with _probe("gemm", 2.0 * M * N * K):
         rc = lib.mrg_gemm_f32_ex(M, N, K, alpha, A, transA, lda, a_hi, a_div, B, transB, ldb, b_hi, b_div,
                                  beta, C, ldc, bias, epi, aux, ldaux, _ptr(ws), splits, asum_out, asum_out2,
-                                 asum_beta, _stream())
+                                 asum_beta, _ptr(_counters(device)) if splits > 1 else None, _stream())
     _lib.check(rc, "gemm")
 
 
 def act_splits(M, N, K):
-    """split-K factor for few-row activation products (the T = 1 decode: M = batch rows):
-    a handful of 64x64 tiles walking K >= 512 is latency-bound, so spread K over the CUs."""
+    """split-K factor for activation products with few output tiles (65..~2000 rows): a handful of
+    64x64 tiles walking K >= 512 is latency-bound, so spread K over the CUs."""
     tiles = ((M + 63) // 64) * ((N + 63) // 64)
-    if tiles >= 64 or K < 512 or _lib.load().mrg_gemm_get_mode() != 1:
-        return 1
-    return int(max(1, min(K // 64, 128 // tiles)))
+    if M <= 64 or tiles >= 64 or K < 512 or _lib.load().mrg_gemm_get_mode() != 1:
+        return 1  # M <= 64: the few-row kernel (gemm_rows_kernel) needs no split
+    # <= 4 slices of 64x64 tiles: the slabs (<= 64 KB per tile) are combined in-launch
+    return int(max(1, min(4, K // 64, 128 // tiles)))
 
 
 def wgrad_splits(M, N, K):

@@ -67,6 +67,40 @@ def test_linear_fwd_bwd_vs_torch_fp32(M, N, K, gemm_mode):
     assert rel_err(bd.grad, br.grad) < TOL
 
 
+@pytest.mark.parametrize("M,N,K,epi,split", [
+    (64, 1024, 256, 0, False), (64, 256, 1024, 3, False), (3, 70, 300, 1, False), (64, 6, 40, 0, False),
+    (130, 200, 520, 0, True), (200, 128, 1024, 3, True)])
+def test_few_row_gemms(M, N, K, epi, split):
+    """M <= 64 (the T = 1 decode's batch rows) runs the register-fed exact-f32 MFMA kernel
+    (gemm_rows_kernel); a few-tile product with K >= 512 runs split-K with the slabs combined by
+    the last K slice of each tile (mrg_gemm_f32_ex counters).  Three back-to-back calls check
+    that the tickets return to zero and that both are bitwise repeatable."""
+    from multimodalreactiongeneration_amd import functional as Fn
+    assert (Fn.act_splits(M, N, K) > 1) == split
+    g = torch.Generator().manual_seed(M * N + K)
+    a = torch.randn(M, K, generator=g)
+    w = torch.randn(N, K, generator=g) / math.sqrt(K)
+    bias = torch.randn(N, generator=g)
+    c0 = torch.randn(M, N, generator=g)
+    aux = torch.randn(M, N, generator=g)
+    ad, wd, bd, auxd = a.to(DEV), w.to(DEV), bias.to(DEV), aux.to(DEV)
+    outs = []
+    for _ in range(3):
+        c = c0.to(DEV)
+        Fn.gemm(M, N, K, Fn._ptr(ad), 0, K, Fn._ptr(wd), 1, K, Fn._ptr(c), N, beta=0.5, bias=Fn._ptr(bd),
+                epi=epi, aux=Fn._ptr(auxd) if epi >= 2 else None, ldaux=N, device=DEV)
+        outs.append(c)
+    torch.cuda.synchronize()
+    ref = a.double() @ w.double().t() + 0.5 * c0.double() + bias.double()
+    if epi == 1:
+        ref = ref.clamp_min(0)
+    elif epi == 3:
+        ref = ref + aux.double()
+    assert rel_err(outs[0], ref) < TOL
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[1], outs[2])
+    assert int(Fn._counters(DEV).abs().sum()) == 0
+
+
 @pytest.mark.parametrize("rows,N,In,splits,time_shift", [
     (19200, 1024, 256, 32, False), (19200, 256, 256, 120, False), (1000, 70, 45, 1, False),
     (777, 130, 33, 5, False), (64 * 299, 1024, 256, 16, True)])
