@@ -214,33 +214,42 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
       tk.load(kb_, a.k_ts, k0 + TT, a.Tk);
       tv.load(vb_, a.v_ts, k0 + TT, a.Tk);
     }
+    // 32 keys per online-softmax update: two independent S^T sub-tiles (four MFMA chains), one
+    // max / sum reduction and one rescale of O per pair
 #pragma unroll
-    for (int sub = 0; sub < TT / 16; ++sub) {
-      const int kb = k0 + sub * 16;
+    for (int sp = 0; sp < TT / 16; sp += 2) {
+      const int kb = k0 + sp * 16;
       if (kb >= klim) break;
-      f32x4 s4 = qk16<D>(Ks, sub * 16, qreg, lq, lg);
-      float sv[4];
+      const bool two = kb + 16 < klim;  // wave-uniform: the second sub-tile has visible keys
+      f32x4 s4[2];
+      s4[0] = qk16<D>(Ks, sp * 16, qreg, lq, lg);
+      s4[1] = two ? qk16<D>(Ks, sp * 16 + 16, qreg, lq, lg) : f32x4{0.f, 0.f, 0.f, 0.f};
+      float sv[8];
       float mx = -INFINITY;
-      if (!pad && kb + 16 <= wmin) {  // every query of the wave sees all 16 keys
 #pragma unroll
-        for (int r = 0; r < 4; ++r) { sv[r] = s4[r]; mx = fmaxf(mx, sv[r]); }
-      } else {
+      for (int h = 0; h < 2; ++h) {
+        const int kh = kb + 16 * h;
+        if (!pad && kh + 16 <= wmin) {  // every query of the wave sees all 16 keys
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int kl = sub * 16 + lg * 4 + r;
-          const bool vis = (k0 + kl < kmax) && !(qp && Kp[kl]);
-          sv[r] = vis ? s4[r] : -INFINITY;
-          mx = fmaxf(mx, sv[r]);
+          for (int r = 0; r < 4; ++r) { sv[4 * h + r] = s4[h][r]; mx = fmaxf(mx, sv[4 * h + r]); }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int kl = (sp + h) * 16 + lg * 4 + r;
+            const bool vis = (k0 + kl < kmax) && !(qp && Kp[kl]);
+            sv[4 * h + r] = vis ? s4[h][r] : -INFINITY;
+            mx = fmaxf(mx, sv[4 * h + r]);
+          }
         }
       }
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mn = fmaxf(m, mx);
       const float alpha = (mn == -INFINITY) ? 1.0f : __expf(m - mn);
-      float p[4];
+      float p[8];
       float ps = 0.0f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+      for (int r = 0; r < 8; ++r) {
         p[r] = (sv[r] == -INFINITY) ? 0.0f : __expf(sv[r] - mn);
         ps += p[r];
       }
@@ -251,11 +260,16 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
       for (int dt = 0; dt < C::DT; ++dt) o[dt] *= alpha;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        float vv[C::DT];
-        col_operands<D, C::SV>(Vs, sub * 16 + 4 * lg + s, lq, vv);
+      for (int h = 0; h < 2; ++h) {
+        if (h == 1 && !two) break;
 #pragma unroll
-        for (int dt = 0; dt < C::DT; ++dt) o[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[dt], p[s], o[dt], 0, 0, 0);
+        for (int s = 0; s < 4; ++s) {
+          float vv[C::DT];
+          col_operands<D, C::SV>(Vs, (sp + h) * 16 + 4 * lg + s, lq, vv);
+#pragma unroll
+          for (int dt = 0; dt < C::DT; ++dt)
+            o[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[dt], p[4 * h + s], o[dt], 0, 0, 0);
+        }
       }
     }
   }
