@@ -189,6 +189,23 @@ int mrg_adamw_step(float* params, const float* grads, float* exp_avg, float* exp
                    float* step_lr, float weight_decay, float beta1, float beta2, float eps,
                    hipStream_t stream);
 
+/* ---------------------------------------------------------------- features (data loader)
+ * AudioPreprocessor (mr_gen/utils/preprocess/audio.py:6-67).  The power spectrum comes from one
+ * GEMM of the frames (read in place from the waveform, row stride `hop`) with the windowed DFT
+ * basis [2*NF, nfft] (cos rows then sin rows); mrg_fbank_finish turns spec [F][spec_ld] into
+ * out[f] = [log(max(mel_j, 1e-6)) for j < NM, log(max(sum_n frame_f[n]^2, 1e-10))]
+ * (MelSpectrogram + log, audio.py:33-35; compute_log_power, :43-56), melfb [NF][NM], where
+ * frame f starts at wave + (f / frames_per_clip) * clip_len + (f % frames_per_clip) * hop
+ * (equal-length clips stacked: one launch for a batch; one clip: frames_per_clip = F).
+ * mrg_feature_delta stacks [x[d:], delta1[d-1:], delta2] (compute_delta, audio.py:58-67,
+ * motion_nx.py:49-58) for order d in 0..2 over nclip sequences x [nclip][T][C] (row stride
+ * ldx): out [nclip][T-d][C*(d+1)].                                                           */
+int mrg_fbank_finish(int F, int NF, int NM, const float* spec, long spec_ld, const float* melfb,
+                     const float* wave, long hop, int nfft, int frames_per_clip, long clip_len,
+                     float* out, long out_ld, hipStream_t stream);
+int mrg_feature_delta(int nclip, int T, int C, const float* x, long ldx, int order, float* out,
+                      hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

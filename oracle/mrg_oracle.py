@@ -399,3 +399,64 @@ def run_train_step(loss_fn, sd: SD, optim_cfg, *args, **kw):
     after = {k: p.detach().clone() for k, p in params.items()}
     adamw_step(after, grads, {}, optim_cfg["lr"], optim_cfg["weight_decay"])
     return loss.detach(), y.detach(), grads, after
+
+
+# ---------------------------------------------------------- data-loader features
+def melscale_fbanks_htk(n_freqs: int, f_min: float, f_max: float, n_mels: int, sample_rate: int) -> Tensor:
+    """Triangular mel filterbank [n_freqs, n_mels] as torchaudio.functional.melscale_fbanks
+    (norm=None, mel_scale="htk") builds it for transforms.MelSpectrogram (audio.py:16-22).
+
+    torchaudio is a third-party dependency the reference does not pin (its Docker base,
+    pytorch 23.04, ships torchaudio 2.1) and it is absent here, so this restates its published
+    algorithm: linear frequency grid, n_mels + 2 points equally spaced in HTK mel
+    (2595 log10(1 + f / 700)), and min(down, up) slopes clamped at 0; float32 throughout.
+    Parity of this part is UNPINNED (no fixture can be produced without torchaudio).
+    """
+    all_freqs = torch.linspace(0, sample_rate // 2, n_freqs)
+    m_min = 2595.0 * math.log10(1.0 + f_min / 700.0)
+    m_max = 2595.0 * math.log10(1.0 + f_max / 700.0)
+    m_pts = torch.linspace(m_min, m_max, n_mels + 2)
+    f_pts = 700.0 * (10 ** (m_pts / 2595.0) - 1.0)
+    f_diff = f_pts[1:] - f_pts[:-1]
+    slopes = f_pts.unsqueeze(0) - all_freqs.unsqueeze(1)
+    down = (-1.0 * slopes[:, :-2]) / f_diff[:-1]
+    up = slopes[:, 2:] / f_diff[1:]
+    return torch.clamp(torch.min(down, up), min=0.0)
+
+
+def compute_log_power(wave: Tensor, nfft: int, shift: int) -> Tensor:
+    """AudioPreprocessor.compute_log_power (audio.py:43-56): per-frame log of the raw frame's
+    energy, frame by frame as the reference loops."""
+    num_frames = (len(wave) - nfft) // shift + 1
+    out = torch.zeros(num_frames)
+    for f in range(num_frames):
+        s = torch.sum(torch.pow(wave[f * shift:f * shift + nfft], 2))
+        out[f] = torch.log(torch.clamp(s, 1e-10))
+    return out
+
+
+def compute_delta(x: Tensor, delta_order: int) -> Tensor:
+    """compute_delta (audio.py:58-67, motion_nx.py:49-58)."""
+    if delta_order == 0:
+        return x
+    d1 = x[1:] - x[:-1]
+    if delta_order == 1:
+        return torch.cat([x[1:], d1], dim=1)
+    d2 = d1[1:] - d1[:-1]
+    if delta_order == 2:
+        return torch.cat([x[2:], d1[1:], d2], dim=1)
+    raise ValueError("delta_order must be 0, 1 or 2")
+
+
+def audio_features(wave: Tensor, sample_rate: int, nfft: int, shift: int, nmels: int, delta_order: int) -> Tensor:
+    """AudioPreprocessor.__call__ after the file read (audio.py:25-41): MelSpectrogram(n_fft,
+    hop, n_mels, center=False) = |STFT|^2 with a periodic Hann window, mel projection, log with
+    the two clamps, the log power as an extra row, transpose, deltas."""
+    spec = torch.stft(wave, n_fft=nfft, hop_length=shift, win_length=nfft, window=torch.hann_window(nfft),
+                      center=False, normalized=False, onesided=True, return_complex=True).abs().pow(2.0)
+    fb = melscale_fbanks_htk(nfft // 2 + 1, 0.0, float(sample_rate // 2), nmels, sample_rate)
+    mel = torch.matmul(spec.transpose(-1, -2), fb).transpose(-1, -2)
+    fbank = torch.log(torch.clamp(torch.clamp(mel, 1e-10), 1e-6) * 1)
+    power = compute_log_power(wave, nfft, shift)
+    fbank = torch.cat([fbank, power.unsqueeze(0)], dim=0).T.to(torch.float32)
+    return compute_delta(fbank, delta_order)

@@ -282,6 +282,46 @@ def state_dict_keys():
     print("wrote state_dict_keys", {k: len(v) for k, v in res.items()})
 
 
+def feature_cases():
+    """Data-loader features: the reference's compute_log_power (audio.py:43-56,
+    a per-frame Python loop) and compute_delta (audio.py:58-67) on a synthetic 16 kHz waveform,
+    and MotionPreprocessorNX.__call__ (motion_nx.py:14-58) on a synthetic angle/centroid npz.
+    The MelSpectrogram part needs torchaudio, which is absent: not pinned here."""
+    import tempfile
+    from ref_harness import load_preprocessors, AttrDict
+    P = load_preprocessors()
+    rs = np.random.RandomState(21)
+    n = 16000 * 13 // 10
+    t = np.arange(n) / 16000.0
+    wave = (0.1 * rs.randn(n) + 0.3 * np.sin(2 * np.pi * 220 * t) + 0.2 * np.sin(2 * np.pi * 1250 * t)
+            * (t > 0.4)).astype(np.float32)
+    wave[4000:6000] = 0.0  # a silent stretch: the 1e-10 / 1e-6 clamps are live
+    out = {"wave": wave}
+    ap = object.__new__(P.AudioPreprocessor)
+    ap.nfft, ap.shift = 400, 160
+    out["log_power"] = _np(ap.compute_log_power(torch.from_numpy(wave)))
+    x = torch.from_numpy(rs.randn(50, 27).astype(np.float32))
+    out["delta_in"] = _np(x)
+    for d in (0, 1, 2):
+        ap.delta_order = d
+        out[f"delta{d}"] = _np(ap.compute_delta(x))
+    N = 40
+    mz = {"angle": rs.randn(N, 3), "centroid": rs.randn(N, 3), "angle_std": rs.rand(3) + 0.5,
+          "angle_mean": rs.randn(3), "centroid_std": rs.rand(3) + 0.5, "centroid_mean": rs.randn(3)}
+    for k, v in mz.items():
+        out[f"npz/{k}"] = v
+    with tempfile.TemporaryDirectory() as tmp:
+        path = os.path.join(tmp, "m.npz")
+        np.savez(path, **mz)
+        for by_std in (False, True):
+            for d in (0, 2):
+                mp = P.MotionPreprocessorNX(AttrDict(delta_order=d, use_centroid=True, use_angle=True,
+                                                     train_by_std=by_std))
+                out[f"motion/std{int(by_std)}/d{d}"] = _np(mp(path, 3, 33, 2))
+    np.savez_compressed(os.path.join(HERE, "features.npz"), **out)
+    print("wrote features")
+
+
 def generation_cases():
     metaformer_generation_case("metaformer_gen_r2_pad", 32, 2, 2, 16, B=3, T=6, lead=2, ratio=2,
                                lengths=[6, 5, 4], seed=3)
@@ -291,7 +331,11 @@ if __name__ == "__main__":
     if sys.argv[1:] == ["generation"]:  # only the generation fixtures (the others stay as committed)
         generation_cases()
         sys.exit(0)
+    if sys.argv[1:] == ["features"]:
+        feature_cases()
+        sys.exit(0)
     generation_cases()
+    feature_cases()
     mask_cases()
     op_cases()
     state_dict_keys()

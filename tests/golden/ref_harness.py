@@ -101,3 +101,28 @@ def load_reference():
                                SimpleLSTM=S.SimpleLSTM, gen_attention_mask=gen_attention_mask)
     _LOADED["ns"] = ns
     return ns
+
+
+def load_preprocessors():
+    """The reference's AudioPreprocessor / MotionPreprocessorNX classes (mr_gen/utils/preprocess).
+
+    torchaudio is not installed: ``torchaudio.transforms`` and the soundfile backend are
+    registered as empty stand-ins so audio.py imports; only the pure-torch methods
+    (compute_log_power, compute_delta) are exercised through them.  MotionPreprocessorNX needs
+    only numpy / torch and runs unchanged.
+    """
+    import importlib.util
+    sys.dont_write_bytecode = True
+    _mod("torchaudio")
+    _mod("torchaudio.transforms", MelSpectrogram=None)
+    _mod("torchaudio._backend")
+    _mod("torchaudio._backend.soundfile_backend", load=None)
+    base = os.path.join(REF_ROOT, "mr_gen", "utils", "preprocess")
+    out = {}
+    for name in ("audio", "motion_nx"):
+        spec = importlib.util.spec_from_file_location(f"_ref_preprocess_{name}", os.path.join(base, name + ".py"))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        out[name] = mod
+    return types.SimpleNamespace(AudioPreprocessor=out["audio"].AudioPreprocessor,
+                                 MotionPreprocessorNX=out["motion_nx"].MotionPreprocessorNX)

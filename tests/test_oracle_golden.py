@@ -222,3 +222,41 @@ def test_metaformer_generation(mode):
     with torch.no_grad():
         pred = O.metaformer_prediction(sd, cfg["model"], batch, mask)
     assert rel_err(pred, d[f"pred/{mode}"]) < TOL
+
+
+def test_feature_log_power_and_deltas_golden():
+    """compute_log_power (audio.py:43-56) and compute_delta (audio.py:58-67) as the reference
+    itself computed them (tests/golden/features.npz): bit-exact."""
+    d = load("features")
+    lp = O.compute_log_power(torch.from_numpy(d["wave"]), 400, 160)
+    assert torch.equal(lp, torch.from_numpy(d["log_power"]))
+    x = torch.from_numpy(d["delta_in"])
+    for k in range(3):
+        assert torch.equal(O.compute_delta(x, k), torch.from_numpy(d[f"delta{k}"])), k
+
+
+def test_mel_filterbank_restatement_properties():
+    """The torchaudio HTK filterbank restatement (parity unpinned: torchaudio is absent):
+    triangles of peak <= 1 with successive, overlapping supports covering 0..sr/2."""
+    fb = O.melscale_fbanks_htk(201, 0.0, 8000.0, 26, 16000)
+    assert fb.shape == (201, 26) and fb.dtype == torch.float32
+    assert float(fb.min()) == 0.0 and float(fb.max()) <= 1.0
+    peaks = fb.argmax(0)
+    assert bool((peaks[1:] > peaks[:-1]).all())
+    assert bool((fb.sum(1)[1:-1] > 0).all())
+
+
+def test_feature_constants_match_restatement():
+    """The product's constant tables (features.py, built on the host) against the oracle:
+    the filterbank equals the restatement and the DFT basis reproduces |torch.stft|^2."""
+    from multimodalreactiongeneration_amd import features as FT
+    assert torch.equal(FT.melscale_fbanks(201, 0.0, 8000.0, 40, 16000), O.melscale_fbanks_htk(201, 0.0, 8000.0, 40, 16000))
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(400 + 160 * 4, generator=g, dtype=torch.float64)
+    basis = FT.dft_basis(400).double()
+    frames = x.unfold(0, 400, 160)
+    spec = frames @ basis.t()
+    p = spec[:, :201] ** 2 + spec[:, 201:] ** 2
+    ref = torch.stft(x, 400, 160, 400, torch.hann_window(400, dtype=torch.float64), center=False,
+                     return_complex=True).abs().pow(2).t()
+    assert rel_err(p, ref) < 1e-6
