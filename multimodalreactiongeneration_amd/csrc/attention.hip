@@ -177,8 +177,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) float Ks[TT * C::SA];
   __shared__ __attribute__((aligned(16))) float Vs[TT * C::SV];
   __shared__ unsigned char Kp[TT];
-  const int b = blockIdx.z, h = blockIdx.y;
-  const int q0 = blockIdx.x * 64;
+  // grid (heads, B, query blocks), the last (most keys under the causal mask) dispatched first
+  const int h = blockIdx.x, b = blockIdx.y;
+  const int q0 = (gridDim.z - 1 - blockIdx.z) * 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int lq = lane & 15, lg = lane >> 4;
   const int qi = q0 + wave * 16 + lq;
@@ -295,8 +296,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) float Ks[TT * C::SA];
   __shared__ __attribute__((aligned(16))) float Vs[TT * C::SA];
   __shared__ unsigned char Kp[TT];
-  const int b = blockIdx.z, h = blockIdx.y;
-  const int q0 = blockIdx.x * 64;
+  // grid (heads, B, query blocks), the last (most keys under the causal mask) dispatched first
+  const int h = blockIdx.x, b = blockIdx.y;
+  const int q0 = (gridDim.z - 1 - blockIdx.z) * 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int lq = lane & 15, lg = lane >> 4;
   const int qi = q0 + wave * 16 + lq;
@@ -396,8 +398,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) float Ds[TT * C::SA];
   __shared__ float Ls[TT], Dl[TT];
   __shared__ unsigned char Qp[TT];
-  const int b = blockIdx.z, h = blockIdx.y;
-  const int kb0 = blockIdx.x * 64;
+  // grid (heads, B, key blocks), the first (seen by the most queries) dispatched first
+  const int h = blockIdx.x, b = blockIdx.y;
+  const int kb0 = blockIdx.z * 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int lk = lane & 15, lg = lane >> 4;
   const int kj = kb0 + wave * 16 + lk;
@@ -546,7 +549,7 @@ MRG_API int mrg_attention_fwd(int B, int Hh, int Tq, int Tk, int D,
               "attention fwd: K/V rows must be 16-B aligned (strides multiple of 4 floats)");
   AttnArgs a = attn_base(B, Hh, Tq, Tk, q, q_bs, q_ts, k, k_bs, k_ts, v, v_bs, v_ts, o, o_bs, o_ts, lse,
                          qpad, kpad, causal, scale);
-  dim3 grid((Tq + 63) / 64, Hh, B);
+  dim3 grid(Hh, B, (Tq + 63) / 64);
   MRG_ATTN_DISPATCH(attn_fwd_kernel, grid, a);
   return check_launch("attn_fwd_kernel");
 }
@@ -572,10 +575,10 @@ MRG_API int mrg_attention_bwd(int B, int Hh, int Tq, int Tk, int D,
   a.dout = dout; a.do_bs = do_bs; a.do_ts = do_ts; a.dlt = workspace;
   a.dq = dq; a.dq_bs = dq_bs; a.dq_ts = dq_ts; a.dk = dk; a.dk_bs = dk_bs; a.dk_ts = dk_ts;
   a.dv = dv; a.dv_bs = dv_bs; a.dv_ts = dv_ts;
-  dim3 gq((Tq + 63) / 64, Hh, B);
+  dim3 gq(Hh, B, (Tq + 63) / 64);
   MRG_ATTN_DISPATCH(attn_bwd_dq_kernel, gq, a);  // also writes delta = rowsum(dO * O) to the workspace
   if (check_launch("attn_bwd_dq_kernel")) return 1;
-  dim3 gk((Tk + 63) / 64, Hh, B);
+  dim3 gk(Hh, B, (Tk + 63) / 64);
   MRG_ATTN_DISPATCH(attn_bwd_dkv_kernel, gk, a);
   return check_launch("attn_bwd_dkv_kernel");
 }
