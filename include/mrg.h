@@ -205,6 +205,11 @@ int mrg_fbank_finish(int F, int NF, int NM, const float* spec, long spec_ld, con
                      float* out, long out_ld, hipStream_t stream);
 int mrg_feature_delta(int nclip, int T, int C, const float* x, long ldx, int order, float* out,
                       hipStream_t stream);
+/* collate_fn (lstmformer/dataloader.py:114-121): pack_sequence + pad_packed_sequence with
+ * padding_value -100.  seqs: device table of B pointers to contiguous [lens[b], F] rows; lens:
+ * device int[B]; out [B, Tmax, F].                                                            */
+int mrg_pad_sequences(int B, int Tmax, int F, const float* const* seqs, const int* lens, float pad,
+                      float* out, hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -61,6 +61,7 @@ SIGNATURES = {
     "mrg_lstm_cell_bwd": (c_int, [c_int, c_int, P, P, P, P, c_long, P, P, P, P, P]),
     "mrg_fbank_finish": (c_int, [c_int, c_int, c_int, P, c_long, P, P, c_long, c_int, c_int, c_long, P, c_long, P]),
     "mrg_feature_delta": (c_int, [c_int, c_int, c_int, P, c_long, c_int, P, P]),
+    "mrg_pad_sequences": (c_int, [c_int, c_int, c_int, P, P, c_float, P, P]),
     "mrg_lstm_debug_stamps": (c_int, [P]),
     "mrg_attention_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int,
                                   P, c_long, c_long, P, c_long, c_long, P, c_long, c_long,

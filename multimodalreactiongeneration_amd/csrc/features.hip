@@ -111,3 +111,27 @@ MRG_API int mrg_feature_delta(int nclip, int T, int C, const float* x, long ldx,
   feature_delta_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(nclip, T, C, x, ldx, order, out);
   return check_launch("feature_delta_kernel");
 }
+
+// ---------------------------------------------------------------------------------------------
+// collate_fn (lstmformer/dataloader.py:114-121: pack_sequence + pad_packed_sequence(batch_first,
+// padding_value=-100)): B variable-length [len_b, F] sequences -> out [B, Tmax, F], rows past
+// len_b filled with `pad`.  Sequence b's rows are read from seqs[b] (device pointer table).
+__global__ __launch_bounds__(256) void pad_sequences_kernel(int B, int Tmax, int F, const float* const* seqs,
+                                                            const int* lens, float pad, float* out) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const long per = (long)Tmax * F;
+  if (i >= (long)B * per) return;
+  const int b = i / per;
+  const long r = i - (long)b * per;
+  const int t = r / F;
+  out[i] = t < lens[b] ? seqs[b][r] : pad;
+}
+
+MRG_API int mrg_pad_sequences(int B, int Tmax, int F, const float* const* seqs, const int* lens, float pad,
+                              float* out, hipStream_t stream) {
+  MRG_REQUIRE(B >= 0 && Tmax >= 0 && F >= 0, "mrg_pad_sequences: bad sizes");
+  const long n = (long)B * Tmax * F;
+  if (n == 0) return 0;
+  pad_sequences_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(B, Tmax, F, seqs, lens, pad, out);
+  return check_launch("pad_sequences_kernel");
+}

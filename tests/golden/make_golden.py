@@ -322,6 +322,79 @@ def feature_cases():
     print("wrote features")
 
 
+def dataset_cases():
+    """Segment dataset + collate (lstmformer/dataloader.py:20-121).  The
+    reference's own HeadMotionDatasetNX.__getitem__ orchestrates a synthetic segment (one-line
+    JSON in DataBuilderNX's format, databuild_nx.py:296-342; a 16-bit PCM wav; two angle/centroid
+    npz files) with its MotionPreprocessorNX and, for the audio (torchaudio absent), the oracle's
+    restatement; its collate_fn pads a ragged batch."""
+    import tempfile
+    import wave as _wave
+    from ref_harness import load_preprocessors, AttrDict
+    from oracle import mrg_oracle as O
+    import mr_gen.model.lstmformer.dataloader as DL
+    P = load_preprocessors()
+    rs = np.random.RandomState(33)
+    out = {}
+    pcm = (rs.randn(16000 * 2) * 2500).astype(np.int16)
+    out["files/partner_wav"] = pcm
+    npzs = {}
+    for who in ("partner", "self"):
+        npzs[who] = {"angle": rs.randn(300, 3), "centroid": rs.randn(300, 3), "angle_std": rs.rand(3) + 0.5,
+                     "angle_mean": rs.randn(3), "centroid_std": rs.rand(3) + 0.5, "centroid_mean": rs.randn(3)}
+        for k, v in npzs[who].items():
+            out[f"files/{who}_npz/{k}"] = v
+    seg = {"partner_motion": {"path": "partner.npz", "seq": {"start": 70, "end": 122, "stride": 1},
+                              "lead": {"start": 58, "end": 70, "stride": 1}, "offset": 10, "delta_order": 2},
+           "partner_audio": {"path": "partner.wav", "seq": {"start": 4000, "end": 12560, "stride": 1},
+                             "lead": {"start": 2000, "end": 4160, "stride": 1}, "delta_order": 2},
+           "self_motion": {"path": "self.npz", "seq": {"start": 70, "end": 123, "stride": 1},
+                           "lead": {"start": 58, "end": 70, "stride": 1}, "offset": 0, "delta_order": 2},
+           "self_audio": None,
+           "target": {"shift_real_seq": 1, "shift_input_seq": 1, "delta_order": 2}}
+    out["segment_json"] = np.array(json.dumps(seg))
+    audio_cfg = AttrDict(nfft=400, shift=160, nmels=26, sample_rate=16000, delta_order=2)
+    motion_cfg = AttrDict(delta_order=2, use_centroid=True, use_angle=True, train_by_std=False)
+
+    class OracleAudio:  # the reference call signature; reading + oracle features (torchaudio absent)
+        def __init__(self, cfg):
+            self.cfg = cfg
+
+        def __call__(self, path, start, end):
+            with _wave.open(path, "rb") as f:
+                f.setpos(start)
+                x = np.frombuffer(f.readframes(end - start), "<i2").astype(np.float32) / 32768.0
+            c = self.cfg
+            return O.audio_features(torch.from_numpy(x), c.sample_rate, c.nfft, c.shift, c.nmels, c.delta_order)
+    DL.AudioPreprocessor, DL.MotionPreprocessorNX = OracleAudio, P.MotionPreprocessorNX
+    with tempfile.TemporaryDirectory() as tmp:
+        with _wave.open(os.path.join(tmp, "partner.wav"), "wb") as f:
+            f.setnchannels(1)
+            f.setsampwidth(2)
+            f.setframerate(16000)
+            f.writeframes(pcm.tobytes())
+        for who in ("partner", "self"):
+            np.savez(os.path.join(tmp, f"{who}.npz"), **npzs[who])
+        s2 = json.loads(json.dumps(seg))
+        for k in ("partner_motion", "partner_audio", "self_motion"):
+            s2[k]["path"] = os.path.join(tmp, s2[k]["path"])
+        with open(os.path.join(tmp, "seg_0001.json"), "w", encoding="utf-8") as f:
+            f.write(json.dumps(s2) + "\n")
+        ds = DL.HeadMotionDatasetNX(tmp, motion_cfg, audio_cfg)
+        item = ds[0]
+    for i, t in enumerate(item):
+        out[f"item/{i}"] = _np(t)
+    batch = [tuple(torch.from_numpy(rs.randn(n, f).astype(np.float32)) for f in (3, 6)) for n in (5, 9, 2, 7)]
+    for b, it in enumerate(batch):
+        for m, t in enumerate(it):
+            out[f"collate_in/{b}/{m}"] = _np(t)
+    for m, (padded, lens) in enumerate(DL.collate_fn(batch)):
+        out[f"collate_out/{m}"] = _np(padded)
+        out[f"collate_len/{m}"] = lens.numpy()
+    np.savez_compressed(os.path.join(HERE, "dataset.npz"), **out)
+    print("wrote dataset", [tuple(t.shape) for t in item])
+
+
 def generation_cases():
     metaformer_generation_case("metaformer_gen_r2_pad", 32, 2, 2, 16, B=3, T=6, lead=2, ratio=2,
                                lengths=[6, 5, 4], seed=3)
@@ -334,8 +407,12 @@ if __name__ == "__main__":
     if sys.argv[1:] == ["features"]:
         feature_cases()
         sys.exit(0)
+    if sys.argv[1:] == ["dataset"]:
+        dataset_cases()
+        sys.exit(0)
     generation_cases()
     feature_cases()
+    dataset_cases()
     mask_cases()
     op_cases()
     state_dict_keys()
