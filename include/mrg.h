@@ -130,6 +130,18 @@ int mrg_lstm_cell_bwd(int B, int H, const float* gates, const float* c, const fl
                       long dh_ld, const float* dh2, const float* dc, float* dG, float* dc0,
                       hipStream_t stream);
 
+/* GRU mixer (mixer_block.py:169-208, torch.nn.GRU gate order r, z, n), one time step: the step's
+ * products are GEMMs (gx = x W_ih^T + b_ih for all steps, gh = h_{t-1} W_hh^T per step), the cell
+ * fuses the rest.  fwd: h = (1-z) n + z h_{t-1}, saves gates (r, z, n) and ghn = gh_n + b_hn.
+ * bwd: dh = dy + dh_next; writes dgx, dgh (= dgx with the n column times r) and dhp = dh z (the
+ * caller's GEMM adds dgh W_hh).  hp / dy / dh_next nullable (zero).                          */
+int mrg_gru_cell_fwd(int B, int H, const float* gx, long gx_ld, const float* gh, const float* b_hh,
+                     const float* hp, long hp_ld, float* h, long h_ld, float* gates, long g_ld, float* ghn,
+                     long n_ld, hipStream_t stream);
+int mrg_gru_cell_bwd(int B, int H, const float* gates, long g_ld, const float* ghn, long n_ld, const float* hp,
+                     long hp_ld, const float* dy, long dy_ld, const float* dh_next, float* dgx, float* dgh,
+                     long d_ld, float* dhp, hipStream_t stream);
+
 /* Diagnostics only: record per-step phase clocks (s_memtime) of block 0 of the next
  * LSTM launches into buf ([T][8] u64); null disables.  Never in timed runs. */
 int mrg_lstm_debug_stamps(void* buf);

@@ -50,13 +50,13 @@ def _metrics(delta_order=0):
 
 def lstmformer_config(hidden=256, num_block=5, encoder_num_layer=5, num_heads=4,
                       bottleneck=64, nmels=39, delta_order=0, ratio=1, lr=5e-6,
-                      loss_type="huber"):
+                      loss_type="huber", emb_mixers=("lstm", "lstm", "lstm")):
     """Resolved mr_gen/model/lstmformer/config.yaml model section (+ bench overrides)."""
     model = AttrDict(
         main_modal_idx=2, hidden_size=hidden, num_block=num_block, dropout=0.0,
         num_layerd=1, encoder_num_layer=encoder_num_layer, num_internal_layer=1,
         residual=True, residual_layer_norm=True, bias=True,
-        emb_mixers=["lstm", "lstm", "lstm"],
+        emb_mixers=list(emb_mixers),  # config_gru.yaml:50-52: ["gru"] * 3
         bottleneck_size=bottleneck, nonlinearity="none", ffn_nonlinearity="relu",
         proj_size=0, num_heads=num_heads, add_bias_kv=False, add_zero_attn=False,
         max_context_len=10, repeat_with_encoder=False, interlayer_residual=False,

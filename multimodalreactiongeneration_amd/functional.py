@@ -749,6 +749,101 @@ def lstm_bidirectional_layer(x, fw, bw, h0=None, c0=None, force_bs=0):
 
 
 # ------------------------------------------------------------------ multi-head attention
+class _GRUFn(Function):
+    """One direction of one torch.nn.GRU layer (gate order r, z, n; mixer_block.py:169-208), batch
+    first: the input GEMM for all steps, then per step the few-row recurrent GEMM h W_hh^T and the
+    fused cell (gru.hip); backward runs the cell derivative and dh_{t-1} += dGH_t W_hh per step, then
+    the weight / bias / input gradients as GEMMs over all steps.  Returns (y [B, T, H], hT [B, H])."""
+
+    @staticmethod
+    def forward(ctx, reverse, x, w_ih, w_hh, b_ih, b_hh, h0):
+        _lib.require_device(x)
+        dev = x.device
+        B, T, In = x.shape
+        H = w_hh.shape[1]
+        H3 = 3 * H
+        lib = _lib.load()
+        x = x.contiguous()
+        gx = torch.empty(B, T, H3, device=dev, dtype=torch.float32)
+        gemm(B * T, H3, In, _ptr(x), 0, In, _ptr(w_ih), 1, In, _ptr(gx), H3, bias=_ptr(b_ih), device=dev)
+        y = torch.empty(B, T, H, device=dev, dtype=torch.float32)
+        gates = torch.empty(B, T, H3, device=dev, dtype=torch.float32)
+        ghn = torch.empty(B, T, H, device=dev, dtype=torch.float32)
+        gh = torch.empty(B, H3, device=dev, dtype=torch.float32)
+        zero = torch.zeros(B, H3, device=dev, dtype=torch.float32) if h0 is None else None
+        h0c = None if h0 is None else h0.contiguous()
+        prev = None
+        for t in (range(T - 1, -1, -1) if reverse else range(T)):
+            if prev is None:
+                hp, hp_ld = _ptr(h0c), H
+            else:
+                hp, hp_ld = _ptr(y, prev * H), T * H
+            if hp is not None:
+                gemm(B, H3, H, hp, 0, hp_ld, _ptr(w_hh), 1, H, _ptr(gh), H3, device=dev)
+            _lib.check(lib.mrg_gru_cell_fwd(B, H, _ptr(gx, t * H3), T * H3, _ptr(gh if hp is not None else zero),
+                                            _ptr(b_hh), hp, hp_ld, _ptr(y, t * H), T * H, _ptr(gates, t * H3), T * H3,
+                                            _ptr(ghn, t * H), T * H, _stream()), "gru cell fwd")
+            prev = t
+        hT = y[:, prev].clone() if T > 0 else (h0c.clone() if h0c is not None else torch.zeros(B, H, device=dev))
+        ctx.reverse = bool(reverse)
+        ctx.save_for_backward(x, w_ih, w_hh, b_ih, b_hh, h0c, y, gates, ghn)
+        ctx.set_materialize_grads(False)
+        return y, hT
+
+    @staticmethod
+    def backward(ctx, dy, dhT):
+        x, w_ih, w_hh, b_ih, b_hh, h0c, y, gates, ghn = ctx.saved_tensors
+        reverse = ctx.reverse
+        dev = x.device
+        B, T, In = x.shape
+        H = w_hh.shape[1]
+        H3 = 3 * H
+        lib = _lib.load()
+        dy = None if dy is None else dy.contiguous()
+        dGX = torch.empty(B, T, H3, device=dev, dtype=torch.float32)
+        dGH = torch.empty(B, T, H3, device=dev, dtype=torch.float32)
+        dh_next = None if dhT is None else dhT.contiguous()
+        for t in (range(T) if reverse else range(T - 1, -1, -1)):
+            pt = t + 1 if reverse else t - 1
+            if 0 <= pt < T:
+                hp, hp_ld = _ptr(y, pt * H), T * H
+            else:
+                hp, hp_ld = _ptr(h0c), H
+            dhp = torch.empty(B, H, device=dev, dtype=torch.float32)
+            _lib.check(lib.mrg_gru_cell_bwd(B, H, _ptr(gates, t * H3), T * H3, _ptr(ghn, t * H), T * H, hp, hp_ld,
+                                            _ptr(dy, t * H) if dy is not None else None, T * H, _ptr(dh_next),
+                                            _ptr(dGX, t * H3), _ptr(dGH, t * H3), T * H3, _ptr(dhp), _stream()),
+                       "gru cell bwd")
+            gemm(B, H, H3, _ptr(dGH, t * H3), 0, T * H3, _ptr(w_hh), 0, H, _ptr(dhp), H, beta=1.0, device=dev)
+            dh_next = dhp
+        need = ctx.needs_input_grad
+        dh0 = dh_next if (h0c is not None and need[6]) else None
+        _wgrad(_ptr(dGX), H3, _ptr(x), In, B * T, H3, In, _gbuf(w_ih), dev, gb=_gbuf(b_ih))
+        gw = _gbuf(w_hh)
+        if gw is not None and T > 1:
+            # sum_t dGH_t^T h_{t-1}: forward pairs (dGH[t], y[t-1]), reverse (dGH[t], y[t+1])
+            a_off = 0 if reverse else H3
+            b_off = H if reverse else 0
+            _wgrad(_ptr(dGH, a_off), H3, _ptr(y, b_off), H, B * (T - 1), H3, H, gw, dev,
+                   dy_hi=T * H3, dy_div=T - 1, x_hi=T * H, x_div=T - 1)
+        if gw is not None and h0c is not None:
+            t0 = T - 1 if reverse else 0
+            gemm(H3, H, B, _ptr(dGH, t0 * H3), 1, T * H3, _ptr(h0c), 0, H, _ptr(gw), H, beta=1.0, device=dev)
+        gbh = _gbuf(b_hh)
+        if gbh is not None:
+            colsum(B * T, H3, _ptr(dGH), H3, _ptr(gbh), device=dev)
+        dx = None
+        if need[1]:
+            dx = torch.empty(B, T, In, device=dev, dtype=torch.float32)
+            gemm(B * T, In, H3, _ptr(dGX), 0, H3, _ptr(w_ih), 0, In, _ptr(dx), In, device=dev)
+        return None, dx, None, None, None, None, dh0
+
+
+def gru_layer(x, w_ih, w_hh, b_ih, b_hh, h0=None, reverse=False):
+    """One direction of one nn.GRU layer (batch_first).  Returns (y, hT)."""
+    return _GRUFn.apply(bool(reverse), x, w_ih, w_hh, b_ih, b_hh, h0)
+
+
 def visible_pairs(Tq, Tk, causal):
     """(query, key) pairs the block-causal rule admits per (sample, head) (gen_attention_mask rules)."""
     if not causal:

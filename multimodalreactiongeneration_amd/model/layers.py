@@ -198,6 +198,53 @@ class LSTM(nn.Module):
         return x, (torch.stack(hs), torch.stack(cs))
 
 
+class GRU(nn.Module):
+    """nn.GRU parameter layout (batch_first; gate order r, z, n) on the GRU cell kernels."""
+
+    def __init__(self, input_size, hidden_size, num_layers=1, bias=True, batch_first=True,
+                 dropout=0.0, bidirectional=False, device=None, dtype=None):
+        super().__init__()
+        if not batch_first:
+            _unsupported("GRU batch_first=False")
+        if not bias:
+            _unsupported("GRU without bias")
+        self.input_size, self.hidden_size, self.num_layers = input_size, hidden_size, num_layers
+        self.bidirectional, self.dropout, self.batch_first = bidirectional, dropout, batch_first
+        D = 2 if bidirectional else 1
+        k = 1.0 / math.sqrt(hidden_size)
+        for layer in range(num_layers):
+            in_sz = input_size if layer == 0 else hidden_size * D
+            for d in range(D):
+                sfx = f"l{layer}" + ("_reverse" if d else "")
+                for name, shape in ((f"weight_ih_{sfx}", (3 * hidden_size, in_sz)),
+                                    (f"weight_hh_{sfx}", (3 * hidden_size, hidden_size)),
+                                    (f"bias_ih_{sfx}", (3 * hidden_size,)),
+                                    (f"bias_hh_{sfx}", (3 * hidden_size,))):
+                    p = nn.Parameter(torch.empty(shape, device=device, dtype=dtype))
+                    nn.init.uniform_(p, -k, k)
+                    self.register_parameter(name, p)
+
+    def direction_params(self, layer, reverse=False):
+        sfx = f"l{layer}" + ("_reverse" if reverse else "")
+        return (getattr(self, f"weight_ih_{sfx}"), getattr(self, f"weight_hh_{sfx}"),
+                getattr(self, f"bias_ih_{sfx}"), getattr(self, f"bias_hh_{sfx}"))
+
+    def forward(self, x, hx=None):
+        if self.dropout and self.training and self.num_layers > 1:
+            _unsupported("GRU inter-layer dropout")
+        D = 2 if self.bidirectional else 1
+        hs = []
+        for layer in range(self.num_layers):
+            ys = []
+            for d in range(D):
+                h0 = None if hx is None else hx[layer * D + d]
+                y, hT = Fn.gru_layer(x, *self.direction_params(layer, bool(d)), h0, reverse=bool(d))
+                ys.append(y)
+                hs.append(hT)
+            x = ys[0] if D == 1 else torch.cat(ys, dim=-1)
+        return x, torch.stack(hs)
+
+
 class MultiheadAttention(nn.Module):
     """nn.MultiheadAttention parameter layout (kdim = vdim = embed_dim, batch_first)."""
 

@@ -3,8 +3,8 @@
 Same constructor arguments, module attribute names and forward tuple
 conventions as the reference (nn.Sequential-friendly tuples, the
 ``split_state`` state plumbing), so configs and checkpoints carry over.
-LSTM and MHA mixers run on libmrg.so.  The MLP and GRU mixers are outside
-the benchmarked path (unused by the BASELINE configs) and raise.
+LSTM, GRU and MHA mixers run on libmrg.so.  The MLP mixer is outside the
+benchmarked path (unused by the BASELINE configs) and raises.
 """
 from __future__ import annotations
 
@@ -15,7 +15,7 @@ import torch
 from torch import nn
 
 from .. import functional as Fn
-from .layers import LSTM, MHAforSequentail, ResidualConnection, FeedForward
+from .layers import GRU, LSTM, MHAforSequentail, ResidualConnection, FeedForward
 
 
 def split_state(state, prev_state):
@@ -114,8 +114,22 @@ class MLPMixer(Mixer):
 
 
 class GRUMixer(Mixer):
-    def __init__(self, *a, **k):
-        raise NotImplementedError("GRU mixer is outside the MI355X path (SURVEY §8f rank 4)")
+    """nn.GRU token mixer (mixer_block.py:169-208)."""
+
+    def __init__(self, input_size: int, hidden_size: int, num_layers: int = 1, batch_first: bool = True,
+                 dropout: float = 0.0, bidirectional: bool = False, bias: bool = True, device=None, dtype=None):
+        super().__init__()
+        if num_layers < 1:
+            raise ValueError("num_layers must be greater than 0.")
+        if bidirectional:
+            if hidden_size % 2 != 0:
+                raise ValueError("hidden_size must be even number when bidirectional is True.")
+            hidden_size //= 2
+        self.mixer = GRU(input_size, hidden_size, num_layers=num_layers, bias=bias, batch_first=batch_first,
+                         dropout=dropout, bidirectional=bidirectional, device=device, dtype=dtype)
+
+    def forward(self, x, hn=None):
+        return self.mixer(x, hn)
 
 
 class LSTMMixerBlock(MixerBlock):
@@ -136,6 +150,33 @@ class LSTMMixerBlock(MixerBlock):
     def lstm_params(self):
         m = self.mixer.module if isinstance(self.mixer, ResidualConnection) else self.mixer
         return m.mixer.direction_params(0)
+
+    def forward(self, x, hx=None, prev_hx=None):
+        if isinstance(x, (tuple, list)):
+            x, hx, prev_hx = x
+        elif not isinstance(x, torch.Tensor):
+            raise TypeError(f"x must be torch.Tensor or tuple or list, but got {type(x)}.")
+        first, hx, prev_hx = split_state(hx, prev_hx)
+        y, first = self.mixer(x, first)
+        y = self.feed_forward(y)
+        prev_hx.append(first)
+        return (y, hx, prev_hx)
+
+
+class GRUMixerBlock(MixerBlock):
+    """Residual GRU mixer + FeedForward (mixer_block.py:355-428)."""
+
+    def __init__(self, hidden_size: int, num_layers: int = 1, dropout: float = 0.0, batch_first: bool = True,
+                 bidirectional: bool = False, nonlinearity=None, residual: bool = False,
+                 residual_layer_norm: bool = False, bottleneck_size: int = None, bias: bool = True,
+                 device=None, dtype=None):
+        super().__init__()
+        self.mixer = GRUMixer(hidden_size, hidden_size, num_layers, batch_first, dropout, bidirectional, bias,
+                              device, dtype)
+        if residual:
+            self.mixer = ResidualConnection(self.mixer, residual_layer_norm, hidden_size)
+        self.feed_forward = FeedForward(hidden_size, bottleneck_size, None, nonlinearity, residual,
+                                        residual_layer_norm, bias, device, dtype)
 
     def forward(self, x, hx=None, prev_hx=None):
         if isinstance(x, (tuple, list)):
@@ -275,12 +316,35 @@ class MLPMixerLayerd(MixerLayerd):
         raise NotImplementedError("MLP mixer is outside the MI355X path (not in the BASELINE configs)")
 
 
-class GRUMixerLayerd(MixerLayerd):
-    def __init__(self, *a, **k):
-        raise NotImplementedError("GRU mixer is outside the MI355X path (SURVEY §8f rank 4)")
+class GRUMixerLayerd(_Layerd):
+    """num_layerd GRUMixerBlocks; returns the REST hx, like the LSTM layerd (mixer_block.py:679-761)."""
+
+    def __init__(self, hidden_size: int, input_projection: bool = False, input_projection_size: int = None,
+                 output_projection: bool = False, output_projection_size: int = None, num_layerd: int = 1,
+                 num_internal_layer: int = 1, dropout: float = 0.0, batch_first: bool = True,
+                 bidirectional: bool = False, nonlinearity=None, residual: bool = False,
+                 residual_layer_norm: bool = False, bottleneck_size: int = None, bias: bool = True,
+                 device=None, dtype=None):
+        super().__init__()
+        self._projections(hidden_size, input_projection, input_projection_size, output_projection,
+                          output_projection_size, bias)
+        self.mixer = nn.ModuleList([
+            GRUMixerBlock(hidden_size, num_internal_layer, dropout, batch_first, bidirectional, nonlinearity,
+                          residual, residual_layer_norm, bottleneck_size, bias, device, dtype)
+            for _ in range(num_layerd)])
+
+    def forward(self, x, hx=None, other=(None,)):
+        if self.input_projection is not None:
+            x = self.input_projection(x)
+        phx = None
+        for block in self.mixer:
+            x, hx, phx = block(x, hx, phx)
+        if self.output_projection is not None:
+            x = self.output_projection(x)
+        return (x, hx, other)
 
 
-_BLOCKS = {"mlp": None, "gru": None, "lstm": LSTMMixerBlock, "mha": MHAMixerBlock}
+_BLOCKS = {"mlp": None, "gru": GRUMixerBlock, "lstm": LSTMMixerBlock, "mha": MHAMixerBlock}
 _LAYERDS = {"mlp": MLPMixerLayerd, "gru": GRUMixerLayerd, "lstm": LSTMMixerLayerd, "mha": MHAMixerLayerd}
 
 
@@ -307,10 +371,7 @@ def _accepted(cls):
 
 _LAYERD_ARGS = {
     "lstm": _accepted(LSTMMixerLayerd), "mha": _accepted(MHAMixerLayerd),
-    "gru": ["hidden_size", "input_projection", "input_projection_size", "output_projection",
-            "output_projection_size", "num_layerd", "num_internal_layer", "dropout", "batch_first",
-            "bidirectional", "nonlinearity", "residual", "residual_layer_norm", "bottleneck_size", "bias",
-            "device", "dtype"],
+    "gru": _accepted(GRUMixerLayerd),
     "mlp": ["hidden_size", "input_projection", "input_projection_size", "output_projection",
             "output_projection_size", "num_layerd", "num_internal_layer", "nonlinearity", "residual",
             "residual_layer_norm", "bottleneck_size", "bias", "device", "dtype"],
@@ -323,7 +384,7 @@ def mixer_layerd_argments_select(mixer_type: str, hidden_size: int, **kw) -> dic
         raise ValueError(f"mixer_type must be in {list(_LAYERD_ARGS)}")
     cls = _LAYERDS[mixer_type]
     defaults = {}
-    if mixer_type in ("lstm", "mha"):
+    if mixer_type in ("lstm", "mha", "gru"):
         defaults = {k: v.default for k, v in inspect.signature(cls.__init__).parameters.items()
                     if k != "self" and v.default is not inspect.Parameter.empty}
     out = {k: defaults.get(k) for k in _LAYERD_ARGS[mixer_type]}

@@ -75,6 +75,29 @@ def lstm_layer(x: Tensor, w_ih: Tensor, w_hh: Tensor, b_ih: Tensor, b_hh: Tensor
     return torch.stack(ys, dim=1), h, c
 
 
+def gru_layer(x: Tensor, w_ih: Tensor, w_hh: Tensor, b_ih: Tensor, b_hh: Tensor,
+              h0: Optional[Tensor] = None, reverse: bool = False) -> Tuple[Tensor, Tensor]:
+    """One direction of one torch.nn.GRU layer (gate order r, z, n), batch_first: the op GRUMixer
+    calls (mixer_block.py:169-208).  n = tanh(W_in x + b_in + r * (W_hn h + b_hn))."""
+    B, T, _ = x.shape
+    H = w_hh.shape[1]
+    gx = F.linear(x, w_ih, b_ih)
+    h = x.new_zeros(B, H) if h0 is None else h0
+    ys: List[Optional[Tensor]] = [None] * T
+    for t in (range(T - 1, -1, -1) if reverse else range(T)):
+        gh = F.linear(h, w_hh, b_hh)
+        xr, xz, xn = gx[:, t].chunk(3, dim=-1)
+        hr, hz, hn = gh.chunk(3, dim=-1)
+        r = torch.sigmoid(xr + hr)
+        z = torch.sigmoid(xz + hz)
+        n = torch.tanh(xn + r * hn)
+        h = (1 - z) * n + z * h
+        ys[t] = h
+    if T == 0:
+        return x.new_zeros(B, 0, H), h
+    return torch.stack(ys, dim=1), h
+
+
 def lstm_stack(x: Tensor, sd: SD, prefix: str, num_layers: int, bidirectional: bool,
                hx: Optional[Tuple[Tensor, Tensor]] = None):
     """torch.nn.LSTM(num_layers, bidirectional, batch_first) over ``{prefix}weight_ih_l{k}[_reverse]``."""

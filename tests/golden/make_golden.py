@@ -65,10 +65,10 @@ def run_train_step(model, batch, out, save_params=True, full_grads=True):
 
 
 def metaformer_case(name, hidden, nb, enc, bn, B, T, lead, ratio, lengths=None, seed=0,
-                    full_width=False):
+                    full_width=False, **cfg_kw):
     model_cfg, optim, metrics = C.lstmformer_config(hidden=hidden, num_block=nb,
                                                     encoder_num_layer=enc, bottleneck=bn,
-                                                    ratio=ratio, lr=1e-3)
+                                                    ratio=ratio, lr=1e-3, **cfg_kw)
     torch.manual_seed(seed)
     m = R.Metaformer(model_cfg, optim, metrics)
     if full_width:
@@ -395,6 +395,13 @@ def dataset_cases():
     print("wrote dataset", [tuple(t.shape) for t in item])
 
 
+def gru_cases():
+    """lstmformer with config_gru.yaml's embedding mixers (["gru"] * 3, config_gru.yaml:50-52):
+    nn.GRU mixers in every embedding."""
+    metaformer_case("metaformer_gru_r2_pad", 32, 2, 2, 16, B=3, T=8, lead=2, ratio=2,
+                    lengths=[8, 6, 5], seed=4, emb_mixers=("gru", "gru", "gru"))
+
+
 def generation_cases():
     metaformer_generation_case("metaformer_gen_r2_pad", 32, 2, 2, 16, B=3, T=6, lead=2, ratio=2,
                                lengths=[6, 5, 4], seed=3)
@@ -410,9 +417,13 @@ if __name__ == "__main__":
     if sys.argv[1:] == ["dataset"]:
         dataset_cases()
         sys.exit(0)
+    if sys.argv[1:] == ["gru"]:
+        gru_cases()
+        sys.exit(0)
     generation_cases()
     feature_cases()
     dataset_cases()
+    gru_cases()
     mask_cases()
     op_cases()
     state_dict_keys()

@@ -260,3 +260,19 @@ def test_feature_constants_match_restatement():
     ref = torch.stft(x, 400, 160, 400, torch.hann_window(400, dtype=torch.float64), center=False,
                      return_complex=True).abs().pow(2).t()
     assert rel_err(p, ref) < 1e-6
+
+
+@pytest.mark.parametrize("rev,state", [(False, False), (True, True)])
+def test_gru_restatement_matches_nn_gru(rev, state):
+    """oracle.gru_layer vs torch.nn.GRU itself (the op GRUMixer wraps, mixer_block.py:193-201)."""
+    torch.manual_seed(5)
+    gru = torch.nn.GRU(7, 12, batch_first=True, bidirectional=rev)
+    x = torch.randn(3, 9, 7)
+    h0 = torch.randn(2 if rev else 1, 3, 12) if state else None
+    y, hn = gru(x, h0)
+    d = 1 if rev else 0
+    sfx = "_reverse" if rev else ""
+    w = [getattr(gru, f"{n}_l0{sfx}") for n in ("weight_ih", "weight_hh", "bias_ih", "bias_hh")]
+    yo, ho = O.gru_layer(x, *w, None if h0 is None else h0[d], reverse=rev)
+    assert rel_err(yo, y[..., d * 12:(d + 1) * 12]) < 1e-5
+    assert rel_err(ho, hn[d]) < 1e-5
