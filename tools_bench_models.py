@@ -1,6 +1,6 @@
 """Step times of the other BASELINE configs (not the headline bench line): eager fwd+bwd+AdamW.
 
-    python tools_bench_models.py [steps] [C2|C3|C3tf|gen|all] [graph]     (on a GPU box)
+    python tools_bench_models.py [steps] [C2|C3|C3tf|gen|gru|all] [graph]     (on a GPU box)
 
   graph=1 replays each step as one HIP graph (graphs.capture); C3's sampling mask then lives in a
   static device buffer refreshed from the host RNG draw before every replay.
@@ -57,6 +57,8 @@ def main():
     torch.manual_seed(0)
     if only == "gen":
         return main_gen(steps, out)
+    if only == "gru":
+        return main_gru(steps, out)
     if only and only != "C2":
         return main_lws(steps, only, out)
     mc, oc, me = C.simple_lstm_config()
@@ -74,6 +76,25 @@ def main():
     if not only:
         main_lws(steps, only, out)
         main_gen(steps, out)
+
+
+def main_gru(steps, out):
+    """lstmformer with config_gru.yaml's embedding mixers (["gru"] * 3), B=64 T=300 r=1 train step."""
+    from multimodalreactiongeneration_amd.model import Metaformer
+    mc, oc, me = C.lstmformer_config(ratio=1, emb_mixers=("gru", "gru", "gru"))
+    torch.manual_seed(0)
+    m = Metaformer(mc, oc, me).to(DEV)
+    opt = m.configure_optimizers()["optimizer"]
+    batch = make_batch(B=64, T=300, seed=1234, device=DEV)
+
+    def step():
+        opt.zero_grad()
+        m.training_step(list(batch))["loss"].backward()
+        opt.step()
+    ms = timed(step, steps)
+    key = "lstmformer_gru_B64_T300" + ("_graph" if GRAPH else "")
+    out[key] = {"ms_per_step": round(ms, 2), "frames_per_s": round(64 * 300 / ms * 1e3)}
+    print(json.dumps(out), flush=True)
 
 
 def main_gen(steps, out):
