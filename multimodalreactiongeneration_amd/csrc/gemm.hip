@@ -864,9 +864,10 @@ static void launch_tile_x6(GemmArgs a, int ta, int tb, bool va, bool vb, int spl
 // quarters and each wave's 4 lane groups contiguous sub-ranges of those (operands load as runs),
 // all loads of a chunk are in flight at once, and the 4 partial blocks are summed in LDS in a
 // fixed order before the epilogue.  Arithmetic: fp32 FMA chains (no bf16 split needed).
-template <int TB, int CH>
+template <int TA, int TB, int CH>
 __global__ __launch_bounds__(256) void gemm_rows_kernel(GemmArgs a) {
   __shared__ float red[4][16][17];
+  __shared__ float rsum[16][16];  // fused row sums of op(A) (TA: the bias gradient), per (wave, group)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, l16 = lane & 15;
   const int m0 = blockIdx.y * 16, n0 = blockIdx.x * 16;
@@ -875,24 +876,32 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(GemmArgs a) {
   const int ke = min(a.K, kb + KQ);
   const int m = m0 + l16, n = n0 + l16;
   const bool mv = m < a.M, nv = n < a.N;
-  const float* ap = a.A + (mv ? a.amap.off(m) : 0);
+  // A(m, k): row m of A (TA = 0) or element m of row k (TA = 1, A stored k-major)
+  const float* ap = a.A + (TA ? m : (mv ? a.amap.off(m) : 0));
   const float* bp = a.B + (TB ? (nv ? a.bmap.off(n) : 0) : n);
+  const bool sums = TA && a.asum_out && blockIdx.x == 0;
   f32x4v acc = f32x4v{0.f, 0.f, 0.f, 0.f};
+  float rs = 0.0f;
   for (int k0 = kb; k0 < ke; k0 += CH) {
     float av[CH], bv[CH];
 #pragma unroll
     for (int s = 0; s < CH; ++s) {
       const int k = k0 + s;
       const bool ok = k < ke;
-      av[s] = (ok && mv) ? ap[k] : 0.0f;
+      av[s] = (ok && mv) ? (TA ? ap[a.amap.off(k)] : ap[k]) : 0.0f;
       bv[s] = (ok && nv) ? (TB ? bp[k] : bp[a.bmap.off(k)]) : 0.0f;
     }
 #pragma unroll
     for (int s = 0; s < CH; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[s], acc, 0, 0, 0);
+    if (sums) {
+#pragma unroll
+      for (int s = 0; s < CH; ++s) rs += av[s];
+    }
   }
   // lane holds C[4g + i][l16] of this wave's partial block
 #pragma unroll
   for (int i = 0; i < 4; ++i) red[wave][4 * g + i][l16] = acc[i];
+  if (sums) rsum[wave * 4 + g][l16] = rs;
   __syncthreads();
   const int r = threadIdx.x >> 4, c = threadIdx.x & 15;
   const int mo = m0 + r, no = n0 + c;
@@ -900,18 +909,27 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(GemmArgs a) {
     const float v = ((red[0][r][c] + red[1][r][c]) + red[2][r][c]) + red[3][r][c];
     a.C[(long)mo * a.ldc + no] = apply_epi(a, v, mo, no);
   }
+  if (sums && threadIdx.x < 16 && m0 + (int)threadIdx.x < a.M) {  // bias gradient rows, fixed order
+    const int mm = m0 + threadIdx.x;
+    float t = 0.0f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) t += rsum[q][threadIdx.x];
+    a.asum_out[mm] = (a.asum_beta != 0.0f ? a.asum_beta * a.asum_out[mm] : 0.0f) + t;
+    if (a.asum_out2) a.asum_out2[mm] = (a.asum_beta != 0.0f ? a.asum_beta * a.asum_out2[mm] : 0.0f) + t;
+  }
 }
 
 static void launch_rows(const GemmArgs& a, hipStream_t s) {
   const dim3 grid((a.N + 15) / 16, (a.M + 15) / 16);
-  const int kq = (a.K + 15) / 16;
-  if (a.transB) {
-    if (kq <= 16) gemm_rows_kernel<1, 16><<<grid, 256, 0, s>>>(a);
-    else gemm_rows_kernel<1, 64><<<grid, 256, 0, s>>>(a);
-  } else {
-    if (kq <= 16) gemm_rows_kernel<0, 16><<<grid, 256, 0, s>>>(a);
-    else gemm_rows_kernel<0, 64><<<grid, 256, 0, s>>>(a);
+  const bool big = (a.K + 15) / 16 > 16;
+#define MRG_R(TA, TB)                                                                            \
+  if (a.transA == TA && a.transB == TB) {                                                        \
+    if (big) gemm_rows_kernel<TA, TB, 64><<<grid, 256, 0, s>>>(a);                               \
+    else gemm_rows_kernel<TA, TB, 16><<<grid, 256, 0, s>>>(a);                                   \
+    return;                                                                                      \
   }
+  MRG_R(0, 0) MRG_R(0, 1) MRG_R(1, 0) MRG_R(1, 1)
+#undef MRG_R
 }
 
 static int g_tile_override = -1;
@@ -1036,8 +1054,11 @@ MRG_API int mrg_gemm_f32_ex(int M, int N, int K, float alpha,
   const bool va = aligned(A, a.amap), vb = aligned(B, a.bmap);
   a.vec = ((((uintptr_t)C | (uintptr_t)bias | (uintptr_t)aux | (uintptr_t)workspace) & 15) == 0 && (ldc & 3) == 0 &&
            (!aux || (ldaux & 3) == 0) && (!a.ws || (N & 3) == 0)) ? 1 : 0;
-  // few-row products (x6 mode): exact f32 MFMA from registers, no split, no LDS staging
-  if (g_gemm_mode == 1 && !transA && M <= 64 && splits == 1 && !asum_out) {
+  // few-row products (x6 mode): exact f32 MFMA from registers, no split, no LDS staging: M <= 64
+  // rows of activations, or a weight gradient over <= 64 rows (K), its bias sums fused
+  if (g_gemm_mode == 1 && splits == 1 && ((!transA && M <= 64 && !asum_out) || (transA && K <= 64))) {
+    a.transA = transA ? 1 : 0;
+    a.transB = transB ? 1 : 0;
     launch_rows(a, stream);
     return check_launch("gemm_rows_kernel");
   }

@@ -103,7 +103,8 @@ def test_few_row_gemms(M, N, K, epi, split):
 
 @pytest.mark.parametrize("rows,N,In,splits,time_shift", [
     (19200, 1024, 256, 32, False), (19200, 256, 256, 120, False), (1000, 70, 45, 1, False),
-    (777, 130, 33, 5, False), (64 * 299, 1024, 256, 16, True)])
+    (777, 130, 33, 5, False), (64 * 299, 1024, 256, 16, True), (64, 1024, 256, 1, False),
+    (37, 130, 33, 1, False)])
 def test_weight_grad_with_fused_bias_sums(rows, N, In, splits, time_shift, gemm_mode):
     """gw += dY^T X and gb (+ gb2) += colsum(dY) in one mrg_gemm_f32_ex call, incl. a RowMap'd
     (time-shifted, [:, 1:] of [64, 300, F]) operand pair as the LSTM's dW_hh uses."""
