@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--wgrad-stream", type=int, default=1,
+                    help="weight-gradient GEMMs on a side stream (functional._side); 0 = one stream")
     ap.add_argument("--lstm-group", type=int, default=0, help="workgroups per LSTM row group at H=256 (8|16; 0 = library default)")
     return ap.parse_args()
 
@@ -133,6 +135,7 @@ def main():
     if args.lstm_group:
         from multimodalreactiongeneration_amd import _lib
         _lib.check(_lib.load().mrg_lstm_config(args.lstm_group), "mrg_lstm_config")
+    Fn.set_wgrad_stream(bool(args.wgrad_stream))
     torch.manual_seed(0)
     model = Metaformer(mc, oc, me).to(dev)
     broadcast_parameters(model)
@@ -194,12 +197,15 @@ def main():
     # live per-family kernel timing: HIP events recorded on the launch stream around every library
     # call of two eager steps right after the timed region (a graph replay cannot be bracketed);
     # each launch carries its algorithmic FLOPs (functional._probe), so achieved = FLOPs / time
+    # (weight gradients on the current stream here, so the brackets time uncontended launches)
     fams = tuple(FAMILIES)
+    side = Fn.set_wgrad_stream(False)
     if rank == 0:
         Fn.probe_start(*fams)
     for _ in range(2):      # every rank steps (the all-reduce is collective); rank 0 records
         step()
     per = Fn.probe_stop(with_work=True) if rank == 0 else {}
+    Fn.set_wgrad_stream(side)
     kernels, roof = {}, None
     if rank == 0:
         for f in fams:
@@ -231,7 +237,8 @@ def main():
         "config": {"workload": "lstmformer train step (fwd+Huber+bwd+AdamW), BASELINE configs[3]/[4]",
                    "model": "lstmformer H=256 blocks=5 enc_layers=5 heads=4 bottleneck=64 (13,052,678 params)",
                    "global_batch": args.batch * world, "seq_len": args.seq, "audio_ratio": args.ratio,
-                   "parallelism": f"dp{world}", "hip_graph": bool(args.graph)},
+                   "parallelism": f"dp{world}", "hip_graph": bool(args.graph),
+                   "wgrad_side_stream": bool(args.wgrad_stream)},
         "whole_step_roofline": {"bound": "mfma", "algorithmic_tflop_per_step": round(step_flop / 1e12, 4),
                                 "achieved_tflops": round(step_flop / (ms / 1000.0) / 1e12, 3),
                                 "peak": FP32_MFMA_PEAK_TF,

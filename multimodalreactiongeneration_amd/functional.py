@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 from typing import List, Optional, Sequence
 
 import torch
@@ -183,16 +184,80 @@ def colsum(rows, N, X, ld, out, *, out2=None, beta=1.0, ld_hi=0, rdiv=0, device=
                "colsum")
 
 
+# --- weight gradients on a side stream
+# Parameter gradients are consumed only by the optimizer / all-reduce, so the weight-gradient
+# GEMMs (dW = dY^T X, fused bias sums) leave the backward's critical path: they run on one side
+# stream per device, forked from the current stream when their operands are ready and joined back
+# at the end of the backward pass (an autograd final callback), so `loss.backward()` returns with
+# every gradient ordered before anything the caller issues next (graph capture included).  Their
+# operands are record_stream'ed so the caching allocator does not recycle them early.  EVERY
+# parameter-gradient write of the GEMM path goes through this one stream (also the few-row T = 1
+# decode products), so the accumulations into any one gradient buffer stay in order.
+# MRG_WGRAD_STREAM=0 (or set_wgrad_stream(False)) issues everything on the current stream.
+_WGRAD_SIDE = [os.environ.get("MRG_WGRAD_STREAM", "1") != "0"]
+_SIDE = {}
+_JOIN_PENDING = set()
+
+
+def set_wgrad_stream(on: bool) -> bool:
+    """Enable / disable side-stream weight gradients; returns the previous setting."""
+    prev = _WGRAD_SIDE[0]
+    _WGRAD_SIDE[0] = bool(on)
+    return prev
+
+
+class _side:
+    """Issue the enclosed launches on the device's weight-gradient stream (see above)."""
+    __slots__ = ("dev", "keep", "ctx")
+
+    def __init__(self, device, keep=()):
+        self.dev, self.keep, self.ctx = device, keep, None
+
+    def __enter__(self):
+        if not _WGRAD_SIDE[0]:
+            return self
+        dev = torch.device(self.dev)
+        key = dev.index or 0
+        cur = torch.cuda.current_stream(dev)
+        s = _SIDE.get(key)
+        if s is None:
+            s = _SIDE[key] = torch.cuda.Stream(device=dev)
+        if key not in _JOIN_PENDING:
+            def join(cur=cur, s=s, key=key):
+                cur.wait_stream(s)
+                _JOIN_PENDING.discard(key)
+            try:
+                torch.autograd.Variable._execution_engine.queue_callback(join)
+            except RuntimeError:  # not inside a backward pass: stay on the current stream
+                return self
+            _JOIN_PENDING.add(key)
+        s.wait_stream(cur)
+        for t in self.keep:
+            if t is not None:
+                t.record_stream(s)
+        self.ctx = torch.cuda.stream(s)
+        self.ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.ctx is not None:
+            self.ctx.__exit__(*exc)
+        return False
+
+
 def _wgrad(dY, ldy, X, ldx, rows, Nout, Nin, gw, device, *, dy_hi=0, dy_div=0, x_hi=0, x_div=0, gb=None,
-           gb2=None):
-    """gw[Nout, Nin] += sum_rows dY[row, :]^T X[row, :]; gb (and gb2) += sum_rows dY[row, :] (fused)."""
-    if gw is None:
-        if gb is not None:
-            colsum(rows, Nout, dY, ldy, _ptr(gb), out2=_ptr(gb2), ld_hi=dy_hi, rdiv=dy_div, device=device)
-        return
-    gemm(Nout, Nin, rows, dY, 1, ldy, X, 0, ldx, _ptr(gw), Nin, beta=1.0, a_hi=dy_hi, a_div=dy_div,
-         b_hi=x_hi, b_div=x_div, splits=wgrad_splits(Nout, Nin, rows), device=device,
-         asum_out=_ptr(gb), asum_out2=_ptr(gb2))
+           gb2=None, keep=()):
+    """gw[Nout, Nin] += sum_rows dY[row, :]^T X[row, :]; gb (and gb2) += sum_rows dY[row, :] (fused).
+
+    keep: the tensors behind the dY / X pointers (side-stream lifetime, see _side)."""
+    with _side(device, keep):
+        if gw is None:
+            if gb is not None:
+                colsum(rows, Nout, dY, ldy, _ptr(gb), out2=_ptr(gb2), ld_hi=dy_hi, rdiv=dy_div, device=device)
+            return
+        gemm(Nout, Nin, rows, dY, 1, ldy, X, 0, ldx, _ptr(gw), Nin, beta=1.0, a_hi=dy_hi, a_div=dy_div,
+             b_hi=x_hi, b_div=x_div, splits=wgrad_splits(Nout, Nin, rows), device=device,
+             asum_out=_ptr(gb), asum_out2=_ptr(gb2))
 
 
 # ------------------------------------------------------------------ Linear
@@ -216,7 +281,7 @@ class _LinearFn(Function):
         dy2 = dy.reshape(-1, N).contiguous()
         M = dy2.shape[0]
         dev = dy.device
-        _wgrad(_ptr(dy2), N, _ptr(x2), In, M, N, In, _gbuf(w), dev, gb=_gbuf(b))
+        _wgrad(_ptr(dy2), N, _ptr(x2), In, M, N, In, _gbuf(w), dev, gb=_gbuf(b), keep=(dy2, x2))
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(M, In, device=dev, dtype=torch.float32)
@@ -258,8 +323,8 @@ class _FFNFn(Function):
         dh = torch.empty(M, Hb, device=dev, dtype=torch.float32)
         gemm(M, Hb, N, _ptr(dz2), 0, N, _ptr(w2), 0, Hb, _ptr(dh), Hb, epi=2, aux=_ptr(h), ldaux=Hb,
              device=dev)
-        _wgrad(_ptr(dz2), N, _ptr(h), Hb, M, N, Hb, _gbuf(w2), dev, gb=_gbuf(b2))
-        _wgrad(_ptr(dh), Hb, _ptr(x2), In, M, Hb, In, _gbuf(w1), dev, gb=_gbuf(b1))
+        _wgrad(_ptr(dz2), N, _ptr(h), Hb, M, N, Hb, _gbuf(w2), dev, gb=_gbuf(b2), keep=(dz2, h))
+        _wgrad(_ptr(dh), Hb, _ptr(x2), In, M, Hb, In, _gbuf(w1), dev, gb=_gbuf(b1), keep=(dh, x2))
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(M, In, device=dev, dtype=torch.float32)
@@ -373,7 +438,7 @@ class _LinResLNFn(Function):
         M, E = x2.shape
         dev = dy.device
         g = _resln_bwd(dy.reshape(M, E).contiguous(), z, x2, gamma, beta, mean, rstd)
-        _wgrad(_ptr(g), E, _ptr(x2), E, M, E, E, _gbuf(w), dev, gb=_gbuf(b))
+        _wgrad(_ptr(g), E, _ptr(x2), E, M, E, E, _gbuf(w), dev, gb=_gbuf(b), keep=(g, x2))
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(M, E, device=dev, dtype=torch.float32)
@@ -414,8 +479,8 @@ class _FFNResLNFn(Function):
         g = _resln_bwd(dy.reshape(M, E).contiguous(), z, x2, gamma, beta, mean, rstd)
         dh = torch.empty(M, Hb, device=dev, dtype=torch.float32)
         gemm(M, Hb, E, _ptr(g), 0, E, _ptr(w2), 0, Hb, _ptr(dh), Hb, epi=2, aux=_ptr(h), ldaux=Hb, device=dev)
-        _wgrad(_ptr(g), E, _ptr(h), Hb, M, E, Hb, _gbuf(w2), dev, gb=_gbuf(b2))
-        _wgrad(_ptr(dh), Hb, _ptr(x2), E, M, Hb, E, _gbuf(w1), dev, gb=_gbuf(b1))
+        _wgrad(_ptr(g), E, _ptr(h), Hb, M, E, Hb, _gbuf(w2), dev, gb=_gbuf(b2), keep=(g, h))
+        _wgrad(_ptr(dh), Hb, _ptr(x2), E, M, Hb, E, _gbuf(w1), dev, gb=_gbuf(b1), keep=(dh, x2))
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(M, E, device=dev, dtype=torch.float32)
@@ -604,15 +669,17 @@ class _LSTMFn(Function):
                 a_off = 0 if reverse[i] else 4 * H
                 b_off = yoff + (y_ts[i] if reverse[i] else 0)
                 _wgrad(_ptr(g, a_off), 4 * H, _ptr(yb, b_off), y_ts[i], B * (T - 1), 4 * H, H, gw, dev,
-                       dy_hi=T * 4 * H, dy_div=T - 1, x_hi=y_bs[i], x_div=T - 1)
+                       dy_hi=T * 4 * H, dy_div=T - 1, x_hi=y_bs[i], x_div=T - 1, keep=(g, yb))
             if gw is not None and h0 is not None:
                 t0 = T - 1 if reverse[i] else 0
-                gemm(4 * H, H, B, _ptr(g, t0 * 4 * H), 1, T * 4 * H, _ptr(h0), 0, H, _ptr(gw), H,
-                     beta=1.0, device=dev)
+                with _side(dev, (g, h0)):
+                    gemm(4 * H, H, B, _ptr(g, t0 * 4 * H), 1, T * 4 * H, _ptr(h0), 0, H, _ptr(gw), H,
+                         beta=1.0, device=dev)
             gbi, gbh = _gbuf(b_ih), _gbuf(b_hh)
             first = gbi if gbi is not None else gbh
             second = gbh if gbi is not None else None
-            _wgrad(_ptr(g), 4 * H, _ptr(x), In, rows, 4 * H, In, _gbuf(w_ih), dev, gb=first, gb2=second)
+            _wgrad(_ptr(g), 4 * H, _ptr(x), In, rows, 4 * H, In, _gbuf(w_ih), dev, gb=first, gb2=second,
+                   keep=(g, x))
             dx = None
             if need[1 + K * i]:
                 if ctx.shared_x[i] and dx_first is not None:
@@ -679,10 +746,10 @@ class _LSTMCellFn(Function):
         gbi, gbh = _gbuf(b_ih), _gbuf(b_hh)
         first = gbi if gbi is not None else gbh
         _wgrad(_ptr(dG), 4 * H, _ptr(x2), In, B, 4 * H, In, _gbuf(w_ih), dev, gb=first,
-               gb2=gbh if gbi is not None else None)
+               gb2=gbh if gbi is not None else None, keep=(dG, x2))
         gw = _gbuf(w_hh)  # zero state: dW_hh = dG^T h0 = 0 (the buffer still exists, as with nn.LSTM)
         if gw is not None and h0c is not None:
-            _wgrad(_ptr(dG), 4 * H, _ptr(h0c), H, B, 4 * H, H, gw, dev)
+            _wgrad(_ptr(dG), 4 * H, _ptr(h0c), H, B, 4 * H, H, gw, dev, keep=(dG, h0c))
         dx = dh0 = None
         if need[0]:
             dx = torch.empty(B, 1, In, device=dev, dtype=torch.float32)
@@ -818,20 +885,22 @@ class _GRUFn(Function):
             dh_next = dhp
         need = ctx.needs_input_grad
         dh0 = dh_next if (h0c is not None and need[6]) else None
-        _wgrad(_ptr(dGX), H3, _ptr(x), In, B * T, H3, In, _gbuf(w_ih), dev, gb=_gbuf(b_ih))
+        _wgrad(_ptr(dGX), H3, _ptr(x), In, B * T, H3, In, _gbuf(w_ih), dev, gb=_gbuf(b_ih), keep=(dGX, x))
         gw = _gbuf(w_hh)
         if gw is not None and T > 1:
             # sum_t dGH_t^T h_{t-1}: forward pairs (dGH[t], y[t-1]), reverse (dGH[t], y[t+1])
             a_off = 0 if reverse else H3
             b_off = H if reverse else 0
             _wgrad(_ptr(dGH, a_off), H3, _ptr(y, b_off), H, B * (T - 1), H3, H, gw, dev,
-                   dy_hi=T * H3, dy_div=T - 1, x_hi=T * H, x_div=T - 1)
+                   dy_hi=T * H3, dy_div=T - 1, x_hi=T * H, x_div=T - 1, keep=(dGH, y))
         if gw is not None and h0c is not None:
             t0 = T - 1 if reverse else 0
-            gemm(H3, H, B, _ptr(dGH, t0 * H3), 1, T * H3, _ptr(h0c), 0, H, _ptr(gw), H, beta=1.0, device=dev)
+            with _side(dev, (dGH, h0c)):
+                gemm(H3, H, B, _ptr(dGH, t0 * H3), 1, T * H3, _ptr(h0c), 0, H, _ptr(gw), H, beta=1.0, device=dev)
         gbh = _gbuf(b_hh)
         if gbh is not None:
-            colsum(B * T, H3, _ptr(dGH), H3, _ptr(gbh), device=dev)
+            with _side(dev, (dGH,)):
+                colsum(B * T, H3, _ptr(dGH), H3, _ptr(gbh), device=dev)
         dx = None
         if need[1]:
             dx = torch.empty(B, T, In, device=dev, dtype=torch.float32)
@@ -913,7 +982,7 @@ class _MHAFn(Function):
             do2 = dout.contiguous()
         dO = torch.empty(B, Tq, E, device=dev, dtype=torch.float32)
         gemm(B * Tq, E, E, _ptr(do2), 0, E, _ptr(out_w), 0, E, _ptr(dO), E, device=dev)
-        _wgrad(_ptr(do2), E, _ptr(O), E, B * Tq, E, E, _gbuf(out_w), dev, gb=_gbuf(out_b))
+        _wgrad(_ptr(do2), E, _ptr(O), E, B * Tq, E, E, _gbuf(out_w), dev, gb=_gbuf(out_b), keep=(do2, O))
         dQ = torch.empty(B, Tq, E, device=dev, dtype=torch.float32)
         dKV = torch.empty(B, Tk, 2 * E, device=dev, dtype=torch.float32)
         ws = _ws(lib.mrg_attention_bwd_workspace_bytes(B, heads, Tq), dev)
@@ -926,9 +995,9 @@ class _MHAFn(Function):
         _lib.check(rc, "attention bwd")
         gw, gb = _gbuf(in_w), _gbuf(in_b)
         _wgrad(_ptr(dQ), E, _ptr(q2), E, B * Tq, E, E, None if gw is None else gw[:E], dev,
-               gb=None if gb is None else gb[:E])
+               gb=None if gb is None else gb[:E], keep=(dQ, q2))
         _wgrad(_ptr(dKV), 2 * E, _ptr(kv2), E, B * Tk, 2 * E, E, None if gw is None else gw[E:], dev,
-               gb=None if gb is None else gb[E:])
+               gb=None if gb is None else gb[E:], keep=(dKV, kv2))
         dq_in = dkv_in = None
         if ctx.needs_input_grad[1]:
             dq_in = torch.empty(B, Tq, E, device=dev, dtype=torch.float32)

@@ -252,3 +252,39 @@ def test_metaformer_generation_benchmark_width_vs_oracle():
         ref = O.metaformer_prediction(sd, mc, clone_batch(batch), mask)
     torch.cuda.synchronize()
     assert rel_err(pred, ref) < TOL
+
+
+def test_wgrad_side_stream_bitwise():
+    """Weight gradients on the side stream (functional._side), eager and graph-replayed, give the
+    bit-identical gradients of the single-stream schedule (every kernel is deterministic)."""
+    from multimodalreactiongeneration_amd import configs as C
+    from multimodalreactiongeneration_amd import functional as Fn
+    from multimodalreactiongeneration_amd.graphs import capture
+    from multimodalreactiongeneration_amd.model import Metaformer
+    from multimodalreactiongeneration_amd.synthetic import make_batch
+    mc, oc, me = C.lstmformer_config(ratio=1)
+    torch.manual_seed(0)
+    m = Metaformer(mc, oc, me).to(DEV)
+    opt = m.configure_optimizers()["optimizer"]
+    batch = make_batch(B=8, T=300, ratio=1, seed=5, device=DEV)
+
+    def step():
+        opt.zero_grad()
+        m.training_step(list(batch))["loss"].backward()
+
+    prev = Fn.set_wgrad_stream(False)
+    try:
+        step()
+        torch.cuda.synchronize()
+        ref = opt.flat_grad.clone()
+        Fn.set_wgrad_stream(True)
+        step()
+        torch.cuda.synchronize()
+        assert torch.equal(opt.flat_grad, ref)
+        replay = capture(step, 1)
+        opt.flat_grad.zero_()
+        replay()
+        torch.cuda.synchronize()
+        assert torch.equal(opt.flat_grad, ref)
+    finally:
+        Fn.set_wgrad_stream(prev)
