@@ -180,6 +180,11 @@ int mrg_residual_layernorm_bwd(int rows, int E, const float* dy, const float* a,
                                const float* gamma, const float* mean, const float* rstd,
                                float* dx, float* dgamma, float* dbeta, int accumulate,
                                float* workspace, hipStream_t stream);
+/* dgamma = dbeta = NULL in mrg_residual_layernorm_bwd leaves the per-block partials in the
+ * workspace; this reduces them (dgamma/dbeta += or = their sums) — e.g. on another stream, since
+ * only the optimizer reads parameter gradients.                                              */
+int mrg_residual_layernorm_param_reduce(int rows, int E, const float* workspace, float* dgamma,
+                                        float* dbeta, int accumulate, hipStream_t stream);
 
 /* ---------------------------------------------------------------- loss
  * Masked regression loss of training_step (lstmformer.py:372-380,

@@ -77,6 +77,7 @@ SIGNATURES = {
     "mrg_residual_layernorm_fwd": (c_int, [c_int, c_int, P, P, P, P, c_float, P, P, P, P]),
     "mrg_residual_layernorm_bwd_workspace_bytes": (c_size, [c_int, c_int]),
     "mrg_residual_layernorm_bwd": (c_int, [c_int, c_int, P, P, P, P, P, P, P, P, P, c_int, P, P]),
+    "mrg_residual_layernorm_param_reduce": (c_int, [c_int, c_int, P, P, P, c_int, P]),
     "mrg_loss_workspace_bytes": (c_size, [c_int, c_int, c_int]),
     "mrg_masked_loss_fwd": (c_int, [c_int, c_int, c_int, P, c_long, P, c_int, c_float, c_float,
                                     c_int, c_int, c_float, P, P, P]),

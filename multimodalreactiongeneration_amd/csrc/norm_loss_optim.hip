@@ -413,6 +413,9 @@ MRG_API size_t mrg_residual_layernorm_bwd_workspace_bytes(int rows, int E) {
   return (size_t)nblk * 2 * E * sizeof(float);
 }
 
+MRG_API int mrg_residual_layernorm_param_reduce(int rows, int E, const float* workspace, float* dgamma,
+                                                float* dbeta, int accumulate, hipStream_t stream);
+
 MRG_API int mrg_residual_layernorm_bwd(int rows, int E, const float* dy, const float* a,
                                        const float* b, const float* gamma, const float* mean,
                                        const float* rstd, float* dx, float* dgamma, float* dbeta,
@@ -435,6 +438,17 @@ MRG_API int mrg_residual_layernorm_bwd(int rows, int E, const float* dy, const f
   else if (epl <= 8) resln_bwd_kernel<8><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, rpb, E);
   else resln_bwd_kernel<16><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, rpb, E);
   if (check_launch("resln_bwd_kernel")) return 1;
+  if (!dgamma && !dbeta) return 0;  // partials stay in the workspace (mrg_residual_layernorm_param_reduce)
+  MRG_REQUIRE(dgamma && dbeta, "mrg_residual_layernorm_bwd: dgamma and dbeta must both be given or both null");
+  return mrg_residual_layernorm_param_reduce(rows, E, workspace, dgamma, dbeta, accumulate, stream);
+}
+
+MRG_API int mrg_residual_layernorm_param_reduce(int rows, int E, const float* workspace, float* dgamma,
+                                                float* dbeta, int accumulate, hipStream_t stream) {
+  if (rows == 0) return 0;
+  MRG_REQUIRE(E >= 1 && E <= 1024 && dgamma && dbeta && workspace,
+              "mrg_residual_layernorm_param_reduce: bad arguments (E=%d)", E);
+  const int nblk = (rows + RESLN_RPB - 1) / RESLN_RPB;
   resln_param_reduce_kernel<<<(2 * E + 63) / 64, 1024, 0, stream>>>(workspace, nblk, E, dgamma, dbeta,
                                                                    accumulate);
   return check_launch("resln_param_reduce_kernel");

@@ -360,21 +360,8 @@ class _ResLNFn(Function):
     @staticmethod
     def backward(ctx, dy):
         a2, b2, gamma, beta, mean, rstd = ctx.saved_tensors
-        rows, E = a2.shape
-        dev = dy.device
-        dy2 = dy.reshape(-1, E).contiguous()
-        dx = torch.empty_like(a2)
-        lib = _lib.load()
-        ws = _ws(lib.mrg_residual_layernorm_bwd_workspace_bytes(rows, E), dev)
-        gg, gb = _gbuf(gamma), _gbuf(beta)
-        scratch = None
-        if gg is None or gb is None:
-            scratch = torch.empty(2, E, device=dev, dtype=torch.float32)
-        _lib.check(lib.mrg_residual_layernorm_bwd(
-            rows, E, _ptr(dy2), _ptr(a2), _ptr(b2), _ptr(gamma), _ptr(mean), _ptr(rstd), _ptr(dx),
-            _ptr(gg if gg is not None else scratch[0]), _ptr(gb if gb is not None else scratch[1]),
-            1, _ptr(ws), _stream()), "layernorm bwd")
-        dx = dx.view(ctx.shape)
+        dy2 = dy.reshape(-1, a2.shape[1]).contiguous()
+        dx = _resln_bwd(dy2, a2, b2, gamma, beta, mean, rstd).view(ctx.shape)
         return dx, dx, None, None, None
 
 
@@ -403,13 +390,18 @@ def _resln_bwd(dy2, a2, b2, gamma, beta, mean, rstd):
     lib = _lib.load()
     ws = _ws(lib.mrg_residual_layernorm_bwd_workspace_bytes(rows, E), dev)
     gg, gb = _gbuf(gamma), _gbuf(beta)
-    scratch = None
-    if gg is None or gb is None:
-        scratch = torch.empty(2, E, device=dev, dtype=torch.float32)
     _lib.check(lib.mrg_residual_layernorm_bwd(
         rows, E, _ptr(dy2), _ptr(a2), _ptr(b2), _ptr(gamma), _ptr(mean), _ptr(rstd), _ptr(g),
-        _ptr(gg if gg is not None else scratch[0]), _ptr(gb if gb is not None else scratch[1]),
-        1, _ptr(ws), _stream()), "layernorm bwd")
+        None, None, 1, _ptr(ws), _stream()), "layernorm bwd")
+    if gg is not None or gb is not None:
+        # dgamma / dbeta from the per-block partials: parameter gradients, off the critical path
+        with _side(dev, (ws,)):
+            scratch = None
+            if gg is None or gb is None:
+                scratch = torch.empty(2, E, device=dev, dtype=torch.float32)
+            _lib.check(lib.mrg_residual_layernorm_param_reduce(
+                rows, E, _ptr(ws), _ptr(gg if gg is not None else scratch[0]),
+                _ptr(gb if gb is not None else scratch[1]), 1, _stream()), "layernorm param reduce")
     return g
 
 
