@@ -190,11 +190,14 @@ def colsum(rows, N, X, ld, out, *, out2=None, beta=1.0, ld_hi=0, rdiv=0, device=
 # stream per device, forked from the current stream when their operands are ready and joined back
 # at the end of the backward pass (an autograd final callback), so `loss.backward()` returns with
 # every gradient ordered before anything the caller issues next (graph capture included).  Their
-# operands are record_stream'ed so the caching allocator does not recycle them early.  EVERY
-# parameter-gradient write of the GEMM path goes through this one stream (also the few-row T = 1
-# decode products), so the accumulations into any one gradient buffer stay in order.
+# operands are record_stream'ed so the caching allocator does not recycle them early.  Products
+# over fewer than _SIDE_MIN_ROWS rows (the T = 1 decode steps of the autoregressive loops, where
+# a fork/join per frame costs more than it hides: C3 scheduled sampling 80 -> 130 ms measured)
+# stay on the current stream; if the side stream already has work in this backward pass, the
+# current stream first waits for it, so the writes into any one gradient buffer stay in order.
 # MRG_WGRAD_STREAM=0 (or set_wgrad_stream(False)) issues everything on the current stream.
 _WGRAD_SIDE = [os.environ.get("MRG_WGRAD_STREAM", "1") != "0"]
+_SIDE_MIN_ROWS = 2048
 _SIDE = {}
 _JOIN_PENDING = set()
 
@@ -208,10 +211,10 @@ def set_wgrad_stream(on: bool) -> bool:
 
 class _side:
     """Issue the enclosed launches on the device's weight-gradient stream (see above)."""
-    __slots__ = ("dev", "keep", "ctx")
+    __slots__ = ("dev", "rows", "keep", "ctx")
 
-    def __init__(self, device, keep=()):
-        self.dev, self.keep, self.ctx = device, keep, None
+    def __init__(self, device, rows, keep=()):
+        self.dev, self.rows, self.keep, self.ctx = device, rows, keep, None
 
     def __enter__(self):
         if not _WGRAD_SIDE[0]:
@@ -219,6 +222,10 @@ class _side:
         dev = torch.device(self.dev)
         key = dev.index or 0
         cur = torch.cuda.current_stream(dev)
+        if self.rows < _SIDE_MIN_ROWS:
+            if key in _JOIN_PENDING:  # order this write after the side stream's pending ones
+                cur.wait_stream(_SIDE[key])
+            return self
         s = _SIDE.get(key)
         if s is None:
             s = _SIDE[key] = torch.cuda.Stream(device=dev)
@@ -250,7 +257,7 @@ def _wgrad(dY, ldy, X, ldx, rows, Nout, Nin, gw, device, *, dy_hi=0, dy_div=0, x
     """gw[Nout, Nin] += sum_rows dY[row, :]^T X[row, :]; gb (and gb2) += sum_rows dY[row, :] (fused).
 
     keep: the tensors behind the dY / X pointers (side-stream lifetime, see _side)."""
-    with _side(device, keep):
+    with _side(device, rows, keep):
         if gw is None:
             if gb is not None:
                 colsum(rows, Nout, dY, ldy, _ptr(gb), out2=_ptr(gb2), ld_hi=dy_hi, rdiv=dy_div, device=device)
@@ -395,7 +402,7 @@ def _resln_bwd(dy2, a2, b2, gamma, beta, mean, rstd):
         None, None, 1, _ptr(ws), _stream()), "layernorm bwd")
     if gg is not None or gb is not None:
         # dgamma / dbeta from the per-block partials: parameter gradients, off the critical path
-        with _side(dev, (ws,)):
+        with _side(dev, rows, (ws,)):
             scratch = None
             if gg is None or gb is None:
                 scratch = torch.empty(2, E, device=dev, dtype=torch.float32)
@@ -664,7 +671,7 @@ class _LSTMFn(Function):
                        dy_hi=T * 4 * H, dy_div=T - 1, x_hi=y_bs[i], x_div=T - 1, keep=(g, yb))
             if gw is not None and h0 is not None:
                 t0 = T - 1 if reverse[i] else 0
-                with _side(dev, (g, h0)):
+                with _side(dev, B * T, (g, h0)):
                     gemm(4 * H, H, B, _ptr(g, t0 * 4 * H), 1, T * 4 * H, _ptr(h0), 0, H, _ptr(gw), H,
                          beta=1.0, device=dev)
             gbi, gbh = _gbuf(b_ih), _gbuf(b_hh)
@@ -887,11 +894,11 @@ class _GRUFn(Function):
                    dy_hi=T * H3, dy_div=T - 1, x_hi=T * H, x_div=T - 1, keep=(dGH, y))
         if gw is not None and h0c is not None:
             t0 = T - 1 if reverse else 0
-            with _side(dev, (dGH, h0c)):
+            with _side(dev, B * T, (dGH, h0c)):
                 gemm(H3, H, B, _ptr(dGH, t0 * H3), 1, T * H3, _ptr(h0c), 0, H, _ptr(gw), H, beta=1.0, device=dev)
         gbh = _gbuf(b_hh)
         if gbh is not None:
-            with _side(dev, (dGH,)):
+            with _side(dev, B * T, (dGH,)):
                 colsum(B * T, H3, _ptr(dGH), H3, _ptr(gbh), device=dev)
         dx = None
         if need[1]:
