@@ -262,9 +262,11 @@ class Metaformer(LightningSurface):
         dev = self.device
         (fb, lf), (mp, lp), (ms, ls) = batch[0], batch[1], batch[2]
         T, B = mp.shape[1], mp.shape[0]
-        fb = fb.to(dev).view(B, T, self.ratio, fb.shape[-1]).transpose(0, 1)
-        mp = mp.to(dev).transpose(0, 1).unsqueeze(2)
-        ms = ms.to(dev).transpose(0, 1).unsqueeze(2)
+        # time-major copies made once: every per-frame slice below is then contiguous, so the
+        # ops of the T single-frame forwards run on it in place (no per-frame layout copies)
+        fb = fb.to(dev).view(B, T, self.ratio, fb.shape[-1]).transpose(0, 1).contiguous()
+        mp = mp.to(dev).transpose(0, 1).unsqueeze(2).contiguous()
+        ms = ms.to(dev).transpose(0, 1).unsqueeze(2).contiguous()
         fb = fb * (fb != PADDING_VALUE).to(fb.dtype)
         mp = mp * (mp != PADDING_VALUE).to(mp.dtype)
         msk = (ms != PADDING_VALUE).to(ms.dtype)
@@ -390,9 +392,11 @@ class LSTMwithSample(LightningSurface):
         dev = self.device
         (fb, lf), (mp, lp), (ms, ls) = batch[0], batch[1], batch[2]
         T, B = mp.shape[1], mp.shape[0]
-        fb = fb.to(dev).view(B, T, self.ratio, fb.shape[-1]).transpose(0, 1)
-        mp = mp.to(dev).transpose(0, 1).unsqueeze(2)
-        ms = ms.to(dev).transpose(0, 1).unsqueeze(2)
+        # time-major copies made once: every per-frame slice below is then contiguous, so the
+        # ops of the T single-frame forwards run on it in place (no per-frame layout copies)
+        fb = fb.to(dev).view(B, T, self.ratio, fb.shape[-1]).transpose(0, 1).contiguous()
+        mp = mp.to(dev).transpose(0, 1).unsqueeze(2).contiguous()
+        ms = ms.to(dev).transpose(0, 1).unsqueeze(2).contiguous()
         target = batch[-1][0].to(dev)
         empty = [(torch.empty(x.shape[0], 0, x.shape[2], device=dev), n) for x, n in batch]
         _, _, cell = self.forward(*empty[:3], *batch[3:6], cell_state=None)
