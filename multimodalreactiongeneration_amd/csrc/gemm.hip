@@ -882,14 +882,35 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(GemmArgs a) {
   const bool sums = TA && a.asum_out && blockIdx.x == 0;
   f32x4v acc = f32x4v{0.f, 0.f, 0.f, 0.f};
   float rs = 0.0f;
+  // k-contiguous operands (A when TA = 0, B when TB = 1) load as float4 when this lane's run is
+  // 16-B aligned: a quarter of the load instructions
+  const bool va = !TA && (KQ & 3) == 0 && (((uintptr_t)(ap + kb)) & 15) == 0;
+  const bool vb = TB && (KQ & 3) == 0 && (((uintptr_t)(bp + kb)) & 15) == 0;
   for (int k0 = kb; k0 < ke; k0 += CH) {
     float av[CH], bv[CH];
 #pragma unroll
-    for (int s = 0; s < CH; ++s) {
+    for (int s = 0; s < CH; s += 4) {
       const int k = k0 + s;
-      const bool ok = k < ke;
-      av[s] = (ok && mv) ? (TA ? ap[a.amap.off(k)] : ap[k]) : 0.0f;
-      bv[s] = (ok && nv) ? (TB ? bp[k] : bp[a.bmap.off(k)]) : 0.0f;
+      if (va && k + 3 < ke) {
+        const float4 v = mv ? *reinterpret_cast<const float4*>(ap + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+        av[s] = v.x; av[s + 1] = v.y; av[s + 2] = v.z; av[s + 3] = v.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool ok = k + e < ke;
+          av[s + e] = (ok && mv) ? (TA ? ap[a.amap.off(k + e)] : ap[k + e]) : 0.0f;
+        }
+      }
+      if (vb && k + 3 < ke) {
+        const float4 v = nv ? *reinterpret_cast<const float4*>(bp + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+        bv[s] = v.x; bv[s + 1] = v.y; bv[s + 2] = v.z; bv[s + 3] = v.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool ok = k + e < ke;
+          bv[s + e] = (ok && nv) ? (TB ? bp[k + e] : bp[a.bmap.off(k + e)]) : 0.0f;
+        }
+      }
     }
 #pragma unroll
     for (int s = 0; s < CH; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[s], acc, 0, 0, 0);

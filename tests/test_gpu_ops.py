@@ -101,6 +101,25 @@ def test_few_row_gemms(M, N, K, epi, split):
     assert int(Fn._counters(DEV).abs().sum()) == 0
 
 
+@pytest.mark.parametrize("M,N,K,transB,a_off", [
+    (64, 256, 1024, 0, 0), (64, 128, 512, 1, 0), (37, 96, 516, 0, 0), (64, 256, 1024, 1, 1), (50, 40, 64, 1, 3)])
+def test_few_row_gemm_operand_layouts(M, N, K, transB, a_off):
+    """gemm_rows_kernel with B row-major [K, N] (the dX form dG W) or [N, K], k-runs loaded as float4
+    when aligned and element-wise otherwise (odd K per lane group, an A view offset off 16 B)."""
+    from multimodalreactiongeneration_amd import functional as Fn
+    g = torch.Generator().manual_seed(M + N + K + a_off)
+    abuf = torch.randn(M * K + a_off, generator=g)
+    a = abuf[a_off:].view(M, K)
+    w = torch.randn((K, N) if transB == 0 else (N, K), generator=g) / math.sqrt(K)
+    abd, wd = abuf.to(DEV), w.to(DEV)
+    c = torch.zeros(M, N, device=DEV)
+    Fn.gemm(M, N, K, Fn._ptr(abd, a_off), 0, K, Fn._ptr(wd), transB, N if transB == 0 else K, Fn._ptr(c), N,
+            device=DEV)
+    torch.cuda.synchronize()
+    wm = w.double() if transB == 0 else w.double().t()
+    assert rel_err(c, a.double() @ wm) < TOL
+
+
 @pytest.mark.parametrize("rows,N,In,splits,time_shift", [
     (19200, 1024, 256, 32, False), (19200, 256, 256, 120, False), (1000, 70, 45, 1, False),
     (777, 130, 33, 5, False), (64 * 299, 1024, 256, 16, True), (64, 1024, 256, 1, False),
