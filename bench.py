@@ -41,7 +41,7 @@ PEAK_NOTES = {
     "lstm_fwd": "latency-bound (one cross-CU hand-off per time step); VALU v_pk_fma_f32 peak = 157.3",
     "lstm_bwd": "latency-bound (one cross-CU hand-off per time step); VALU v_pk_fma_f32 peak = 157.3",
 }
-# rocprofv3 kernel-name prefix of each family in the PMC summary (tools_pmc_summary.py)
+# rocprofv3 kernel-name prefix of each family in the PMC summary (tools/tools_pmc_summary.py)
 PMC_KEYS = {"gemm": "gemm_x6_kernel", "lstm_fwd": "lstm_fwd_kernel", "lstm_bwd": "lstm_bwd_kernel",
             "attn_fwd": "attn_fwd_kernel", "attn_bwd": "attn_bwd"}
 

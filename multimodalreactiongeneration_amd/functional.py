@@ -164,7 +164,7 @@ def wgrad_splits(M, N, K):
     """split-K factor for weight-gradient GEMMs (small M x N output, long B*T reduction).
 
     About 512 workgroups: 128x128 tiles under the x6 arithmetic (chunks of >= 128 rows),
-    64x64 tiles under exact f32 (chunks of >= 256 rows); tools_gemm_sweep.py measured both.
+    64x64 tiles under exact f32 (chunks of >= 256 rows); tools/tools_gemm_sweep.py measured both.
     """
     if _lib.load().mrg_gemm_get_mode() == 1:
         tiles = ((M + 127) // 128) * ((N + 127) // 128)

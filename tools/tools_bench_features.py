@@ -1,7 +1,7 @@
 """Data-loader features: one training batch's partner audio, 64 clips of
 312 + 2 prediction frames (lead 12, delta order 2) at 16 kHz, nfft 400, hop 160, 26 mels.
 
-    python tools_bench_features.py        (on a GPU box)
+    python tools/tools_bench_features.py        (on a GPU box)
 
 GPU: AudioPreprocessor.features on the resident batch [64, samples] (one GEMM + one finish +
 one delta launch) and clip by clip; CPU: the reference's algorithm (oracle.audio_features:
@@ -9,12 +9,13 @@ torch.stft MelSpectrogram + the per-frame log-power loop of audio.py:43-56), one
 DataLoader worker runs it, on a sample of clips.
 """
 import json
+import os
 import sys
 import time
 
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # repo root
 from multimodalreactiongeneration_amd.features import AudioPreprocessor  # noqa: E402
 from oracle import mrg_oracle as O  # noqa: E402
 

@@ -1,6 +1,6 @@
 """Step times of the other BASELINE configs (not the headline bench line): eager fwd+bwd+AdamW.
 
-    python tools_bench_models.py [steps] [C2|C3|C3tf|gen|gru|all] [graph]     (on a GPU box)
+    python tools/tools_bench_models.py [steps] [C2|C3|C3tf|gen|gru|all] [graph]     (on a GPU box)
 
   graph=1 replays each step as one HIP graph (graphs.capture); C3's sampling mask then lives in a
   static device buffer refreshed from the host RNG draw before every replay.
@@ -11,13 +11,14 @@
   C3' lstm_with_sampling teacher-forced, B=64, T=300
 """
 import json
+import os
 import sys
 import time
 
 import numpy as np
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # repo root
 from multimodalreactiongeneration_amd import configs as C  # noqa: E402
 from multimodalreactiongeneration_amd import functional as Fn  # noqa: E402
 from multimodalreactiongeneration_amd.model import LSTMwithSample, SimpleLSTM  # noqa: E402

@@ -1,6 +1,6 @@
 """Idle gaps of a graph-replayed step from a rocprofv3 kernel trace (tools_gpu_gaps.sh).
 
-    python tools_gaps.py gpurun_out/gaps/run_kernel_trace.csv
+    python tools/tools_gaps.py gpurun_out/gaps/run_kernel_trace.csv
 Steps are delimited by adamw_kernel; the last `--steps` replays before the eager probe steps.
 """
 import csv

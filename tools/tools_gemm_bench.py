@@ -1,14 +1,15 @@
 """Per-shape timing of mrg_gemm_f32 on the GEMM shapes of the lstmformer step (B=64, T=300, H=256).
 
-    python tools_gemm_bench.py            (on a GPU box)
+    python tools/tools_gemm_bench.py            (on a GPU box)
 
 Prints TFLOP/s per shape against the 157.3 TF f32 MFMA peak, plus the step-weighted total.
 """
+import os
 import sys
 
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # repo root
 from multimodalreactiongeneration_amd import functional as Fn  # noqa: E402
 
 R = 64 * 300

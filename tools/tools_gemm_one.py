@@ -1,9 +1,10 @@
 """Run one GEMM shape repeatedly (for rocprofv3 counter passes): python tools_gemm_one.py M N K ta tb [iters]"""
+import os
 import sys
 
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # repo root
 from tools_gemm_bench import run_shape  # noqa: E402
 
 M, N, K, ta, tb = (int(x) for x in sys.argv[1:6])

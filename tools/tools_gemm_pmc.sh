@@ -11,7 +11,7 @@ i=0
 for shape in ${GPMC_SHAPES:-"19200 1024 256 0 1"}; do
   for P in "$P1" "$P2"; do
     i=$((i+1))
-    timeout -k 10 200 rocprofv3 --pmc $P -d $R/gpurun_out/gpmc/p$i -o p --output-format csv -- python3 $R/tools_gemm_one.py $shape 5 > $R/gpurun_out/gpmc/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $R/gpurun_out/gpmc/p$i.log; exit 1; }
+    timeout -k 10 200 rocprofv3 --pmc $P -d $R/gpurun_out/gpmc/p$i -o p --output-format csv -- python3 $R/tools/tools_gemm_one.py $shape 5 > $R/gpurun_out/gpmc/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $R/gpurun_out/gpmc/p$i.log; exit 1; }
     echo "pass $i ($shape) ok"
   done
 done

@@ -1,12 +1,13 @@
 """Sweep GEMM arithmetic mode x tile shape (x split-K for weight gradients) on the step's shapes.
 
-    python tools_gemm_sweep.py            (on a GPU box)
+    python tools/tools_gemm_sweep.py            (on a GPU box)
 """
+import os
 import sys
 
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # repo root
 from multimodalreactiongeneration_amd import _lib  # noqa: E402
 from tools_gemm_bench import SHAPES, run_shape  # noqa: E402
 import tools_gemm_bench as TB  # noqa: E402

@@ -1,9 +1,10 @@
 """Where the x6 GEMM's time goes: structural variants (mrg_gemm_x6_variant) on the step's shapes."""
+import os
 import sys
 
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # repo root
 from multimodalreactiongeneration_amd import _lib, functional as Fn  # noqa: E402
 
 NAMES = {0: "x6 product", 1: "split + 1 MFMA", 2: "plane0 + 6 MFMA", 3: "plane0 + 1 MFMA (bf16 GEMM)"}

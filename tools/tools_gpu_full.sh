@@ -11,4 +11,4 @@ tail -1 gpurun_out/bench.log
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run --output-format csv -- python3 $R/bench.py --graph 0 --wgrad-stream 0 --cpu-baseline 0 --steps 3 --warmup 1 > $R/gpurun_out/prof.log 2>&1 || { echo "prof failed"; tail -5 $R/gpurun_out/prof.log; exit 1; }
 echo "prof ok"
 cd $R
-if [ "${PMC:-1}" = "1" ]; then bash tools_pmc.sh; fi
+if [ "${PMC:-1}" = "1" ]; then bash tools/tools_pmc.sh; fi

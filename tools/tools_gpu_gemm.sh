@@ -9,6 +9,6 @@ for c in ${CONFIGS:-32:auto}; do
   export MRG_GEMM_BK=$bk  # (ignored unless a BK variant is instantiated)
   if [ "$t" = "auto" ]; then unset MRG_GEMM_TILE; else export MRG_GEMM_TILE=$t; fi
   echo "=== BK $bk tile $t"
-  timeout -k 10 300 python tools_gemm_bench.py > gpurun_out/gemm_bench_$bk_$t.log 2>&1 || { echo "gemm bench failed"; tail -20 gpurun_out/gemm_bench_$bk_$t.log; exit 1; }
+  timeout -k 10 300 python tools/tools_gemm_bench.py > gpurun_out/gemm_bench_$bk_$t.log 2>&1 || { echo "gemm bench failed"; tail -20 gpurun_out/gemm_bench_$bk_$t.log; exit 1; }
   grep -v amdgpu.ids gpurun_out/gemm_bench_$bk_$t.log
 done

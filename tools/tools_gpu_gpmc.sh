@@ -4,4 +4,4 @@ set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --cpu-baseline 0 > gpurun_out/bench.log 2>&1 || exit 1
 tail -1 gpurun_out/bench.log
-bash tools_gemm_pmc.sh
+bash tools/tools_gemm_pmc.sh

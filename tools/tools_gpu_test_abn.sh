@@ -2,4 +2,4 @@ set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -30 gpurun_out/gpu_tests.log; exit 1; }
 tail -1 gpurun_out/gpu_tests.log
-AB_ARGS="--wgrad-stream 0" bash tools_gpu_abn.sh
+AB_ARGS="--wgrad-stream 0" bash tools/tools_gpu_abn.sh

@@ -1,15 +1,16 @@
 """LSTM recurrence launch time vs group size (members per batch-row group) and problems per launch.
 
-    python tools_lstm_groups.py        (on a GPU box)
+    python tools/tools_lstm_groups.py        (on a GPU box)
 
 H = 256, B = 64, T = 300 (the lstmformer encoder layers); fwd = one persistent forward launch of
 nprob independent recurrences, bwd = the matching backward launch (timed from the probes).
 """
+import os
 import sys
 
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # repo root
 from multimodalreactiongeneration_amd import _lib, functional as Fn  # noqa: E402
 
 DEV = "cuda:0"

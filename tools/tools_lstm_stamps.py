@@ -1,6 +1,6 @@
 """Diagnostics: where a persistent LSTM step spends its time (in-kernel s_memtime stamps, block 0).
 
-    python tools_lstm_stamps.py            (on a GPU box)
+    python tools/tools_lstm_stamps.py            (on a GPU box)
 """
 import ctypes
 import os
@@ -9,7 +9,7 @@ import time
 
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # repo root
 from multimodalreactiongeneration_amd import _lib, functional as Fn  # noqa: E402
 
 H, B, T = 256, 64, 300
