@@ -195,6 +195,8 @@ class LSTM(nn.Module):
                                                         self.direction_params(layer, True), h0, c0)
                 hs += [hT[0], hT[1]]
                 cs += [cT[0], cT[1]]
+        if len(hs) == 1:  # one layer, one direction: a view, no copy kernel (T = 1 decode frames)
+            return x, (hs[0].unsqueeze(0), cs[0].unsqueeze(0))
         return x, (torch.stack(hs), torch.stack(cs))
 
 
