@@ -115,6 +115,10 @@ int mrg_lstm_bwd(int nprob, int B, int T, int H,
                  float* const* dG, float* const* dh0, float* const* dc0, const int* reverse,
                  void* const* xbuf, int* err, int cus, int force_bs, hipStream_t stream);
 
+/* Fault injection (tests only): mode 1 makes the NEXT mrg_lstm_fwd launch drop member 0's first
+ * hand-off, so the recurrence times out and reports through *err; 0 disarms.  Process-wide.  */
+int mrg_lstm_debug_inject(int mode);
+
 /* Tuning knob: number of workgroups that share one batch row group at H = 256
  * (8 or 16; default 8).  Process-wide; set before capture, not during. */
 int mrg_lstm_config(int group256);
@@ -199,12 +203,34 @@ int mrg_masked_loss_bwd(int B, int T, int F, const float* y, long y_bstride, con
                         int type, float delta, float beta, int mask_padding, int delta_start,
                         float dscale, const float* grad_out, float* dy, hipStream_t stream);
 
+/* Broadcast-target loss of the lstmformer AR path: Metaformer.prediction returns
+ * target [B,T,F] * motion_s_mask [Tm,B,1,F] -> [Tm,B,T,F] (lstmformer.py:434-435, mask from
+ * :540-547), and generation_step (:410-424) / the scheduled-sampling training_step (:357-385)
+ * take the padding-masked mean loss over that broadcast tensor, the training scaler
+ * sqrt(delta_loss_scale) applying to time indices t >= t_start (its [:, :, start:] slice lands on
+ * the T axis; pass t_start > T for none).  Computed analytically from per-(b, f) counts of
+ * non-padded motion_s frames: ms is the raw self motion [B, Tm, F] (batch / time strides), y the
+ * prediction [B, T, F] (batch stride y_bstride), target contiguous.  workspace:
+ * mrg_broadcast_loss_workspace_bytes.  Mean over Tm*B*T*F elements.                        */
+size_t mrg_broadcast_loss_workspace_bytes(int B, int T, int F);
+int mrg_broadcast_loss_fwd(int B, int T, int F, const float* y, long y_bstride, const float* target,
+                           const float* ms, long ms_bs, long ms_ts, int Tm, int type, float delta,
+                           float beta, int t_start, float dscale, float* loss_out, float* workspace,
+                           hipStream_t stream);
+int mrg_broadcast_loss_bwd(int B, int T, int F, const float* y, long y_bstride, const float* target,
+                           const float* ms, long ms_bs, long ms_ts, int Tm, int type, float delta,
+                           float beta, int t_start, float dscale, const float* grad_out, float* dy,
+                           float* workspace, hipStream_t stream);
+
 /* ---------------------------------------------------------------- AdamW
  * torch.optim.AdamW step over flat buffers (configure_optimizers,
- * lstmformer.py:327-333).  step_lr = device float[2] {steps done, lr}.     */
+ * lstmformer.py:327-333).  step_lr = device float[2] {steps done, lr}.
+ * err (nullable): the device error flag the persistent LSTM kernels OR into on a hand-off
+ * timeout; when it is set the update and the step count are skipped (garbage gradients never
+ * reach the weights, even inside a replayed graph).                                       */
 int mrg_adamw_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, long n,
                    float* step_lr, float weight_decay, float beta1, float beta2, float eps,
-                   hipStream_t stream);
+                   const int* err, hipStream_t stream);
 
 /* ---------------------------------------------------------------- features (data loader)
  * AudioPreprocessor (mr_gen/utils/preprocess/audio.py:6-67).  The power spectrum comes from one

@@ -83,7 +83,13 @@ SIGNATURES = {
                                     c_int, c_int, c_float, P, P, P]),
     "mrg_masked_loss_bwd": (c_int, [c_int, c_int, c_int, P, c_long, P, c_int, c_float, c_float,
                                     c_int, c_int, c_float, P, P, P]),
-    "mrg_adamw_step": (c_int, [P, P, P, P, c_long, P, c_float, c_float, c_float, c_float, P]),
+    "mrg_broadcast_loss_workspace_bytes": (c_size, [c_int, c_int, c_int]),
+    "mrg_broadcast_loss_fwd": (c_int, [c_int, c_int, c_int, P, c_long, P, P, c_long, c_long, c_int, c_int,
+                                       c_float, c_float, c_int, c_float, P, P, P]),
+    "mrg_broadcast_loss_bwd": (c_int, [c_int, c_int, c_int, P, c_long, P, P, c_long, c_long, c_int, c_int,
+                                       c_float, c_float, c_int, c_float, P, P, P, P]),
+    "mrg_adamw_step": (c_int, [P, P, P, P, c_long, P, c_float, c_float, c_float, c_float, P, P]),
+    "mrg_lstm_debug_inject": (c_int, [c_int]),
 }
 
 _lock = threading.Lock()

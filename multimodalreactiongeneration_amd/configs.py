@@ -50,7 +50,8 @@ def _metrics(delta_order=0):
 
 def lstmformer_config(hidden=256, num_block=5, encoder_num_layer=5, num_heads=4,
                       bottleneck=64, nmels=39, delta_order=0, ratio=1, lr=5e-6,
-                      loss_type="huber", emb_mixers=("lstm", "lstm", "lstm")):
+                      loss_type="huber", emb_mixers=("lstm", "lstm", "lstm"), delta_loss_scale=1,
+                      use_scheduled_sampling=False, max_epochs=60):
     """Resolved mr_gen/model/lstmformer/config.yaml model section (+ bench overrides)."""
     model = AttrDict(
         main_modal_idx=2, hidden_size=hidden, num_block=num_block, dropout=0.0,
@@ -64,7 +65,8 @@ def lstmformer_config(hidden=256, num_block=5, encoder_num_layer=5, num_heads=4,
         pred_fps=100.0 / ratio, modalities=["audio", "motion", "motion"],
         use_centroid=True, use_angle=True, nmels=nmels, delta_order=delta_order,
         loss_type=loss_type, loss_reduction="mean", huber_delta=1.0, smoothl1_beta=1.0,
-        delta_loss_scale=1, use_scheduled_sampling=False, max_epochs=60)
+        delta_loss_scale=delta_loss_scale, use_scheduled_sampling=use_scheduled_sampling,
+        max_epochs=max_epochs)
     return model, _optim(lr), _metrics(delta_order)
 
 

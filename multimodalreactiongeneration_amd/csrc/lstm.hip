@@ -75,6 +75,7 @@ struct LstmBwdProblem {
 struct LstmFwdArgs {
   LstmFwdProblem p[MAXP];
   int nprob, B, T;
+  int inject;  // fault injection (mrg_lstm_debug_inject): 1 = member 0 drops its first hand-off
   int* err;
   unsigned long long* stamps;  // diagnostics only (mrg_lstm_debug_stamps); null in normal use
 };
@@ -325,7 +326,7 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
       float ig = sigmoidf_(zi), fg = sigmoidf_(zf), gg = tanhf_(zg), og = sigmoidf_(zo);
       c = fg * c + ig * gg;
       h = og * tanhf_(c);
-      put_granule(xb + ((long)par * B + bg) * H + hcol, (unsigned)(tt + 1), h);
+      if (!(args.inject == 1 && j == 0 && tt == 0)) put_granule(xb + ((long)par * B + bg) * H + hcol, (unsigned)(tt + 1), h);
       P.y[(long)bg * P.y_bs + (long)t * P.y_ts + hcol] = h;
       float* gs = P.gates + ((long)bg * T + t) * 4 * H + hcol;
       gs[0] = ig; gs[H] = fg; gs[2 * H] = gg; gs[3 * H] = og;
@@ -635,6 +636,14 @@ static int group_size(int H) {
 using namespace mrg;
 
 static unsigned long long* g_stamps = nullptr;
+static int g_inject = 0;
+
+// Tests only: arm a fault for the next forward launch (see mrg.h).
+MRG_API int mrg_lstm_debug_inject(int mode) {
+  MRG_REQUIRE(mode == 0 || mode == 1, "mrg_lstm_debug_inject: mode must be 0 or 1");
+  g_inject = mode;
+  return 0;
+}
 
 // Diagnostics: next LSTM launches record per-step phase clocks of block 0 into buf ([T][8] u64);
 // pass null to disable.  Not for timed runs.
@@ -677,6 +686,8 @@ MRG_API int mrg_lstm_fwd(int nprob, int B, int T, int H,
   LstmFwdArgs a;
   memset(&a, 0, sizeof(a));
   a.nprob = nprob; a.B = B; a.T = T; a.err = err; a.stamps = g_stamps;
+  a.inject = g_inject;
+  g_inject = 0;  // one launch only
   for (int i = 0; i < nprob; ++i) {
     LstmFwdProblem& p = a.p[i];
     p.gx = gx[i]; p.gx_bs = gx_bs[i]; p.gx_ts = gx_ts[i];

@@ -284,20 +284,13 @@ struct LossArgs {
   float dscale;  // sqrt(delta_loss_scale) for features >= delta_start
 };
 
-__device__ __forceinline__ void loss_elem(const LossArgs& a, long i, float& l, float& g) {
-  int f = i % a.F;
-  long bt = i / a.F;
-  int b = bt / a.T, tt = bt % a.T;
-  float y = a.y[(long)b * a.ys + (long)tt * a.F + f];
-  float t = a.t[i];
-  float m = (a.mask_padding && t == -100.0f) ? 0.0f : 1.0f;
-  float s = f >= a.delta_start ? a.dscale : 1.0f;
-  float d = (y * m) * s - (t * m) * s;
-  float z = fabsf(d);
-  switch (a.type) {
+// elementwise loss l(d) and dl/dd of the four reference loss types
+__device__ __forceinline__ void loss_fn(int type, float d, float delta, float beta, float& l, float& g) {
+  const float z = fabsf(d);
+  switch (type) {
     case 0:
-      l = z < a.delta ? 0.5f * d * d : a.delta * (z - 0.5f * a.delta);
-      g = d <= -a.delta ? -a.delta : (d >= a.delta ? a.delta : d);
+      l = z < delta ? 0.5f * d * d : delta * (z - 0.5f * delta);
+      g = d <= -delta ? -delta : (d >= delta ? delta : d);
       break;
     case 1:
       l = d * d;
@@ -308,11 +301,98 @@ __device__ __forceinline__ void loss_elem(const LossArgs& a, long i, float& l, f
       g = d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f);
       break;
     default:
-      l = z < a.beta ? 0.5f * d * d / a.beta : z - 0.5f * a.beta;
-      g = z < a.beta ? d / a.beta : (d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f));
+      l = z < beta ? 0.5f * d * d / beta : z - 0.5f * beta;
+      g = z < beta ? d / beta : (d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f));
       break;
   }
+}
+
+__device__ __forceinline__ void loss_elem(const LossArgs& a, long i, float& l, float& g) {
+  int f = i % a.F;
+  long bt = i / a.F;
+  int b = bt / a.T, tt = bt % a.T;
+  float y = a.y[(long)b * a.ys + (long)tt * a.F + f];
+  float t = a.t[i];
+  float m = (a.mask_padding && t == -100.0f) ? 0.0f : 1.0f;
+  float s = f >= a.delta_start ? a.dscale : 1.0f;
+  float d = (y * m) * s - (t * m) * s;
+  loss_fn(a.type, d, a.delta, a.beta, l, g);
   g *= s * m;
+}
+
+// ------------------------------------------------------------- broadcast-target loss
+// Metaformer.prediction returns target [B,T,F] * motion_s_mask [Tm,B,1,F] = [Tm,B,T,F]
+// (lstmformer.py:434-435); generation_step / scheduled-sampling training_step take the masked
+// loss over that broadcast tensor (the [:, :, start:] scaler then indexes its T axis).  Per
+// (b, t, f) the Tm copies collapse analytically: with c1 = #{t' : ms[b,t',f] != -100}, c0 = Tm - c1,
+//   sum_t' l = c1 * (target pad ? 0 : l(s p - s tgt)) + c0 * l(s p)
+// so nothing of size Tm*B*T*F is ever formed.  counts[b*F + f] = c1 (bcast_count_kernel).
+struct BcastArgs {
+  const float* y;
+  long ys;
+  const float* t;
+  const float* counts;
+  int B, T, F, Tm;
+  int type;
+  float delta, beta;
+  int t_start;   // scaler applies to time index t >= t_start (T // (delta_order + 1); > T: none)
+  float dscale;
+};
+
+__global__ __launch_bounds__(256) void bcast_count_kernel(const float* __restrict__ ms, long ms_bs, long ms_ts,
+                                                          int B, int Tm, int F, float* __restrict__ counts) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= B * F) return;
+  const int b = i / F, f = i % F;
+  const float* p = ms + (long)b * ms_bs + f;
+  int c = 0;
+  for (int t = 0; t < Tm; ++t) c += p[(long)t * ms_ts] != -100.0f;
+  counts[i] = (float)c;
+}
+
+__device__ __forceinline__ void bcast_elem(const BcastArgs& a, long i, float& l, float& g) {
+  const int f = i % a.F;
+  const long bt = i / a.F;
+  const int b = bt / a.T, tt = bt % a.T;
+  const float y = a.y[(long)b * a.ys + (long)tt * a.F + f];
+  const float t = a.t[i];
+  const float c1 = a.counts[b * a.F + f];
+  const float c0 = (float)a.Tm - c1;
+  const float s = tt >= a.t_start ? a.dscale : 1.0f;
+  float l1 = 0.0f, g1 = 0.0f, l0, g0;
+  if (t != -100.0f) loss_fn(a.type, y * s - t * s, a.delta, a.beta, l1, g1);
+  loss_fn(a.type, y * s, a.delta, a.beta, l0, g0);
+  l = c1 * l1 + c0 * l0;
+  g = (c1 * g1 + c0 * g0) * s;
+}
+
+__global__ __launch_bounds__(256) void bcast_loss_partial_kernel(BcastArgs a, float* part) {
+  const long n = (long)a.B * a.T * a.F;
+  float acc = 0.0f;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    float l, g;
+    bcast_elem(a, i, l, g);
+    acc += l;
+  }
+  __shared__ float red[4];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(256) void bcast_loss_bwd_kernel(BcastArgs a, const float* grad_out, float inv_n,
+                                                             float* dy) {
+  const long n = (long)a.B * a.T * a.F;
+  const float go = grad_out[0] * inv_n;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    float l, g;
+    bcast_elem(a, i, l, g);
+    const int f = i % a.F;
+    const long bt = i / a.F;
+    const int b = bt / a.T, tt = bt % a.T;
+    dy[(long)b * a.ys + (long)tt * a.F + f] = g * go;
+  }
 }
 
 __global__ __launch_bounds__(256) void loss_fwd_partial_kernel(LossArgs a, float* part) {
@@ -355,10 +435,13 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(LossArgs a, const float* 
 // ------------------------------------------------------------------ AdamW
 // torch.optim.AdamW (lstmformer.py:327-333), one launch over the flat buffers.
 // step / lr live on the device so a captured graph replays correct bias corrections.
+// err (nullable): the persistent-recurrence error flag; a set flag means this step's gradients
+// are garbage (a hand-off timed out), so the update and the step count are skipped.
 __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v, long n,
                                                     const float* __restrict__ step_lr, float wd, float b1,
-                                                    float b2, float eps) {
+                                                    float b2, float eps, const int* __restrict__ err) {
+  if (err && *err) return;
   float t = step_lr[0] + 1.0f;
   float lr = step_lr[1];
   float bc1 = 1.0f - powf(b1, t);
@@ -376,7 +459,9 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
   }
 }
 
-__global__ void adamw_step_inc_kernel(float* step_lr) { step_lr[0] += 1.0f; }
+__global__ void adamw_step_inc_kernel(float* step_lr, const int* err) {
+  if (!(err && *err)) step_lr[0] += 1.0f;
+}
 
 }  // namespace mrg
 
@@ -499,17 +584,71 @@ MRG_API int mrg_masked_loss_bwd(int B, int T, int F, const float* y, long y_bstr
   return check_launch("loss_bwd_kernel");
 }
 
+static int bcast_setup(BcastArgs& a, int B, int T, int F, const float* y, long y_bstride, const float* target,
+                       const float* ms, long ms_bs, long ms_ts, int Tm, int type, float delta, float beta,
+                       int t_start, float dscale, float* workspace, hipStream_t stream) {
+  MRG_REQUIRE(type >= 0 && type <= 3, "mrg_broadcast_loss: bad loss type %d", type);
+  MRG_REQUIRE(B >= 0 && T >= 0 && F >= 1 && Tm >= 0 && ms && workspace,
+              "mrg_broadcast_loss: bad arguments (B=%d T=%d F=%d Tm=%d)", B, T, F, Tm);
+  a.y = y; a.ys = y_bstride; a.t = target; a.counts = workspace; a.B = B; a.T = T; a.F = F; a.Tm = Tm;
+  a.type = type; a.delta = delta; a.beta = beta; a.t_start = t_start; a.dscale = dscale;
+  if (B * F == 0) return 0;
+  bcast_count_kernel<<<(B * F + 255) / 256, 256, 0, stream>>>(ms, ms_bs, ms_ts, B, Tm, F, workspace);
+  return check_launch("bcast_count_kernel");
+}
+
+MRG_API size_t mrg_broadcast_loss_workspace_bytes(int B, int T, int F) {
+  return ((size_t)B * F + (size_t)loss_blocks((long)B * T * F)) * sizeof(float);
+}
+
+MRG_API int mrg_broadcast_loss_fwd(int B, int T, int F, const float* y, long y_bstride, const float* target,
+                                   const float* ms, long ms_bs, long ms_ts, int Tm, int type, float delta,
+                                   float beta, int t_start, float dscale, float* loss_out, float* workspace,
+                                   hipStream_t stream) {
+  BcastArgs a;
+  if (bcast_setup(a, B, T, F, y, y_bstride, target, ms, ms_bs, ms_ts, Tm, type, delta, beta, t_start, dscale,
+                  workspace, stream))
+    return 1;
+  const long n = (long)B * T * F;
+  const double nn = (double)n * (double)Tm;
+  if (n == 0 || Tm == 0) {
+    (void)hipMemsetAsync(loss_out, 0xff, sizeof(float), stream);  // mean over an empty tensor: NaN, as torch
+    return check_launch("mrg_broadcast_loss_fwd");
+  }
+  float* part = workspace + (size_t)B * F;
+  const int nb = loss_blocks(n);
+  bcast_loss_partial_kernel<<<nb, 256, 0, stream>>>(a, part);
+  if (check_launch("bcast_loss_partial_kernel")) return 1;
+  loss_fwd_final_kernel<<<1, 64, 0, stream>>>(part, nb, (float)(1.0 / nn), loss_out);
+  return check_launch("loss_fwd_final_kernel");
+}
+
+MRG_API int mrg_broadcast_loss_bwd(int B, int T, int F, const float* y, long y_bstride, const float* target,
+                                   const float* ms, long ms_bs, long ms_ts, int Tm, int type, float delta,
+                                   float beta, int t_start, float dscale, const float* grad_out, float* dy,
+                                   float* workspace, hipStream_t stream) {
+  BcastArgs a;
+  if (bcast_setup(a, B, T, F, y, y_bstride, target, ms, ms_bs, ms_ts, Tm, type, delta, beta, t_start, dscale,
+                  workspace, stream))
+    return 1;
+  const long n = (long)B * T * F;
+  if (n == 0 || Tm == 0) return 0;
+  bcast_loss_bwd_kernel<<<loss_blocks(n), 256, 0, stream>>>(a, grad_out, (float)(1.0 / ((double)n * Tm)), dy);
+  return check_launch("bcast_loss_bwd_kernel");
+}
+
 // step_lr: device float[2] = {completed steps, lr}; incremented after the update.
+// err: nullable device int; non-zero skips the update (see adamw_kernel).
 MRG_API int mrg_adamw_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, long n,
                            float* step_lr, float weight_decay, float beta1, float beta2, float eps,
-                           hipStream_t stream) {
+                           const int* err, hipStream_t stream) {
   if (n > 0) {
     long nb = (n + 255) / 256;
     int grid = (int)(nb < 4096 ? nb : 4096);
     adamw_kernel<<<grid, 256, 0, stream>>>(params, grads, exp_avg, exp_avg_sq, n, step_lr, weight_decay,
-                                           beta1, beta2, eps);
+                                           beta1, beta2, eps, err);
     if (check_launch("adamw_kernel")) return 1;
   }
-  adamw_step_inc_kernel<<<1, 1, 0, stream>>>(step_lr);
+  adamw_step_inc_kernel<<<1, 1, 0, stream>>>(step_lr, err);
   return check_launch("adamw_step_inc_kernel");
 }

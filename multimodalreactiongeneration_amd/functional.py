@@ -95,8 +95,9 @@ def _ws(nbytes: int, device) -> torch.Tensor:
 
 def _counters(device) -> torch.Tensor:
     """Split-K tickets of the in-launch slab combine (mrg_gemm_f32_ex): zeroed once, every launch
-    leaves them at zero again."""
-    key = torch.device(device).index or 0
+    leaves them at zero again.  One buffer per (device, stream): launches on different streams
+    (e.g. a weight-gradient product on the side stream) never share tickets."""
+    key = (torch.device(device).index or 0, torch.cuda.current_stream(device).cuda_stream)
     if key not in _CNT:
         _CNT[key] = torch.zeros(4096, dtype=torch.int32, device=device)  # MRG_GEMM_COUNTERS
     return _CNT[key]
@@ -199,7 +200,10 @@ def colsum(rows, N, X, ld, out, *, out2=None, beta=1.0, ld_hi=0, rdiv=0, device=
 _WGRAD_SIDE = [os.environ.get("MRG_WGRAD_STREAM", "1") != "0"]
 _SIDE_MIN_ROWS = 2048
 _SIDE = {}
-_JOIN_PENDING = set()
+# device -> autograd graph-task id whose final callback will join the side stream back.  Keyed by
+# the task (torch._C._current_graph_task_id), not a bare flag: a backward that raised after a fork
+# never ran its callback, and a stale flag would make every later backward skip the join.
+_JOIN_PENDING = {}
 
 
 def set_wgrad_stream(on: bool) -> bool:
@@ -222,22 +226,26 @@ class _side:
         dev = torch.device(self.dev)
         key = dev.index or 0
         cur = torch.cuda.current_stream(dev)
+        task = torch._C._current_graph_task_id()
+        s = _SIDE.get(key)
+        if key in _JOIN_PENDING and _JOIN_PENDING[key] != task:
+            # left over from a backward that did not finish: order after its side-stream work
+            cur.wait_stream(s)
+            del _JOIN_PENDING[key]
         if self.rows < _SIDE_MIN_ROWS:
             if key in _JOIN_PENDING:  # order this write after the side stream's pending ones
-                cur.wait_stream(_SIDE[key])
+                cur.wait_stream(s)
             return self
-        s = _SIDE.get(key)
+        if task < 0:  # not inside a backward pass: stay on the current stream
+            return self
         if s is None:
             s = _SIDE[key] = torch.cuda.Stream(device=dev)
         if key not in _JOIN_PENDING:
             def join(cur=cur, s=s, key=key):
                 cur.wait_stream(s)
-                _JOIN_PENDING.discard(key)
-            try:
-                torch.autograd.Variable._execution_engine.queue_callback(join)
-            except RuntimeError:  # not inside a backward pass: stay on the current stream
-                return self
-            _JOIN_PENDING.add(key)
+                _JOIN_PENDING.pop(key, None)
+            torch.autograd.Variable._execution_engine.queue_callback(join)
+            _JOIN_PENDING[key] = task
         s.wait_stream(cur)
         for t in self.keep:
             if t is not None:
@@ -1081,3 +1089,53 @@ def masked_loss(y, target, lead=0, loss_type="huber", delta=1.0, beta=1.0, mask_
     spec = (_LOSS_TYPES[loss_type], float(delta), float(beta), int(mask_padding),
             int(F // (delta_order + 1)), float(math.sqrt(delta_loss_scale)))
     return _LossFn.apply(y, target, int(lead), spec)
+
+
+class _BcastLossFn(Function):
+    """Mean loss over the reference's broadcast [Tm, B, T, F] target, analytically."""
+
+    @staticmethod
+    def forward(ctx, y, target, ms, spec):
+        _lib.require_device(y)
+        y = y.contiguous()
+        target = target.contiguous()
+        B, T, F = y.shape
+        if tuple(target.shape) != (B, T, F) or ms.shape[0] != B or ms.shape[2] != F or ms.stride(2) != 1:
+            raise RuntimeError(f"broadcast loss shapes: y{tuple(y.shape)} target{tuple(target.shape)} "
+                               f"motion_self{tuple(ms.shape)}")
+        lib = _lib.load()
+        loss = torch.empty(1, device=y.device, dtype=torch.float32)
+        ws = _ws(lib.mrg_broadcast_loss_workspace_bytes(B, T, F), y.device)
+        _lib.check(lib.mrg_broadcast_loss_fwd(B, T, F, _ptr(y), T * F, _ptr(target), _ptr(ms), ms.stride(0),
+                                              ms.stride(1), ms.shape[1], *spec, _ptr(loss), _ptr(ws), _stream()),
+                   "broadcast loss fwd")
+        ctx.save_for_backward(y, target, ms)
+        ctx.spec = spec
+        return loss.view(())
+
+    @staticmethod
+    def backward(ctx, gout):
+        y, target, ms = ctx.saved_tensors
+        B, T, F = y.shape
+        lib = _lib.load()
+        dy = torch.empty_like(y)
+        ws = _ws(lib.mrg_broadcast_loss_workspace_bytes(B, T, F), y.device)
+        go = gout.reshape(1).contiguous()
+        _lib.check(lib.mrg_broadcast_loss_bwd(B, T, F, _ptr(y), T * F, _ptr(target), _ptr(ms), ms.stride(0),
+                                              ms.stride(1), ms.shape[1], *ctx.spec, _ptr(go), _ptr(dy), _ptr(ws),
+                                              _stream()), "broadcast loss bwd")
+        return dy, None, None, None
+
+
+def broadcast_masked_loss(pred, target, motion_self, loss_type="huber", delta=1.0, beta=1.0, scaler=True,
+                          delta_order=0, delta_loss_scale=1.0):
+    """The loss the reference takes on Metaformer.prediction's output (lstmformer.py:372-380 in the
+    scheduled-sampling training_step, :413-418 in generation_step): pred [B, T, F] against
+    target * motion_s_mask, which broadcasts to [Tm, B, T, F], mean over all of it.
+    motion_self: the raw (-100 padded) self motion [B, Tm, F] the mask comes from.  scaler: the
+    training step's sqrt(delta_loss_scale) on the T axis from T // (delta_order + 1)."""
+    T = pred.shape[1]
+    t_start = T // (delta_order + 1) if scaler else T + 1
+    spec = (_LOSS_TYPES[loss_type], float(delta), float(beta), int(t_start),
+            float(math.sqrt(delta_loss_scale)) if scaler else 1.0)
+    return _BcastLossFn.apply(pred, target, motion_self, spec)

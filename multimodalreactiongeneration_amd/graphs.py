@@ -8,14 +8,19 @@ HIP dispatch) is paid at capture only.  The scheduled-sampling decode of lstm_wi
 without this.  Inputs must live in static device buffers that the caller refreshes in place
 between replays (``buf.copy_(new)``).
 """
-from typing import Callable
+from typing import Callable, Sequence
 
 import torch
 
 
-def capture(step: Callable[[], object], warmup: int = 2) -> Callable[[], None]:
+def capture(step: Callable[[], object], warmup: int = 2, preserve: Sequence[torch.Tensor] = ()) -> Callable[[], None]:
     """Run ``step`` ``warmup`` times on a side stream (allocator and lazily created workspaces
-    settle), record one call into a HIP graph and return its ``replay``."""
+    settle), record one call into a HIP graph and return its ``replay``.
+
+    preserve: device tensors the warm-up must not change for good (e.g. ``opt.state_tensors()``
+    when the step includes the optimizer): they are snapshotted first and restored after the
+    capture, so the warm-up runs leave no update behind.  Recording itself executes nothing."""
+    saved = [t.detach().clone() for t in preserve]
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
@@ -26,4 +31,8 @@ def capture(step: Callable[[], object], warmup: int = 2) -> Callable[[], None]:
     graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(graph):
         step()
+    with torch.no_grad():
+        for t, v in zip(preserve, saved):
+            t.copy_(v)
+    torch.cuda.synchronize()
     return graph.replay

@@ -221,8 +221,11 @@ class Metaformer(LightningSurface):
     def training_step(self, batch: List, *args, sampling_mask=None):
         if self.use_scheduled_sampling:
             self.log("scheduled_sampling_rate", self.current_epoch / self.max_epochs, logger=True)
-            y, target = self.prediction(batch, use_scheduled_sampling=True, sampling_mask=sampling_mask)
-            loss = self._masked_loss(y, target, 0)
+            pred = self._generate(batch, use_scheduled_sampling=True, sampling_mask=sampling_mask)
+            # the reference's loss over the [T, B, T, F] broadcast target (Q9, lstmformer.py:372-380)
+            loss = Fn.broadcast_masked_loss(pred, batch[-1][0].to(pred.device), batch[2][0].to(pred.device),
+                                            self.model.loss_type, self.huber_delta, self.smoothl1_beta, True,
+                                            self.delta_order, self.delta_loss_scale)
         else:
             lead = batch[4][0].shape[1]
             target = batch[-1][0]
@@ -242,9 +245,12 @@ class Metaformer(LightningSurface):
         gen_loss = self.generation_step(batch)["loss"]
         return {"loss": loss, "gen_loss": gen_loss}
 
-    def generation_step(self, batch: List):
-        pred, target = self.prediction(batch)
-        loss = Fn.masked_loss(pred, target, 0, self.model.loss_type, self.huber_delta, self.smoothl1_beta, True)
+    def generation_step(self, batch: List, sampling_mask=None):
+        """genrt_loss (lstmformer.py:410-424): teacher-forced generation, loss over the broadcast
+        [T, B, T, F] target of prediction (Q9), no scaler."""
+        pred = self._generate(batch, sampling_mask=sampling_mask)
+        loss = Fn.broadcast_masked_loss(pred, batch[-1][0].to(pred.device), batch[2][0].to(pred.device),
+                                        self.model.loss_type, self.huber_delta, self.smoothl1_beta, scaler=False)
         self.log("genrt_loss", loss, prog_bar=False, logger=True)
         return {"loss": loss}
 
@@ -253,12 +259,21 @@ class Metaformer(LightningSurface):
                    sampling_mask=None):
         """Stateless step-by-step generation (the reference never carries state, Q1).
 
-        The reference multiplies target [B,T,F] by a [T,B,1,F] mask, which
-        broadcasts (Q9); here the target is masked elementwise instead.
-        ``sampling_mask`` ([T] bool) overrides the mask drawn from the flags; on the GPU it
-        selects on the device, so the whole generation can be captured as one HIP graph
-        (``graphs.capture``).
+        Returns (prediction [B, T, F], target) with the reference's target: batch target [B, T, F]
+        times motion_s_mask [T, B, 1, F], i.e. the BROADCAST [T, B, T, F] tensor of
+        lstmformer.py:434-435 (Q9).  The training / generation losses never form it
+        (``Fn.broadcast_masked_loss``).  ``sampling_mask`` ([T] bool) overrides the mask drawn from
+        the flags; on the GPU it selects on the device, so the whole generation can be captured as
+        one HIP graph (``graphs.capture``).
         """
+        pred = self._generate(batch, use_scheduled_sampling, full_generation, sampling_mask)
+        ms = batch[2][0].to(pred.device)
+        target = batch[-1][0].to(pred.device) * (ms.transpose(0, 1).unsqueeze(2) != PADDING_VALUE).to(ms.dtype)
+        return pred, target
+
+    def _generate(self, batch: List, use_scheduled_sampling: bool = False, full_generation: bool = False,
+                  sampling_mask=None):
+        """head_motion_generation (lstmformer.py:466-521) after form_generation_init (:523-547)."""
         dev = self.device
         (fb, lf), (mp, lp), (ms, ls) = batch[0], batch[1], batch[2]
         T, B = mp.shape[1], mp.shape[0]
@@ -269,10 +284,7 @@ class Metaformer(LightningSurface):
         ms = ms.to(dev).transpose(0, 1).unsqueeze(2).contiguous()
         fb = fb * (fb != PADDING_VALUE).to(fb.dtype)
         mp = mp * (mp != PADDING_VALUE).to(mp.dtype)
-        msk = (ms != PADDING_VALUE).to(ms.dtype)
-        ms = ms * msk
-        target = batch[-1][0].to(dev)
-        target = target * (target != PADDING_VALUE).to(target.dtype)
+        ms = ms * (ms != PADDING_VALUE).to(ms.dtype)
         empty = [(torch.empty(x.shape[0], 0, x.shape[2], device=dev), n) for x, n in batch]
         _, cell = self.forward(*empty[:3], *batch[3:6], hxs=None)
         if sampling_mask is not None:
@@ -292,7 +304,7 @@ class Metaformer(LightningSurface):
                 y = torch.where(mask[step], y, ms[step])
             else:
                 y = y if bool(mask[step]) else ms[step]
-        return torch.cat(preds, dim=1), target
+        return torch.cat(preds, dim=1)
 
 
 class LSTMwithSample(LightningSurface):

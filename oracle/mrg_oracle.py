@@ -314,6 +314,59 @@ def metaformer_prediction(sd: SD, cfg, batch, sampling_mask: Tensor) -> Tensor:
     return torch.cat(preds, 1)
 
 
+def metaformer_prediction_target(batch) -> Tensor:
+    """The target Metaformer.prediction returns (lstmformer.py:434-435): target [B, T, F] times
+    motion_s_mask [T', B, 1, F] (form_generation_init, :536-547), which BROADCASTS to
+    [T', B, T, F]."""
+    ms = batch[2][0].transpose(0, 1).unsqueeze(2)
+    return batch[-1][0] * (ms != PADDING_VALUE).int()
+
+
+def broadcast_regression_loss(pred: Tensor, target4: Tensor, loss_type: str = "huber", delta: float = 1.0,
+                              beta: float = 1.0, delta_order: int = 0, delta_loss_scale: float = 1.0,
+                              scaler: bool = True) -> Tensor:
+    """The loss lines of training_step (lstmformer.py:372-380) and generation_step (:413-418)
+    applied, as the reference applies them, to prediction [B, T, F] and the broadcast target
+    [T', B, T, F]: the padding mask broadcasts y too, and the scaler's slice ``[:, :, start:]``
+    lands on the T axis of the 4-d tensor (start = T // (delta_order + 1)).  generation_step has
+    no scaler (``scaler=False``)."""
+    m = (target4 != PADDING_VALUE).int()
+    y = pred * m
+    t = target4 * m
+    if scaler:
+        s = torch.ones_like(y)
+        s[:, :, y.shape[2] // (delta_order + 1):] = math.sqrt(delta_loss_scale)
+        y, t = y * s, t * s
+    if loss_type == "huber":
+        return F.huber_loss(y, t, delta=delta)
+    if loss_type == "mse":
+        return F.mse_loss(y, t)
+    if loss_type == "mae":
+        return F.l1_loss(y, t)
+    if loss_type == "smoothl1":
+        return F.smooth_l1_loss(y, t, beta=beta)
+    raise ValueError("invalid loss type")
+
+
+def metaformer_genrt_loss(sd: SD, cfg, batch) -> Tensor:
+    """Metaformer.generation_step (lstmformer.py:410-424): teacher-forced prediction, loss on the
+    broadcast target (Q9), no scaler."""
+    T = batch[1][0].shape[1]
+    pred = metaformer_prediction(sd, cfg, batch, torch.zeros(T, dtype=torch.bool))
+    return broadcast_regression_loss(pred, metaformer_prediction_target(batch), cfg["loss_type"],
+                                     cfg.get("huber_delta", 1.0), cfg.get("smoothl1_beta", 1.0), scaler=False)
+
+
+def metaformer_ss_training_loss(sd: SD, cfg, batch, sampling_mask: Tensor) -> Tuple[Tensor, Tensor]:
+    """Metaformer.training_step with use_scheduled_sampling (lstmformer.py:357-385): the AR
+    prediction under ``sampling_mask`` (the draw of :476), loss on the broadcast target (Q9)."""
+    pred = metaformer_prediction(sd, cfg, batch, sampling_mask)
+    loss = broadcast_regression_loss(pred, metaformer_prediction_target(batch), cfg["loss_type"],
+                                     cfg.get("huber_delta", 1.0), cfg.get("smoothl1_beta", 1.0),
+                                     cfg["delta_order"], cfg.get("delta_loss_scale", 1.0))
+    return loss, pred
+
+
 # ---------------------------------------------------------- lstm_with_sampling
 def lstm_with_sample_forward(sd: SD, cfg, inputs, hx_sampler=None):
     """LSTMwithSample.forward (lstm_with_sample.py:151-232); returns (y, hx_sampler)."""

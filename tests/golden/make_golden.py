@@ -131,6 +131,52 @@ def metaformer_generation_case(name, hidden, nb, enc, bn, B, T, lead, ratio, len
     print("wrote", name, "ss mask", out["sampling_mask"].astype(int).tolist())
 
 
+def metaformer_q9_case(name, hidden, nb, enc, bn, B, T, lead, ratio, lengths, seed=0, epoch=30,
+                       delta_order=1, delta_loss_scale=2.0):
+    """The broadcast-target losses of the lstmformer AR path: prediction multiplies
+    target [B,T,F] by motion_s_mask [T,B,1,F] (lstmformer.py:434-435, mask from :540-547), so
+    generation_step's genrt_loss (:410-424) and the scheduled-sampling training_step loss
+    (:357-385, scaler along dim 2 of the [T,B,T,F] tensor) are means over a broadcast tensor.
+    Ragged -100 padding, delta_order 1 and delta_loss_scale != 1 make every term of it live."""
+    nm = 39
+    model_cfg, optim, metrics = C.lstmformer_config(hidden=hidden, num_block=nb, encoder_num_layer=enc,
+                                                    bottleneck=bn, ratio=ratio, lr=1e-3, nmels=nm,
+                                                    delta_order=delta_order, delta_loss_scale=delta_loss_scale,
+                                                    use_scheduled_sampling=True)
+    torch.manual_seed(seed)
+    m = R.Metaformer(model_cfg, optim, metrics)
+    m.current_epoch = epoch
+    batch = make_batch(B=B, T=T, lead=lead, ratio=ratio, seed=1234 + seed, lengths=lengths,
+                       feat_audio=(nm + 1) * (delta_order + 1), feat_motion=6 * (delta_order + 1))
+    out = {"meta/config": json.dumps(dict(model=model_cfg, optim=optim, metrics=metrics)),
+           "meta/epoch": np.int64(epoch)}
+    pack_batch(out, batch)
+    m.eval()
+    with torch.no_grad():
+        pred, target4 = m.prediction(clone_batch(batch))
+        out["gen/pred"] = _np(pred)
+        out["gen/target4"] = _np(target4)
+        out["genrt_loss"] = np.float32(m.generation_step(clone_batch(batch))["loss"].item())
+    m.train()
+    rec = {}
+    orig = torch.rand
+
+    def _rand(*a, **k):
+        r = orig(*a, **k)
+        rec.setdefault("mask_rand", r.clone())
+        return r
+    torch.manual_seed(7)
+    torch.rand = _rand
+    try:
+        run_train_step(m, clone_batch(batch), out)
+    finally:
+        torch.rand = orig
+    out["sampling_mask"] = (rec["mask_rand"] < epoch / model_cfg["max_epochs"]).numpy()
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    print("wrote", name, "loss", out["loss"], "genrt", out["genrt_loss"], "mask",
+          out["sampling_mask"].astype(int).tolist())
+
+
 def lstm_with_sample_case(name, hidden, sh, B, T, lead, ratio, scheduled=False, epoch=30,
                           seed=0, lengths=None):
     model_cfg, optim, metrics = C.lstm_with_sampling_config(
@@ -407,7 +453,15 @@ def generation_cases():
                                lengths=[6, 5, 4], seed=3)
 
 
+def q9_cases():
+    metaformer_q9_case("metaformer_q9_r2_pad", 32, 2, 2, 16, B=3, T=6, lead=2, ratio=2,
+                       lengths=[6, 4, 5], seed=6)
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["q9"]:
+        q9_cases()
+        sys.exit(0)
     if sys.argv[1:] == ["generation"]:  # only the generation fixtures (the others stay as committed)
         generation_cases()
         sys.exit(0)
@@ -421,6 +475,7 @@ if __name__ == "__main__":
         gru_cases()
         sys.exit(0)
     generation_cases()
+    q9_cases()
     feature_cases()
     dataset_cases()
     gru_cases()

@@ -132,3 +132,39 @@ def test_synthetic_batch_format():
     assert b[0][0].shape == (3, 10, 40) and b[3][0].shape == (3, 4, 40)
     assert (b[1][0][1, 3:] == -100).all() and (b[0][0][1, 6:] == -100).all()
     assert b[1][1].tolist() == [5, 3, 1]
+
+
+@pytest.mark.parametrize("model_type", ["lstmformer", "lstm_with_sampling", "simple_lstm"])
+def test_checkpoint_round_trip_through_load_model(tmp_path, model_type):
+    """model_loader.load_model (model_loader.py:13-26): a Lightning-shaped checkpoint
+    {"state_dict", "epoch", "global_step", optimizer / scheduler states} written with torch.save
+    loads through the pickle-free weights_only path into a fresh model, bit-exact."""
+    from multimodalreactiongeneration_amd import configs as C
+    from multimodalreactiongeneration_amd.model import models as M
+    build = {"lstmformer": (C.lstmformer_config, dict(hidden=32, num_block=2, encoder_num_layer=2, bottleneck=16)),
+             "lstm_with_sampling": (C.lstm_with_sampling_config, dict(hidden=32, sampler_hidden=16, bottleneck=8)),
+             "simple_lstm": (C.simple_lstm_config, dict(hidden=32, lstm=16, bottleneck=8, att_heads=4))}
+    fn, kw = build[model_type]
+    mc, oc, me = fn(**kw)
+    cls = {"lstmformer": M.Metaformer, "lstm_with_sampling": M.LSTMwithSample, "simple_lstm": M.SimpleLSTM}
+    torch.manual_seed(11)
+    src = cls[model_type](mc, oc, me)
+    sd = src.state_dict()
+    ckpt = {"state_dict": sd, "epoch": 7, "global_step": 1234, "pytorch-lightning_version": "2.0.2",
+            "optimizer_states": [{"state": {0: {"step": torch.tensor(3.0), "exp_avg": torch.zeros(3)}},
+                                  "param_groups": [{"lr": 5e-6, "weight_decay": 1e-2, "params": [0]}]}],
+            "lr_schedulers": [{"T_max": 100, "last_epoch": 7, "base_lrs": [5e-6]}]}
+    path = tmp_path / "last.ckpt"
+    torch.save(ckpt, path)
+    cfg = {"model": mc, "optim": oc, "metrics": me}
+    got = M.load_model(model_type, str(path), cfg)
+    out = got.state_dict()
+    assert list(out.keys()) == list(sd.keys())
+    for k in sd:
+        assert torch.equal(out[k], sd[k]), k
+    # a bare state_dict file (no Lightning wrapper) loads too
+    torch.save(sd, tmp_path / "bare.pt")
+    got2 = M.load_model(model_type, str(tmp_path / "bare.pt"), cfg)
+    assert all(torch.equal(got2.state_dict()[k], sd[k]) for k in sd)
+    with pytest.raises(ValueError):
+        M.load_model("gru_former", str(path), cfg)

@@ -288,3 +288,104 @@ def test_wgrad_side_stream_bitwise():
         assert torch.equal(opt.flat_grad, ref)
     finally:
         Fn.set_wgrad_stream(prev)
+
+
+def test_metaformer_q9_broadcast_losses_golden():
+    """the reference's genrt_loss (generation_step, lstmformer.py:410-424) and its
+    scheduled-sampling training_step (:357-385) take the loss over target * motion_s_mask, a
+    [T, B, T, F] broadcast (:434-435); ragged padding, delta_order 1, delta_loss_scale 2.  Loss,
+    every gradient and the AdamW step vs the reference's own numbers."""
+    from multimodalreactiongeneration_amd.model import Metaformer
+    d = load("metaformer_q9_r2_pad")
+    m, cfg = _build(Metaformer, d)
+    m.current_epoch = int(d["meta/epoch"])
+    batch = batch_from(d, DEV)
+    m.eval()
+    with torch.no_grad():
+        pred, target4 = m.prediction([(x.clone(), n) for x, n in batch])
+        assert rel_err(pred, d["gen/pred"]) < TOL
+        assert tuple(target4.shape) == d["gen/target4"].shape
+        assert torch.equal(target4.cpu(), torch.from_numpy(d["gen/target4"]))
+        g = m.generation_step([(x.clone(), n) for x, n in batch])["loss"]
+        assert abs(g.item() - float(d["genrt_loss"])) / float(d["genrt_loss"]) < TOL
+    m.train()
+    loss, opt = _train_step(m, batch, sampling_mask=torch.from_numpy(d["sampling_mask"]))
+    _check(d, m, loss)
+    opt.step()
+    torch.cuda.synchronize()
+    _check_after(d, m)
+
+
+def test_lstm_with_sample_benchmark_width_vs_oracle():
+    """BASELINE configs[2] architecture (H=256, sampler 2 x 128, r=1) at T=300: scheduled-sampling
+    training step (mask RandomState(7) < 0.5, lead 12, ragged lengths) and the teacher-forced
+    step, loss + every gradient vs the CPU oracle."""
+    from multimodalreactiongeneration_amd import configs as C
+    from multimodalreactiongeneration_amd.model import LSTMwithSample
+    from multimodalreactiongeneration_amd.synthetic import make_batch, clone_batch
+    from oracle import mrg_oracle as O
+    T = 300
+    mask = torch.from_numpy(np.random.RandomState(7).rand(T) < 0.5)
+    for scheduled in (True, False):
+        mc, oc, me = C.lstm_with_sampling_config(use_scheduled_sampling=scheduled)
+        torch.manual_seed(1)
+        m = LSTMwithSample(mc, oc, me)
+        m.current_epoch = 30
+        sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+        m = m.to(DEV)
+        batch = make_batch(B=3, T=T, lead=12, seed=17, lengths=[300, 251, 177])
+        kw = {"sampling_mask": mask} if scheduled else {}
+        loss, _ = _train_step(m, clone_batch(batch, DEV), **kw)
+        ref_loss, _, grads, _ = O.run_train_step(O.lstm_with_sample_training_loss, sd, oc, mc, clone_batch(batch),
+                                                 **kw)
+        assert abs(loss.item() - ref_loss.item()) / abs(ref_loss.item()) < TOL, scheduled
+        worst = max((rel_err(p.grad, grads[k]), k) for k, p in m.named_parameters())
+        assert worst[0] < TOL, (scheduled, worst)
+
+
+def test_simple_lstm_benchmark_width_vs_oracle():
+    """BASELINE configs[1] architecture (bi-LSTM H=128 encoders x 2, 3 x 8-head cross attention,
+    5-layer bi-LSTM decoder) at T=300, B=2, fp32: loss + every gradient vs the CPU oracle."""
+    from multimodalreactiongeneration_amd import configs as C
+    from multimodalreactiongeneration_amd.model import SimpleLSTM
+    from multimodalreactiongeneration_amd.synthetic import make_simple_batch
+    from oracle import mrg_oracle as O
+    cfg, oc, me = C.simple_lstm_config()
+    torch.manual_seed(2)
+    m = SimpleLSTM(cfg, oc, me)
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.to(DEV)
+    a, mo, t = make_simple_batch(B=2, T=300, seed=19)
+    loss, _ = _train_step(m, (a.to(DEV), mo.to(DEV), t.to(DEV)))
+    ref_loss, _, grads, _ = O.run_train_step(O.simple_lstm_training_loss, sd, oc, cfg, a, mo, t)
+    assert abs(loss.item() - ref_loss.item()) / abs(ref_loss.item()) < TOL
+    worst = max((rel_err(p.grad, grads[k]), k) for k, p in m.named_parameters())
+    assert worst[0] < TOL, worst
+
+
+def test_metaformer_q9_benchmark_width_vs_oracle():
+    """Benchmark architecture (H=256, 5 blocks, 5 encoder layers, r=1), 24 frames, ragged: the
+    scheduled-sampling training loss over the Q9 broadcast target + every gradient, and the
+    genrt_loss, vs the CPU oracle."""
+    from multimodalreactiongeneration_amd import configs as C
+    from multimodalreactiongeneration_amd.model import Metaformer
+    from multimodalreactiongeneration_amd.synthetic import make_batch, clone_batch
+    from oracle import mrg_oracle as O
+    mc, oc, me = C.lstmformer_config(ratio=1, use_scheduled_sampling=True)
+    torch.manual_seed(0)
+    m = Metaformer(mc, oc, me)
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.to(DEV)
+    T = 24
+    batch = make_batch(B=3, T=T, lead=4, seed=23, lengths=[24, 19, 11])
+    mask = torch.from_numpy(np.random.RandomState(7).rand(T) < 0.5)
+    loss, _ = _train_step(m, clone_batch(batch, DEV), sampling_mask=mask)
+    ref_loss, _, grads, _ = O.run_train_step(O.metaformer_ss_training_loss, sd, oc, mc, clone_batch(batch),
+                                             sampling_mask=mask)
+    assert abs(loss.item() - ref_loss.item()) / abs(ref_loss.item()) < TOL
+    worst = max((rel_err(p.grad, grads[k]), k) for k, p in m.named_parameters())
+    assert worst[0] < TOL, worst
+    with torch.no_grad():
+        g = m.generation_step(clone_batch(batch, DEV))["loss"]
+        ref_g = O.metaformer_genrt_loss(sd, mc, clone_batch(batch))
+    assert abs(g.item() - ref_g.item()) / abs(ref_g.item()) < TOL

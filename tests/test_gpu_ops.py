@@ -520,3 +520,65 @@ def test_gru_vs_torch_fp64(In, H, B, T, bidir, state):
     gp = dict(g.named_parameters())
     for k, p in ref.named_parameters():
         assert rel_err(gp[k].grad, p.grad) < TOL, k
+
+
+def test_adamw_graph_replay_follows_lr_scheduler():
+    """A replayed graph holding opt.step() uses the LR the CosineAnnealingLR scheduler sets between
+    replays (the device-side LR follows param_groups[0]['lr']), and capture(preserve=...) leaves
+    no warm-up update behind: three replays == three torch.optim.AdamW steps."""
+    from multimodalreactiongeneration_amd.graphs import capture
+    from multimodalreactiongeneration_amd.optim import FusedAdamW
+    g = torch.Generator().manual_seed(4)
+    p0 = [torch.randn(64, 33, generator=g), torch.randn(517, generator=g)]
+    grads = [torch.randn(t.shape, generator=g) for t in p0]
+    params = [torch.nn.Parameter(t.clone().to(DEV)) for t in p0]
+    opt = FusedAdamW(params, lr=1e-2, weight_decay=1e-2)
+    sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=4)
+    for p, gr in zip(params, grads):
+        p.grad.copy_(gr.to(DEV))
+    replay = capture(opt.step, 2, preserve=opt.state_tensors())
+    ref = [torch.nn.Parameter(t.clone()) for t in p0]
+    ropt = torch.optim.AdamW(ref, lr=1e-2, weight_decay=1e-2)
+    rsched = torch.optim.lr_scheduler.CosineAnnealingLR(ropt, T_max=4)
+    for _ in range(3):
+        replay()
+        for p, gr in zip(ref, grads):
+            p.grad = gr.clone()
+        ropt.step()
+        sched.step()
+        rsched.step()
+    torch.cuda.synchronize()
+    for p, r in zip(params, ref):
+        assert rel_err(p.detach(), r.detach()) < 1e-6
+
+
+def test_lstm_handoff_timeout_skips_adamw_and_raises():
+    """A persistent-LSTM hand-off timeout (forced with mrg_lstm_debug_inject) must not train on its
+    garbage gradients: the AdamW kernel skips the update, FusedAdamW.step raises at the next step
+    and check_errors() raises."""
+    from multimodalreactiongeneration_amd import _lib as L
+    from multimodalreactiongeneration_amd import functional as Fn
+    from multimodalreactiongeneration_amd.optim import FusedAdamW
+    torch.manual_seed(3)
+    H, B, T = 64, 4, 12
+    ws = [torch.nn.Parameter((torch.randn(4 * H, H) * 0.1).to(DEV)) for _ in range(2)]
+    bs = [torch.nn.Parameter(torch.zeros(4 * H).to(DEV)) for _ in range(2)]
+    opt = FusedAdamW(ws + bs, lr=1e-3)
+    x = torch.randn(B, T, H, device=DEV)
+    before = opt.flat.clone()
+    L.check(L.load().mrg_lstm_debug_inject(1), "inject")
+    y, _, _ = Fn.lstm_layer(x, ws[0], ws[1], bs[0], bs[1])
+    y.square().sum().backward()
+    opt.step()
+    torch.cuda.synchronize()
+    assert torch.equal(opt.flat, before)          # update skipped on the device
+    assert float(opt.step_lr[0]) == 0.0           # and not counted
+    with pytest.raises(RuntimeError, match="timed out"):
+        opt.step()                                # the next host-visible point raises
+    Fn.check_errors()                             # flag cleared by the raise above
+    y, _, _ = Fn.lstm_layer(x, ws[0], ws[1], bs[0], bs[1])   # a clean launch works again
+    y.square().sum().backward()
+    opt.step()
+    torch.cuda.synchronize()
+    Fn.check_errors()
+    assert not torch.equal(opt.flat, before)

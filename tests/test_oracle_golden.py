@@ -224,6 +224,28 @@ def test_metaformer_generation(mode):
     assert rel_err(pred, d[f"pred/{mode}"]) < TOL
 
 
+def test_metaformer_q9_broadcast_losses():
+    """SURVEY Q9 (lstmformer.py:434-435): prediction's target broadcasts to [T,B,T,F]; the
+    reference's genrt_loss (generation_step) and scheduled-sampling training_step loss + grads +
+    AdamW step are taken over it (ragged padding, delta_order 1, delta_loss_scale 2)."""
+    d = load("metaformer_q9_r2_pad")
+    cfg = config(d)
+    sd = prefixed(d, "param/")
+    batch = batch_from(d)
+    T = batch[1][0].shape[1]
+    with torch.no_grad():
+        pred = O.metaformer_prediction(sd, cfg["model"], batch, torch.zeros(T, dtype=torch.bool))
+        assert rel_err(pred, d["gen/pred"]) < TOL
+        t4 = O.metaformer_prediction_target(batch)
+        assert t4.shape == d["gen/target4"].shape and torch.equal(t4.float(), torch.from_numpy(d["gen/target4"]))
+        g = O.metaformer_genrt_loss(sd, cfg["model"], batch)
+        assert abs(g.item() - float(d["genrt_loss"])) / float(d["genrt_loss"]) < TOL
+    mask = torch.from_numpy(d["sampling_mask"])
+    loss, y, grads, after = O.run_train_step(O.metaformer_ss_training_loss, sd, cfg["optim"], cfg["model"],
+                                             batch, sampling_mask=mask)
+    _check_train(d, loss, y, grads, after, check_y=False)
+
+
 def test_feature_log_power_and_deltas_golden():
     """compute_log_power (audio.py:43-56) and compute_delta (audio.py:58-67) as the reference
     itself computed them (tests/golden/features.npz): bit-exact."""
