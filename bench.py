@@ -8,6 +8,12 @@ GPU (weak scaling).  Inputs are resident in HBM before timing.  Prints ONE
 JSON line on rank 0 with the live roofline of the dominant kernel (HIP events
 around its launches inside the timed region) and the CPU oracle baseline
 timed on this host (rank 0, N=1 only).
+
+At N=1 the same line carries a ``secondary`` block with the other 1-GPU
+BASELINE configs, each graph-replayed with its own ms/step,
+frames/s, whole-step roofline, dominant-kernel roofline and a CPU baseline on a
+bounded sample: C2 simple_lstm (fp32 and bf16), C3 lstm_with_sampling scheduled
+sampling, and lstmformer autoregressive generation (§8f rank 1).
 """
 import argparse
 import json
@@ -24,6 +30,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "training frames/sec/GPU, lstmformer T=300 B=64; 1→8 GPU scaling"
 FP32_MFMA_PEAK_TF = 157.3   # MI355X_MICROARCH.md chip table (f32 matrix, dense)
+BF16_MFMA_PEAK_TF = 2500.0  # MI355X_MICROARCH.md chip table (bf16 matrix, dense)
 HBM_PEAK_GBS = 8000.0
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
 
@@ -57,6 +64,14 @@ def pmc_traffic(family):
         return None
 
 
+_T0 = time.perf_counter()
+
+
+def progress(msg):
+    """One progress line on stderr (stdout carries only the JSON result line)."""
+    print(f"[bench {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -67,8 +82,10 @@ def parse():
     ap.add_argument("--ratio", type=int, default=1, help="audio frames per prediction frame (8 = reference rate)")
     ap.add_argument("--graph", type=int, default=1, help="replay the step as a HIP graph")
     ap.add_argument("--cpu-baseline", type=int, default=1)
-    ap.add_argument("--cpu-steps", type=int, default=2)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-steps", type=int, default=5, help="timed CPU steps of the headline baseline")
+    ap.add_argument("--cpu-warmup", type=int, default=2)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every physical core this process may use")
+    ap.add_argument("--secondary", type=int, default=1, help="time the other 1-GPU BASELINE configs (N=1 only)")
     ap.add_argument("--wgrad-stream", type=int, default=1,
                     help="weight-gradient GEMMs on a side stream (functional._side); 0 = one stream")
     ap.add_argument("--lstm-group", type=int, default=0, help="workgroups per LSTM row group at H=256 (8|16; 0 = library default)")
@@ -93,29 +110,317 @@ def attn_flops_per_frame(cfg, ratio, T):
     return 3.0 * fwd
 
 
+def host_cpu():
+    """(physical cores, logical CPUs, model name) of the CPUs this process may run on (/proc/cpuinfo
+    restricted to sched_getaffinity): the CPU baseline uses every physical core."""
+    allowed = os.sched_getaffinity(0)
+    cores, model, cur = set(), "unknown", {}
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in list(f) + ["\n"]:
+                if not line.strip():
+                    if cur.get("processor") is not None and int(cur["processor"]) in allowed:
+                        cores.add((cur.get("physical id", "0"), cur.get("core id", cur["processor"])))
+                        model = cur.get("model name", model)
+                    cur = {}
+                    continue
+                k, _, v = line.partition(":")
+                cur[k.strip()] = v.strip()
+    except OSError:
+        pass
+    return max(1, len(cores)), len(allowed), model
+
+
+_CPU = {}
+
+
+def _cpu_setup(args):
+    """Thread count of every CPU baseline, chosen once: the fastest of {8, 16, 32, 64, all physical
+    cores} on a bounded lstmformer training sample (B=8, T=300), because on a shared multi-GPU host
+    the oneDNN LSTM slows down past the cores it really gets (r02: 128 threads ran the headline step
+    5-9x slower than 16).  --cpu-threads N pins it instead.  The sweep is reported."""
+    if _CPU:
+        torch.set_num_threads(_CPU["cores"])
+        return dict(_CPU)
+    phys, logical, model = host_cpu()
+    sweep = {}
+    if args.cpu_threads > 0:
+        best = args.cpu_threads
+    else:
+        from oracle import mrg_oracle as O
+        from multimodalreactiongeneration_amd import configs as C
+        from multimodalreactiongeneration_amd.model import Metaformer
+        from multimodalreactiongeneration_amd.synthetic import make_batch, clone_batch
+        O.ATEN_LSTM = True
+        mc, oc, me = C.lstmformer_config(ratio=1)
+        torch.manual_seed(0)
+        sd = {k: v.detach().clone() for k, v in Metaformer(mc, oc, me).state_dict().items()}
+        batch = make_batch(B=8, T=300, seed=1234)
+        for t in sorted({c for c in (8, 16, 32, 64, phys) if c <= phys}):
+            torch.set_num_threads(t)
+            O.run_train_step(O.metaformer_training_loss, sd, oc, mc, clone_batch(batch))
+            t0 = time.perf_counter()
+            O.run_train_step(O.metaformer_training_loss, sd, oc, mc, clone_batch(batch))
+            sweep[t] = round(time.perf_counter() - t0, 3)
+            progress(f"  cpu thread sweep: {t} threads {sweep[t]:.2f} s")
+        best = min(sweep, key=sweep.get)
+    torch.set_num_threads(best)
+    _CPU.update(cores=torch.get_num_threads(), physical_cores_available=phys, logical_cpus_available=logical,
+                cpu_model=model, thread_sweep_s_per_B8_step=sweep or None)
+    return dict(_CPU)
+
+
+def _median(xs):
+    xs = sorted(xs)
+    return xs[len(xs) // 2]
+
+
+def _time_cpu(fn, warm, steps):
+    for i in range(warm):
+        fn()
+        progress(f"  cpu warm-up {i + 1}/{warm}")
+    times = []
+    for i in range(steps):
+        t0 = time.perf_counter()
+        fn()
+        times.append(time.perf_counter() - t0)
+        progress(f"  cpu step {i + 1}/{steps}: {times[-1]:.2f} s ({torch.get_num_threads()} threads)")
+    return _median(times)
+
+
 def cpu_baseline(args, mc, oc):
     """The oracle (CPU fp32 restatement of the reference, same workload) on this host's cores."""
     from oracle import mrg_oracle as O
     from multimodalreactiongeneration_amd.model import Metaformer
     from multimodalreactiongeneration_amd.synthetic import make_batch, clone_batch
-    torch.set_num_threads(args.cpu_threads)
+    info = _cpu_setup(args)
     O.ATEN_LSTM = True   # the oneDNN LSTM op the reference's nn.LSTM runs on CPU, not the parity loop
     torch.manual_seed(0)
     sd = {k: v.detach().clone() for k, v in Metaformer(mc, oc, {"use_centroid": True, "use_angle": True,
                                                                    "delta_order": 0}).state_dict().items()}
     batch = make_batch(B=args.batch, T=args.seq, ratio=args.ratio, seed=1234)
-    times = []
-    for i in range(1 + args.cpu_steps):
-        t0 = time.perf_counter()
-        O.run_train_step(O.metaformer_training_loss, sd, oc, mc, clone_batch(batch))
-        times.append(time.perf_counter() - t0)
-    t = sorted(times[1:])[len(times[1:]) // 2]
-    return {"value": round(args.batch * args.seq / t, 2), "unit": "frames/s", "cores": torch.get_num_threads(),
-            "kind": "port",
-            "sample": f"oracle/mrg_oracle.py lstmformer train step (fwd+loss+bwd+AdamW; LSTMs on the "
-                      f"fused ATen op nn.LSTM uses on CPU) B={args.batch} T={args.seq} r={args.ratio}, median of "
-                      f"{args.cpu_steps} steps after 1 warm-up, {torch.get_num_threads()} threads, "
-                      f"{time.strftime('%Y-%m-%d')}"}
+    t = _time_cpu(lambda: O.run_train_step(O.metaformer_training_loss, sd, oc, mc, clone_batch(batch)),
+                  args.cpu_warmup, args.cpu_steps)
+    return dict(value=round(args.batch * args.seq / t, 2), unit="frames/s", kind="port", **info,
+                sample=f"oracle/mrg_oracle.py lstmformer train step (fwd+loss+bwd+AdamW; LSTMs on the fused ATen op "
+                       f"nn.LSTM uses on CPU) B={args.batch} T={args.seq} r={args.ratio} (the full workload), median "
+                       f"of {args.cpu_steps} steps after {args.cpu_warmup} warm-up, {info['cores']} threads, "
+                       f"{time.strftime('%Y-%m-%d')}")
+
+
+def families(per, nsteps):
+    """Per kernel family: time, launches, algorithmic FLOPs and achieved TF/s over ``nsteps`` probed
+    steps; returns (kernels, roofline of the family with the most time per step)."""
+    kernels, roof = {}, None
+    for f in FAMILIES:
+        v = per.get(f, [])
+        if not v:
+            continue
+        fms = sum(t for t, _ in v) / nsteps
+        work = sum(w for _, w in v) / nsteps
+        n = len(v) / nsteps
+        tf = work / (fms / 1e3) / 1e12
+        kernels[f] = {"kernel": FAMILIES[f], "ms_per_step": round(fms, 3), "launches_per_step": n,
+                      "avg_launch_ms": round(fms / n, 4), "algorithmic_flop_per_launch": work / n,
+                      "achieved_tflops": round(tf, 2), "frac_of_fp32_peak": round(tf / FP32_MFMA_PEAK_TF, 4)}
+    if kernels:
+        dom = max(kernels, key=lambda f: kernels[f]["ms_per_step"])
+        k = kernels[dom]
+        roof = {"kernel": k["kernel"], "family": dom, "bound": "mfma", "achieved": k["achieved_tflops"],
+                "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s", "frac": k["frac_of_fp32_peak"],
+                "traffic": pmc_traffic(dom), "avg_launch_ms": k["avg_launch_ms"],
+                "launches_per_step": k["launches_per_step"],
+                "algorithmic_flop_per_launch": k["algorithmic_flop_per_launch"],
+                "peak_note": PEAK_NOTES.get(dom, "")}
+    return kernels, roof
+
+
+def gen_flops_per_frame(cfg, ratio):
+    """Algorithmic forward FLOPs of one generated frame (Metaformer.prediction: a T = 1 forward with
+    zero recurrent state, lstmformer.py:498-521): LSTM input projections only (8H^2 per token-layer;
+    h0 = 0 makes h W_hh zero work), the Linear layers at T = 1, one visible attention pair per head."""
+    H, Hb, N, E = cfg.hidden_size, cfg.bottleneck_size, cfg.num_block, cfg.encoder_num_layer
+    Fa, Fm = 40, 6
+    L = N + E * ratio + E
+    lin = (4 * H * Fm + 2 * ratio * H * Fa + 2 * H * H * L
+           + N * (12 * H * H + 4 * H * H * (ratio + 1) + 4 * H * H + 4 * H * Hb) + 2 * (H * Hb + Hb * Fm))
+    return 8 * H * H * L + lin + N * 4 * H * (ratio + 1)
+
+
+# SURVEY §8d algorithmic training FLOPs per frame (fwd x 3), B = 64, T = 300, r = 1
+C2_MFLOP_PER_FRAME = 677.3e3 / (64 * 300)      # simple_lstm: 677.3 GFLOP / step
+C3_MFLOP_PER_FRAME = 97.25e3 / (64 * 300)      # lstm_with_sampling scheduled sampling: 97.25 GFLOP / step
+
+
+def _timed_replay(replay, steps, warm, pre=None):
+    for _ in range(warm):
+        if pre is not None:
+            pre()
+        replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        if pre is not None:
+            pre()
+        replay()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps * 1e3
+
+
+def _probe_steps(step, n=1):
+    from multimodalreactiongeneration_amd import functional as Fn
+    side = Fn.set_wgrad_stream(False)
+    Fn.probe_start(*FAMILIES)
+    for _ in range(n):
+        step()
+    per = Fn.probe_stop(with_work=True)
+    Fn.set_wgrad_stream(side)
+    return families(per, n)
+
+
+def _secondary_entry(workload, ms, frames, flop_per_frame, dtype, kern, cpu, peak=FP32_MFMA_PEAK_TF,
+                     peak_note="fp32 dense matrix peak"):
+    kernels, roof = kern
+    if roof is not None:   # the committed PMC summary is of the headline workload, not this one
+        roof = dict(roof, traffic=None)
+    value = frames / ms * 1e3
+    ach = flop_per_frame * value / 1e12
+    return {"workload": workload, "ms_per_step": round(ms, 3), "value": round(value, 2), "unit": "frames/s",
+            "dtype": dtype,
+            "whole_step_roofline": {"bound": "mfma", "algorithmic_mflop_per_frame": round(flop_per_frame / 1e6, 3),
+                                    "achieved_tflops": round(ach, 3), "peak": peak, "frac": round(ach / peak, 4),
+                                    "peak_note": peak_note},
+            "roofline": roof, "kernels": kernels, "cpu_baseline": cpu,
+            "speedup_vs_cpu_baseline": None if not cpu else round(value / cpu["value"], 1)}
+
+
+def secondary(args, dev):
+    """The other 1-GPU BASELINE configs (configs[1], configs[2]) and lstmformer generation (§8f1)."""
+    import numpy as np
+    from multimodalreactiongeneration_amd import configs as C
+    from multimodalreactiongeneration_amd import functional as Fn
+    from multimodalreactiongeneration_amd.graphs import capture
+    from multimodalreactiongeneration_amd.model import LSTMwithSample, SimpleLSTM, Metaformer
+    from multimodalreactiongeneration_amd.synthetic import make_batch, make_simple_batch
+    out = {}
+    K, W, B, T = 10, 3, 64, 300
+    cpu_on = args.cpu_baseline
+    from oracle import mrg_oracle as O  # CPU baselines only (bounded samples)
+    O.ATEN_LSTM = True
+
+    # C2 simple_lstm, B=64 T=300 (BASELINE configs[1])
+    for dtype in ("fp32", "bf16"):
+        cfg, oc, me = C.simple_lstm_config()
+        torch.manual_seed(0)
+        m = SimpleLSTM(cfg, oc, me).set_precision("32" if dtype == "fp32" else "bf16")
+        sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+        m = m.to(dev)
+        opt = m.configure_optimizers()["optimizer"]
+        batch = make_simple_batch(B=B, T=T, device=dev)
+
+        def step_c2():
+            opt.zero_grad()
+            m.training_step(batch)["loss"].backward()
+            opt.step()
+        progress(f"C2 simple_lstm {dtype}")
+        replay = capture(step_c2, 2, preserve=opt.state_tensors())
+        ms = _timed_replay(replay, K, W)
+        kern = _probe_steps(step_c2)
+        cpu = None
+        if cpu_on and dtype == "fp32":   # one CPU reference (fp32) serves both precisions
+            info = _cpu_setup(args)
+            cb = 8
+            a, mo, tg = make_simple_batch(B=cb, T=T, seed=1234)
+            t = _time_cpu(lambda: O.run_train_step(O.simple_lstm_training_loss, sd, oc, cfg, a, mo, tg), 1, 1)
+            cpu = dict(value=round(cb * T / t, 2), unit="frames/s", kind="port", **info,
+                       sample=f"oracle simple_lstm train step (fwd+MSE+bwd+AdamW, fused ATen LSTMs) on a bounded "
+                              f"sample B={cb} T={T} (same per-clip work as B=64), 1 timed after 1 warm-up")
+        if dtype == "bf16":
+            cpu = out["C2_simple_lstm_fp32"]["cpu_baseline"]
+            out[f"C2_simple_lstm_{dtype}"] = _secondary_entry(
+                "simple_lstm train step B=64 T=300 (BASELINE configs[1]) with model.precision='bf16': GEMM "
+                "operands bf16 on the bf16 matrix cores, fp32 accumulation; recurrence, LayerNorm, softmax, "
+                "loss and AdamW fp32; HIP graph", ms, B * T, C2_MFLOP_PER_FRAME * 1e6,
+                "bf16 (GEMM operands) / fp32 accumulate", kern, cpu, peak=BF16_MFMA_PEAK_TF,
+                peak_note="bf16 dense matrix peak (the configured compute dtype)")
+        else:
+            out[f"C2_simple_lstm_{dtype}"] = _secondary_entry(
+                "simple_lstm train step B=64 T=300 (BASELINE configs[1] shape) in fp32, HIP graph", ms, B * T,
+                C2_MFLOP_PER_FRAME * 1e6, dtype, kern, cpu)
+        del m, opt, replay
+
+    progress("C3 scheduled sampling")
+    # C3 lstm_with_sampling, scheduled sampling (BASELINE configs[2])
+    mc, oc, me = C.lstm_with_sampling_config(use_scheduled_sampling=True)
+    torch.manual_seed(0)
+    m = LSTMwithSample(mc, oc, me)
+    m.current_epoch = 30
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.to(dev)
+    opt = m.configure_optimizers()["optimizer"]
+    batch = make_batch(B=B, T=T, lead=12, seed=1234, device=dev)
+    mask = torch.from_numpy(np.random.RandomState(7).rand(T) < 0.5).to(dev)
+    rng = np.random.RandomState(7)
+
+    def refresh():  # the host draw of lstm_with_sample.py:389 into the static device mask
+        mask.copy_(torch.from_numpy(rng.rand(T) < 0.5), non_blocking=True)
+
+    def step_c3():
+        opt.zero_grad()
+        m.training_step(batch, sampling_mask=mask)["loss"].backward()
+        opt.step()
+    replay = capture(step_c3, 2, preserve=opt.state_tensors())
+    ms = _timed_replay(replay, K, W, pre=refresh)
+    kern = _probe_steps(step_c3)
+    cpu = None
+    if cpu_on:
+        info = _cpu_setup(args)
+        cb = 16
+        cbatch = make_batch(B=cb, T=T, lead=12, seed=1234)
+        cmask = torch.from_numpy(np.random.RandomState(7).rand(T) < 0.5)
+        t = _time_cpu(lambda: O.run_train_step(O.lstm_with_sample_training_loss, sd, oc, mc, cbatch,
+                                               sampling_mask=cmask), 1, 2)
+        cpu = dict(value=round(cb * T / t, 2), unit="frames/s", kind="port", **info,
+                   sample=f"oracle lstm_with_sampling scheduled-sampling train step (300 AR frames, mask "
+                          f"RandomState(7)<0.5, lead 12) on a bounded sample B={cb} T={T}, median of 2 after 1 warm-up")
+    out["C3_lstm_with_sampling_scheduled_sampling"] = _secondary_entry(
+        "lstm_with_sampling scheduled-sampling train step B=64 T=300 lead 12 (BASELINE configs[2]), HIP graph, "
+        "mask refreshed from the host RNG before every replay", ms, B * T, C3_MFLOP_PER_FRAME * 1e6, "fp32",
+        kern, cpu)
+    del m, opt, replay
+
+    progress("lstmformer generation")
+    # lstmformer autoregressive generation (Metaformer.prediction, full generation; SURVEY §8f rank 1)
+    mc, oc, me = C.lstmformer_config(ratio=1)
+    torch.manual_seed(0)
+    m = Metaformer(mc, oc, me)
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.to(dev).eval()
+    batch = make_batch(B=B, T=T, lead=12, seed=1234, device=dev)
+    gmask = torch.ones(T, dtype=torch.bool, device=dev)
+
+    def gen():
+        with torch.no_grad():
+            m._generate(batch, sampling_mask=gmask)
+    replay = capture(gen, 2)
+    ms = _timed_replay(replay, 5, 2)
+    kern = _probe_steps(gen)
+    cpu = None
+    if cpu_on:
+        info = _cpu_setup(args)
+        ct = 40
+        cbatch = make_batch(B=B, T=ct, lead=12, seed=1234)
+        with torch.no_grad():
+            t = _time_cpu(lambda: O.metaformer_prediction(sd, mc, cbatch, torch.ones(ct, dtype=torch.bool)), 0, 1)
+        cpu = dict(value=round(B * ct / t, 2), unit="frames/s", kind="port", **info,
+                   sample=f"oracle Metaformer.prediction (full generation, no grad) on a bounded sample of "
+                          f"{ct} frames x B={B} (per-frame cost is independent of T), 1 run")
+    out["lstmformer_generation"] = _secondary_entry(
+        "lstmformer autoregressive generation (Metaformer.prediction, full_generation, eval, no grad) "
+        "B=64 x 300 frames, HIP graph; one step = one 64-clip batch", ms, B * T, gen_flops_per_frame(mc, 1), "fp32",
+        kern, cpu)
+    Fn.check_errors()
+    return out
 
 
 def main():
@@ -159,7 +464,7 @@ def main():
     if args.graph:
         # capture fwd+bwd(+AdamW at N=1) once; the RCCL all-reduce stays eager between replays at N>1
         captured = step if world == 1 else fwd_bwd
-        replay = capture(captured, max(2, args.warmup))
+        replay = capture(captured, max(2, args.warmup), preserve=opt.state_tensors())
         if world == 1:
             run = replay
         else:
@@ -206,28 +511,7 @@ def main():
         step()
     per = Fn.probe_stop(with_work=True) if rank == 0 else {}
     Fn.set_wgrad_stream(side)
-    kernels, roof = {}, None
-    if rank == 0:
-        for f in fams:
-            v = per.get(f, [])
-            if not v:
-                continue
-            fms = sum(t for t, _ in v) / 2.0
-            work = sum(w for _, w in v) / 2.0
-            n = len(v) / 2.0
-            tf = work / (fms / 1e3) / 1e12
-            kernels[f] = {"kernel": FAMILIES[f], "ms_per_step": round(fms, 3), "launches_per_step": n,
-                          "avg_launch_ms": round(fms / n, 4), "algorithmic_flop_per_launch": work / n,
-                          "achieved_tflops": round(tf, 2), "frac_of_fp32_peak": round(tf / FP32_MFMA_PEAK_TF, 4)}
-        if kernels:
-            dom = max(kernels, key=lambda f: kernels[f]["ms_per_step"])
-            k = kernels[dom]
-            roof = {"kernel": k["kernel"], "family": dom, "bound": "mfma", "achieved": k["achieved_tflops"],
-                    "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s", "frac": k["frac_of_fp32_peak"],
-                    "traffic": pmc_traffic(dom), "avg_launch_ms": k["avg_launch_ms"],
-                    "launches_per_step": k["launches_per_step"],
-                    "algorithmic_flop_per_launch": k["algorithmic_flop_per_launch"],
-                    "peak_note": PEAK_NOTES.get(dom, "")}
+    kernels, roof = families(per, 2) if rank == 0 else ({}, None)
     step_flop = (model_flops_per_frame(mc, args.ratio) + attn_flops_per_frame(mc, args.ratio, args.seq)) \
         * args.batch * args.seq
     out = {
@@ -247,7 +531,13 @@ def main():
         "kernels": kernels,
         "cpu_baseline": None,
     }
+    if rank == 0:
+        progress(f"headline {ms:.3f} ms/step")
+    if rank == 0 and world == 1 and args.secondary:
+
+        out["secondary"] = secondary(args, dev)
     if rank == 0 and world == 1 and args.cpu_baseline:
+        progress("headline CPU baseline")
         out["cpu_baseline"] = cpu_baseline(args, mc, oc)
         out["speedup_vs_cpu_baseline"] = round(out["value"] / out["cpu_baseline"]["value"], 1)
     if rank == 0:

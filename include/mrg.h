@@ -79,6 +79,17 @@ int mrg_gemm_f32_ex(int M, int N, int K, float alpha,
                     float* asum_out, float* asum_out2, float asum_beta,
                     unsigned* counters, hipStream_t stream);
 
+/* Mixed precision (bf16 configs, BASELINE configs[1]): the same GEMM with every operand rounded to
+ * bf16 (RNE) as it is staged and ONE v_mfma_f32_32x32x16_bf16 per block, fp32 accumulation,
+ * fp32 output and epilogue.  Arguments as mrg_gemm_f32_ex.                                  */
+int mrg_gemm_bf16_ex(int M, int N, int K, float alpha,
+                     const float* A, int transA, long lda, long lda_hi, int a_rdiv,
+                     const float* B, int transB, long ldb, long ldb_hi, int b_rdiv,
+                     float beta, float* C, long ldc, const float* bias, int epilogue,
+                     const float* aux, long ldaux, float* workspace, int splits,
+                     float* asum_out, float* asum_out2, float asum_beta,
+                     unsigned* counters, hipStream_t stream);
+
 /* out[n] = beta*out[n] + sum_rows X(row, n); out2 (nullable) receives the same
  * sum (b_ih and b_hh share one gradient).  Bias gradients of every Linear.  */
 size_t mrg_colsum_workspace_bytes(int rows, int N);

@@ -44,6 +44,11 @@ SIGNATURES = {
                                 P, c_int, c_long, c_long, c_int,
                                 c_float, P, c_long, P, c_int, P, c_long, P, c_int,
                                 P, P, c_float, P, P]),
+    "mrg_gemm_bf16_ex": (c_int, [c_int, c_int, c_int, c_float,
+                                 P, c_int, c_long, c_long, c_int,
+                                 P, c_int, c_long, c_long, c_int,
+                                 c_float, P, c_long, P, c_int, P, c_long, P, c_int,
+                                 P, P, c_float, P, P]),
     "mrg_colsum_workspace_bytes": (c_size, [c_int, c_int]),
     "mrg_colsum_f32": (c_int, [c_int, c_int, P, c_long, c_long, c_int, c_float, P, P, P, P]),
     "mrg_lstm_supported_hidden": (c_int, [c_int]),

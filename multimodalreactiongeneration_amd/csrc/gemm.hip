@@ -789,20 +789,27 @@ __global__ __launch_bounds__(1024) void colsum_final_kernel(const float* part, i
   }
 }
 
-// blocks per CU the hardware admits for a kernel (cached per kernel), x CUs of the current device
+// blocks per CU the hardware admits for a kernel (cached per kernel FUNCTION: every instantiation
+// has the same C++ type, so the cache is keyed by its address), x CUs of the current device
 template <typename K>
 static int resident_blocks(K kernel) {
-  static int per_cu = -1;
+  static const void* keys[256];
+  static int vals[256];
+  static int nkeys = 0;
   static int cus[16] = {0};
+  const void* key = reinterpret_cast<const void*>(kernel);
+  int per_cu = -1;
+  for (int i = 0; i < nkeys; ++i)
+    if (keys[i] == key) { per_cu = vals[i]; break; }
+  if (per_cu < 0) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, key, NT, 0) != hipSuccess || n < 1) n = 1;
+    per_cu = n;
+    if (nkeys < 256) { keys[nkeys] = key; vals[nkeys] = n; ++nkeys; }
+  }
   int dev = 0;
   (void)hipGetDevice(&dev);
   if (dev < 0 || dev >= 16) dev = 0;
-  if (per_cu < 0) {
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(kernel), NT, 0) != hipSuccess || n < 1)
-      n = 1;
-    per_cu = n;
-  }
   if (cus[dev] == 0) {
     int n = 0;
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1) n = 256;
@@ -833,7 +840,7 @@ static void launch_tile(GemmArgs a, int ta, int tb, bool va, bool vb, int splits
   }
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int VAR = 0>
 static void launch_tile_x6(GemmArgs a, int ta, int tb, bool va, bool vb, int splits, hipStream_t s) {
   a.tiles_n = (a.N + BN - 1) / BN;
   a.tiles_mn = a.tiles_n * ((a.M + BM - 1) / BM);
@@ -843,7 +850,7 @@ static void launch_tile_x6(GemmArgs a, int ta, int tb, bool va, bool vb, int spl
   switch (code) {
 #define MRG_G(TA, TB, VA, VB)                                                                    \
     case (TA << 3) | (TB << 2) | (VA << 1) | VB: {                                               \
-      auto k = gemm_x6_kernel<BM, BN, TA, TB, (bool)VA, (bool)VB>;                                \
+      auto k = gemm_x6_kernel<BM, BN, TA, TB, (bool)VA, (bool)VB, VAR>;                           \
       const int grid = a.ntiles < resident_blocks(k) ? a.ntiles : resident_blocks(k);           \
       k<<<grid, NT, 0, s>>>(a);                                                                  \
     } break;
@@ -961,12 +968,24 @@ static int g_gemm_mode = [] {
   return (e && atoi(e) != 0) ? 0 : 1;
 }();
 
-static int launch_gemm(const GemmArgs& a, int tile, int bk, int ta, int tb, bool va, bool vb, int splits,
-                       hipStream_t s) {
+static int launch_gemm(int mode, const GemmArgs& a, int tile, int bk, int ta, int tb, bool va, bool vb,
+                       int splits, hipStream_t s) {
   ta = ta ? 1 : 0;
   tb = tb ? 1 : 0;
   (void)bk;  // BK = 64 measured no faster on these shapes (short K): only BK = 32 is instantiated
-  if (g_gemm_mode == 1) {
+  // bf16 operands (one plane, one MFMA per block), fp32 accumulate.  Measured (r02,
+  // tools/tools_gemm_bench.py 2): faster than the x6 split only when both operands are k-contiguous
+  // (NT: the forward products, 1.5-1.7x); with a transposed operand this staging structure runs
+  // the one-plane form slower than the split (dX 35.7 -> 51.5 us, dW 36.9 -> 67.8 us), so those
+  // products keep the split, which is at least as accurate as bf16 operands.
+  if (mode == 2 && !(ta == 0 && tb == 1)) mode = 1;
+  if (mode == 2) {
+    if (tile == 0) launch_tile_x6<128, 128, 3>(a, ta, tb, va, vb, splits, s);
+    else if (tile == 1) launch_tile_x6<128, 64, 3>(a, ta, tb, va, vb, splits, s);
+    else launch_tile_x6<64, 64, 3>(a, ta, tb, va, vb, splits, s);
+    return 0;
+  }
+  if (mode == 1) {
     if (tile == 0) launch_tile_x6<128, 128>(a, ta, tb, va, vb, splits, s);
     else if (tile == 1) launch_tile_x6<128, 64>(a, ta, tb, va, vb, splits, s);
     else launch_tile_x6<64, 64>(a, ta, tb, va, vb, splits, s);
@@ -1037,13 +1056,14 @@ MRG_API int mrg_colsum_f32(int rows, int N, const float* X, long ld, long ld_hi,
                            float beta, float* out, float* out2, float* workspace,
                            hipStream_t stream);
 
-MRG_API int mrg_gemm_f32_ex(int M, int N, int K, float alpha,
-                            const float* A, int transA, long lda, long lda_hi, int a_rdiv,
-                            const float* B, int transB, long ldb, long ldb_hi, int b_rdiv,
-                            float beta, float* C, long ldc, const float* bias, int epilogue,
-                            const float* aux, long ldaux, float* workspace, int splits,
-                            float* asum_out, float* asum_out2, float asum_beta,
-                            unsigned* counters, hipStream_t stream) {
+static int gemm_ex(int mode, int M, int N, int K, float alpha,
+                   const float* A, int transA, long lda, long lda_hi, int a_rdiv,
+                   const float* B, int transB, long ldb, long ldb_hi, int b_rdiv,
+                   float beta, float* C, long ldc, const float* bias, int epilogue,
+                   const float* aux, long ldaux, float* workspace, int splits,
+                   float* asum_out, float* asum_out2, float asum_beta,
+                   unsigned* counters, hipStream_t stream) {
+  const bool mx = mode >= 1;  // bf16 matrix-core paths (x6 split or plain bf16 operands)
   MRG_REQUIRE(M >= 0 && N >= 0 && K >= 0, "mrg_gemm_f32: negative size");
   MRG_REQUIRE(epilogue >= 0 && epilogue <= 3, "mrg_gemm_f32: bad epilogue %d", epilogue);
   MRG_REQUIRE(epilogue < 2 || aux, "mrg_gemm_f32: epilogue %d needs aux", epilogue);
@@ -1066,7 +1086,7 @@ MRG_API int mrg_gemm_f32_ex(int M, int N, int K, float alpha,
   a.asum = nullptr; a.asum_out = asum_out; a.asum_out2 = asum_out2; a.asum_beta = asum_beta;
   a.cnt = nullptr; a.nsplit = splits;
   // fused bias-gradient row sums: x6 path with A = (memory rows k, contiguous along m)
-  const bool fuse_asum = asum_out && g_gemm_mode == 1 && transA && workspace;
+  const bool fuse_asum = asum_out && mx && transA && workspace;
   if (fuse_asum) a.asum = workspace + (splits > 1 ? (long)splits * M * N : 0);
   // vector (float4) global loads need 16-B aligned rows along the contiguous index
   auto aligned = [](const float* p, const RowMap& m) {
@@ -1077,14 +1097,14 @@ MRG_API int mrg_gemm_f32_ex(int M, int N, int K, float alpha,
            (!aux || (ldaux & 3) == 0) && (!a.ws || (N & 3) == 0)) ? 1 : 0;
   // few-row products (x6 mode): exact f32 MFMA from registers, no split, no LDS staging: M <= 64
   // rows of activations, or a weight gradient over <= 64 rows (K), its bias sums fused
-  if (g_gemm_mode == 1 && splits == 1 && ((!transA && M <= 64 && !asum_out) || (transA && K <= 64))) {
+  if (mx && splits == 1 && ((!transA && M <= 64 && !asum_out) || (transA && K <= 64))) {
     a.transA = transA ? 1 : 0;
     a.transB = transB ? 1 : 0;
     launch_rows(a, stream);
     return check_launch("gemm_rows_kernel");
   }
   int tile;  // 0: 128x128, 1: 128x64, 2: 64x64
-  if (g_gemm_mode == 1) {
+  if (mx) {
     // x6 (measured on the step's shapes, tools_gemm_sweep.py): 128x128 for split-K weight
     // gradients and wide/deep products; 64x64 for narrow ones (N <= 128, or N = 256 at K <= 512
     // with K-contiguous B); small problems take the tile that gives the most workgroups
@@ -1104,14 +1124,14 @@ MRG_API int mrg_gemm_f32_ex(int M, int N, int K, float alpha,
   if (g_tile_override >= 0 && g_tile_override <= 2) tile = g_tile_override;
   // small split outputs: the last K slice of each tile combines the slabs in-launch (no reduce
   // kernel) when the slabs it must read stay small (<= 64 KB per tile)
-  if (splits > 1 && counters && g_gemm_mode == 1 && !a.asum && tile == 2) {
+  if (splits > 1 && counters && mx && !a.asum && tile == 2) {
     const long tiles = (long)((M + 63) / 64) * ((N + 63) / 64);
     if (tiles <= MRG_GEMM_COUNTERS && (long)splits * 64 * 64 * 4 <= 65536) a.cnt = counters;
   }
-  if (launch_gemm(a, tile, bk, transA, transB, va, vb, splits, stream)) return 2;
+  if (launch_gemm(mode, a, tile, bk, transA, transB, va, vb, splits, stream)) return 2;
   if (check_launch("gemm_f32_kernel")) return 1;
   // unsplit 64x64-tile GEMM (x6): its n0 == 0 tiles wrote asum_out directly
-  bool asum_done = splits == 1 && tile == 2 && g_gemm_mode == 1;
+  bool asum_done = splits == 1 && tile == 2 && mx;
   if (splits > 1 && !a.cnt) {
     long total = (long)M * N;
     if (a.vec && (N & 3) == 0) {
@@ -1138,6 +1158,33 @@ MRG_API int mrg_gemm_f32_ex(int M, int N, int K, float alpha,
     }
   }
   return 0;
+}
+
+MRG_API int mrg_gemm_f32_ex(int M, int N, int K, float alpha,
+                            const float* A, int transA, long lda, long lda_hi, int a_rdiv,
+                            const float* B, int transB, long ldb, long ldb_hi, int b_rdiv,
+                            float beta, float* C, long ldc, const float* bias, int epilogue,
+                            const float* aux, long ldaux, float* workspace, int splits,
+                            float* asum_out, float* asum_out2, float asum_beta,
+                            unsigned* counters, hipStream_t stream) {
+  return gemm_ex(g_gemm_mode, M, N, K, alpha, A, transA, lda, lda_hi, a_rdiv, B, transB, ldb, ldb_hi, b_rdiv, beta,
+                 C, ldc, bias, epilogue, aux, ldaux, workspace, splits, asum_out, asum_out2, asum_beta, counters,
+                 stream);
+}
+
+// bf16-operand arithmetic (mixed precision): every operand rounded to bf16 (RNE) as it is staged,
+// one v_mfma_f32_32x32x16_bf16 per block, fp32 accumulation and fp32 output / epilogue.  Same
+// arguments as mrg_gemm_f32_ex.  Few-row products (M <= 64) stay on the exact-f32 register kernel.
+MRG_API int mrg_gemm_bf16_ex(int M, int N, int K, float alpha,
+                             const float* A, int transA, long lda, long lda_hi, int a_rdiv,
+                             const float* B, int transB, long ldb, long ldb_hi, int b_rdiv,
+                             float beta, float* C, long ldc, const float* bias, int epilogue,
+                             const float* aux, long ldaux, float* workspace, int splits,
+                             float* asum_out, float* asum_out2, float asum_beta,
+                             unsigned* counters, hipStream_t stream) {
+  return gemm_ex(2, M, N, K, alpha, A, transA, lda, lda_hi, a_rdiv, B, transB, ldb, ldb_hi, b_rdiv, beta,
+                 C, ldc, bias, epilogue, aux, ldaux, workspace, splits, asum_out, asum_out2, asum_beta, counters,
+                 stream);
 }
 
 MRG_API int mrg_gemm_f32(int M, int N, int K, float alpha,

@@ -7,6 +7,16 @@ exchange is a single in-place all-reduce (ReduceOp.AVG) of 52.2 MB for the
 benchmark model, issued on a dedicated communication stream so it can be
 overlapped with other work; the optimizer stream waits on it.  With the gloo
 backend (CPU tests) AVG is emulated by SUM then a scale.
+
+``overlap=True`` does what Lightning's DDP does during backward: the flat buffer
+is cut into buckets at parameter boundaries in reverse registration order (the
+order backward produces them), and each bucket's all-reduce is issued on the comm
+stream as soon as every gradient write into it has been issued (functional's
+gradient-ready listener), ordered after the main and weight-gradient streams.
+The number of writes per parameter is taken from a first, non-overlapped census
+backward (the graph is static, as DDP's ``static_graph``); every rank runs the
+same graph, so the buckets complete in the same order everywhere (RCCL needs one
+collective order on all ranks).  ``finish()`` makes the current stream wait.
 """
 from __future__ import annotations
 
@@ -40,21 +50,137 @@ def broadcast_parameters(module: torch.nn.Module, src: int = 0):
 class GradReducer:
     """Average a flat gradient buffer across ranks, in buckets, on a side stream."""
 
-    def __init__(self, flat_grad: torch.Tensor, bucket_elems: int = 0):
+    def __init__(self, flat_grad: torch.Tensor, bucket_elems: int = 0, params=None, overlap: bool = False,
+                 bucket_bytes: int = 8 << 20):
         self.flat_grad = flat_grad
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.backend = dist.get_backend() if dist.is_initialized() else None
         n = flat_grad.numel()
-        if bucket_elems <= 0:
-            bucket_elems = n
-        self.buckets = [(s, min(n, s + bucket_elems)) for s in range(0, n, bucket_elems)]
+        self.overlap = bool(overlap) and params is not None and self.world > 1
         self.stream = torch.cuda.Stream(device=flat_grad.device) if flat_grad.is_cuda else None
+        if self.overlap:
+            self._init_buckets(list(params), bucket_bytes // flat_grad.element_size())
+        else:
+            if bucket_elems <= 0:
+                bucket_elems = n
+            self.buckets = [(s, min(n, s + bucket_elems)) for s in range(0, n, bucket_elems)]
 
+    # ------------------------------------------------------------ overlapped (bucketed) mode
+    def _init_buckets(self, params, cap):
+        base = self.flat_grad.data_ptr()
+        es = self.flat_grad.element_size()
+        spans = sorted(((p.grad.data_ptr() - base) // es, p.numel(), p) for p in params)
+        self.buckets, self.bucket_of = [], {}
+        cur, start, end = [], None, None
+        for off, k, p in reversed(spans):          # reverse registration order = backward order
+            if cur and (end - off) > cap:
+                self.buckets.append((start, end))
+                cur = []
+            if not cur:
+                end = off + k
+            cur.append(p)
+            start = off
+            self.bucket_of[id(p)] = len(self.buckets)
+        if cur:
+            self.buckets.append((start, end))
+        self.expected = None                        # per-parameter writes per backward (census)
+        self.counts = {}
+        self.launched = [False] * len(self.buckets)
+        self.remaining = None
+        self.order = []                             # bucket launch order of the last backward
+        self.order_in_backward = []                 # those launched before the end-of-backward callback
+        self._task = None
+        from . import functional as Fn
+        Fn.set_grad_listener(self)
+
+    def touch(self):
+        task = torch._C._current_graph_task_id()
+        if task != self._task:                       # first gradient write of a new backward pass
+            self._task = task
+            self.counts = {}
+            self.launched = [False] * len(self.buckets)
+            self.order = []
+            self.order_in_backward = []
+            if self.expected is not None:
+                self.remaining = [0] * len(self.buckets)
+                for pid, c in self.expected.items():
+                    self.remaining[self.bucket_of[pid]] += c
+            if task >= 0:
+                torch.autograd.Variable._execution_engine.queue_callback(self.end_of_backward)
+
+    def ready(self, params):
+        for p in params:
+            pid = id(p)
+            self.counts[pid] = self.counts.get(pid, 0) + 1
+            if self.expected is None:
+                continue
+            b = self.bucket_of[pid]
+            if self.launched[b]:
+                raise RuntimeError("GradReducer(overlap=True): a parameter received more gradient writes than "
+                                   "in the census backward (dynamic graph); use overlap=False")
+            self.remaining[b] -= 1
+            if self.remaining[b] == 0:
+                self._launch(b)
+
+    def end_of_backward(self):
+        from . import functional as Fn
+        self.order_in_backward = list(self.order)
+        Fn._flush_touched()
+        if self.expected is None:                    # census pass: remember the structure
+            self.expected = dict(self.counts)
+        for b in range(len(self.buckets)):
+            if not self.launched[b]:
+                self._launch(b)
+        self._task = None
+
+    def _launch(self, b):
+        from . import functional as Fn
+        s, e = self.buckets[b]
+        self.launched[b] = True
+        self.order.append(b)
+        op, scale = self._op()
+        dev = self.flat_grad.device
+        if self.stream is not None:
+            cur = torch.cuda.current_stream(dev)
+            self.stream.wait_stream(cur)
+            side = Fn._SIDE.get(dev.index or 0)
+            if side is not None:
+                self.stream.wait_stream(side)
+            with torch.cuda.stream(self.stream):
+                dist.all_reduce(self.flat_grad[s:e], op=op)
+                if scale != 1.0:
+                    self.flat_grad[s:e].mul_(scale)
+        else:
+            dist.all_reduce(self.flat_grad[s:e], op=op)
+            if scale != 1.0:
+                self.flat_grad[s:e].mul_(scale)
+
+    def _op(self):
+        if self.backend == "nccl":
+            return dist.ReduceOp.AVG, 1.0
+        return dist.ReduceOp.SUM, 1.0 / self.world
+
+    def finish(self):
+        """Order the caller's stream after every bucket's all-reduce (call after backward)."""
+        if self.world <= 1:
+            return
+        if not self.overlap:
+            return self.allreduce()
+        if self.stream is not None:
+            torch.cuda.current_stream(self.flat_grad.device).wait_stream(self.stream)
+
+    def close(self):
+        if self.overlap:
+            from . import functional as Fn
+            Fn.set_grad_listener(None)
+
+    # ------------------------------------------------------------ after-backward mode
     def allreduce(self):
         if self.world <= 1:
             return
-        use_avg = self.backend == "nccl"
-        op = dist.ReduceOp.AVG if use_avg else dist.ReduceOp.SUM
+        if self.overlap:
+            return self.finish()
+        op, scale = self._op()
         if self.stream is not None:
             cur = torch.cuda.current_stream(self.flat_grad.device)
             self.stream.wait_stream(cur)
@@ -65,5 +191,5 @@ class GradReducer:
         else:
             for s, e in self.buckets:
                 dist.all_reduce(self.flat_grad[s:e], op=op)
-        if not use_avg:
-            self.flat_grad.mul_(1.0 / self.world)
+        if scale != 1.0:
+            self.flat_grad.mul_(scale)

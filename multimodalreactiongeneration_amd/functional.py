@@ -17,7 +17,9 @@ Reference ops replaced (file:line in /root/reference):
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
+import functools
 import math
 import os
 from typing import List, Optional, Sequence
@@ -120,13 +122,79 @@ def check_errors(device=None):
             raise RuntimeError("libmrg: LSTM recurrence hand-off timed out (grid not co-resident?)")
 
 
+# Gradient-ready listener (ddp.GradReducer with overlap): every parameter-gradient write goes
+# through _gbuf() just before its launch, so a touched parameter is announced to the listener when
+# the NEXT autograd Function's backward starts (every launch of the previous one is issued by then)
+# or at the end of the backward pass.
+_GRAD_LISTENER = [None]
+_TOUCHED = []
+
+
+def set_grad_listener(listener):
+    """listener.ready(params) is called with parameters whose gradient writes have been issued
+    (at most one autograd Function late); listener.end_of_backward() once per backward pass."""
+    _GRAD_LISTENER[0] = listener
+    _TOUCHED.clear()
+
+
+def _flush_touched():
+    lst = _GRAD_LISTENER[0]
+    if lst is not None and _TOUCHED:
+        ready = list(_TOUCHED)
+        _TOUCHED.clear()
+        lst.ready(ready)
+
+
 def _gbuf(p: torch.Tensor) -> Optional[torch.Tensor]:
     """The tensor a parameter's gradient accumulates into (created zero-filled on first use)."""
     if p is None or not p.requires_grad:
         return None
     if p.grad is None:
         p.grad = torch.zeros_like(p)
+    if _GRAD_LISTENER[0] is not None:
+        _GRAD_LISTENER[0].touch()
+        _TOUCHED.append(p)
     return p.grad
+
+
+# --- compute precision (mixed-precision configs, BASELINE configs[1] "bf16"): None = fp32 arithmetic
+# (the library's GEMM mode: x6 split or exact f32), "bf16" = GEMM operands rounded to bf16 with fp32
+# accumulation (mrg_gemm_bf16_ex).  Set by the model's forward; every autograd Function records it in
+# forward and restores it around its backward (which runs on autograd's thread, after the context).
+_ARITH = [None]
+PRECISIONS = {None: None, "32": None, 32: None, "fp32": None, "32-true": None,
+              "bf16": "bf16", "bf16-mixed": "bf16", "bf16-true": "bf16"}
+
+
+@contextlib.contextmanager
+def precision(p):
+    """Compute precision of the enclosed ops: '32'/'fp32' or 'bf16'/'bf16-mixed' (Lightning names)."""
+    if p not in PRECISIONS:
+        raise ValueError(f"unsupported precision {p!r} (one of {sorted(map(str, PRECISIONS))})")
+    prev = _ARITH[0]
+    _ARITH[0] = PRECISIONS[p]
+    try:
+        yield
+    finally:
+        _ARITH[0] = prev
+
+
+def _keeps_precision(fn):
+    """Decorator for autograd Function forward/backward: forward records the active precision in ctx,
+    backward runs under it."""
+    @functools.wraps(fn)
+    def wrapper(ctx, *args):
+        if fn.__name__ == "forward":
+            ctx.arith = _ARITH[0]
+            return fn(ctx, *args)
+        _flush_touched()  # the previous Function's gradient writes are all issued
+        prev = _ARITH[0]
+        _ARITH[0] = getattr(ctx, "arith", None)
+        try:
+            return fn(ctx, *args)
+        finally:
+            _ARITH[0] = prev
+    return wrapper
 
 
 def gemm(M, N, K, A, transA, lda, B, transB, ldb, C, ldc, *, alpha=1.0, beta=0.0, bias=None,
@@ -144,8 +212,9 @@ def gemm(M, N, K, A, transA, lda, B, transB, ldb, C, ldc, *, alpha=1.0, beta=0.0
     ws = None
     if splits > 1 or asum_out is not None:
         ws = _ws(lib.mrg_gemm_workspace_bytes(M, N, splits), device)
+    fn = lib.mrg_gemm_bf16_ex if _ARITH[0] == "bf16" else lib.mrg_gemm_f32_ex
     with _probe("gemm", 2.0 * M * N * K):
-        rc = lib.mrg_gemm_f32_ex(M, N, K, alpha, A, transA, lda, a_hi, a_div, B, transB, ldb, b_hi, b_div,
+        rc = fn(M, N, K, alpha, A, transA, lda, a_hi, a_div, B, transB, ldb, b_hi, b_div,
                                  beta, C, ldc, bias, epi, aux, ldaux, _ptr(ws), splits, asum_out, asum_out2,
                                  asum_beta, _ptr(_counters(device)) if splits > 1 else None, _stream())
     _lib.check(rc, "gemm")
@@ -155,7 +224,7 @@ def act_splits(M, N, K):
     """split-K factor for activation products with few output tiles (65..~2000 rows): a handful of
     64x64 tiles walking K >= 512 is latency-bound, so spread K over the CUs."""
     tiles = ((M + 63) // 64) * ((N + 63) // 64)
-    if M <= 64 or tiles >= 64 or K < 512 or _lib.load().mrg_gemm_get_mode() != 1:
+    if M <= 64 or tiles >= 64 or K < 512 or (_lib.load().mrg_gemm_get_mode() != 1 and _ARITH[0] is None):
         return 1  # M <= 64: the few-row kernel (gemm_rows_kernel) needs no split
     # <= 4 slices of 64x64 tiles: the slabs (<= 64 KB per tile) are combined in-launch
     return int(max(1, min(4, K // 64, 128 // tiles)))
@@ -167,7 +236,7 @@ def wgrad_splits(M, N, K):
     About 512 workgroups: 128x128 tiles under the x6 arithmetic (chunks of >= 128 rows),
     64x64 tiles under exact f32 (chunks of >= 256 rows); tools/tools_gemm_sweep.py measured both.
     """
-    if _lib.load().mrg_gemm_get_mode() == 1:
+    if _lib.load().mrg_gemm_get_mode() == 1 or _ARITH[0] == "bf16":
         tiles = ((M + 127) // 128) * ((N + 127) // 128)
         s = max(1, 512 // max(1, tiles))
         return int(max(1, min(s, K // 128, 128)))
@@ -278,6 +347,7 @@ def _wgrad(dY, ldy, X, ldx, rows, Nout, Nin, gw, device, *, dy_hi=0, dy_div=0, x
 # ------------------------------------------------------------------ Linear
 class _LinearFn(Function):
     @staticmethod
+    @_keeps_precision
     def forward(ctx, x, w, b):
         _lib.require_device(x)
         In, N = w.shape[1], w.shape[0]
@@ -290,6 +360,7 @@ class _LinearFn(Function):
         return y.view(*x.shape[:-1], N)
 
     @staticmethod
+    @_keeps_precision
     def backward(ctx, dy):
         x2, w, b = ctx.saved_tensors
         N, In = w.shape
@@ -312,6 +383,7 @@ def linear(x, weight, bias=None):
 # ------------------------------------------------------------------ FFN (Linear -> ReLU -> Linear)
 class _FFNFn(Function):
     @staticmethod
+    @_keeps_precision
     def forward(ctx, x, w1, b1, w2, b2):
         _lib.require_device(x)
         In, Hb, N = w1.shape[1], w1.shape[0], w2.shape[0]
@@ -327,6 +399,7 @@ class _FFNFn(Function):
         return z.view(*x.shape[:-1], N)
 
     @staticmethod
+    @_keeps_precision
     def backward(ctx, dz):
         x2, h, w1, b1, w2, b2 = ctx.saved_tensors
         Hb, In = w1.shape
@@ -355,6 +428,7 @@ def ffn(x, w1, b1, w2, b2):
 # ------------------------------------------------------------------ residual + LayerNorm
 class _ResLNFn(Function):
     @staticmethod
+    @_keeps_precision
     def forward(ctx, a, b, gamma, beta, eps):
         _lib.require_device(a)
         E = a.shape[-1]
@@ -373,6 +447,7 @@ class _ResLNFn(Function):
         return y.view(a.shape)
 
     @staticmethod
+    @_keeps_precision
     def backward(ctx, dy):
         a2, b2, gamma, beta, mean, rstd = ctx.saved_tensors
         dy2 = dy.reshape(-1, a2.shape[1]).contiguous()
@@ -427,6 +502,7 @@ class _LinResLNFn(Function):
     """LN(x W^T + b + x): FeedForward(nonlinearity none, residual, LN) (mixer_block.py:63-83)."""
 
     @staticmethod
+    @_keeps_precision
     def forward(ctx, x, w, b, gamma, beta, eps):
         _lib.require_device(x)
         E = w.shape[0]
@@ -440,6 +516,7 @@ class _LinResLNFn(Function):
         return y.view(x.shape)
 
     @staticmethod
+    @_keeps_precision
     def backward(ctx, dy):
         x2, w, b, z, gamma, beta, mean, rstd = ctx.saved_tensors
         M, E = x2.shape
@@ -462,6 +539,7 @@ class _FFNResLNFn(Function):
     """LN(W2 relu(W1 x + b1) + b2 + x): the metaformer block FeedForward (multi_modal_metaformer.py:328)."""
 
     @staticmethod
+    @_keeps_precision
     def forward(ctx, x, w1, b1, w2, b2, gamma, beta, eps):
         _lib.require_device(x)
         Hb, E = w1.shape
@@ -478,6 +556,7 @@ class _FFNResLNFn(Function):
         return y.view(x.shape)
 
     @staticmethod
+    @_keeps_precision
     def backward(ctx, dy):
         x2, h, z, w1, b1, w2, b2, gamma, beta, mean, rstd = ctx.saved_tensors
         Hb, E = w1.shape
@@ -511,6 +590,7 @@ class _LSTMFn(Function):
     """
 
     @staticmethod
+    @_keeps_precision
     def forward(ctx, spec, *tensors):
         nprob, concat, reverse, force_bs, eps = spec
         resln = eps is not None  # per problem LN(y + x) (ResidualConnection around LSTMMixer)
@@ -594,6 +674,7 @@ class _LSTMFn(Function):
         return tuple(outs)
 
     @staticmethod
+    @_keeps_precision
     def backward(ctx, *grads):
         nprob, concat, reverse, force_bs, B, T, H, resln = ctx.spec
         saved = ctx.saved_tensors
@@ -712,6 +793,7 @@ class _LSTMCellFn(Function):
     these per training step; a persistent recurrence launch per frame would be pure overhead."""
 
     @staticmethod
+    @_keeps_precision
     def forward(ctx, x, w_ih, w_hh, b_ih, b_hh, h0, c0):
         _lib.require_device(x)
         dev = x.device
@@ -736,6 +818,7 @@ class _LSTMCellFn(Function):
         return y, hT, c
 
     @staticmethod
+    @_keeps_precision
     def backward(ctx, dy, dhT, dcT):
         x2, w_ih, w_hh, b_ih, b_hh, h0c, c0c, gates, c = ctx.saved_tensors
         B, In = x2.shape
@@ -830,6 +913,7 @@ class _GRUFn(Function):
     the weight / bias / input gradients as GEMMs over all steps.  Returns (y [B, T, H], hT [B, H])."""
 
     @staticmethod
+    @_keeps_precision
     def forward(ctx, reverse, x, w_ih, w_hh, b_ih, b_hh, h0):
         _lib.require_device(x)
         dev = x.device
@@ -865,6 +949,7 @@ class _GRUFn(Function):
         return y, hT
 
     @staticmethod
+    @_keeps_precision
     def backward(ctx, dy, dhT):
         x, w_ih, w_hh, b_ih, b_hh, h0c, y, gates, ghn = ctx.saved_tensors
         reverse = ctx.reverse
@@ -933,6 +1018,7 @@ def visible_pairs(Tq, Tk, causal):
 
 class _MHAFn(Function):
     @staticmethod
+    @_keeps_precision
     def forward(ctx, spec, q_in, kv_in, in_w, in_b, out_w, out_b, qpad, kpad, gamma=None, beta=None):
         heads, causal, eps = spec  # eps not None: return LN(attn + q) (ResidualConnection(MHAMixer))
         _lib.require_device(q_in)
@@ -970,6 +1056,7 @@ class _MHAFn(Function):
         return res
 
     @staticmethod
+    @_keeps_precision
     def backward(ctx, dout):
         saved = ctx.saved_tensors
         q2, kv2, Q, KV, O, lse, in_w, in_b, out_w, out_b, qpad, kpad = saved[:12]

@@ -12,9 +12,16 @@ signatures and return conventions.  pytorch_lightning is not a dependency:
 ``LightningSurface`` provides ``log`` / ``log_dict`` / ``current_epoch`` /
 ``device`` so a Lightning ``Trainer`` or a plain loop can drive the models.
 torchmetrics logging is out of scope (no effect on loss or grads).
+
+Precision switch: ``model.precision`` ("32" default; "bf16" / "bf16-mixed" as Lightning's
+Trainer(precision=...) names it, or the config key ``precision``) selects the arithmetic of every
+op the model runs: bf16 = GEMM operands rounded to bf16 on the bf16 matrix cores with fp32
+accumulation; LayerNorm, softmax, the recurrent cell state c, the loss and the optimizer stay fp32,
+and parameters / gradients stay fp32 masters (BASELINE configs[1], SURVEY §8c bf16 gate).
 """
 from __future__ import annotations
 
+import functools
 import math
 from collections import OrderedDict
 from typing import Any, Dict, List, Tuple
@@ -33,10 +40,27 @@ from .mixers import mixer_layerd_argments_select, feedforward_block_argments
 PADDING_VALUE = -100
 
 
+def _in_precision(fn):
+    """Run a model entry point under the model's compute precision (functional.precision)."""
+    @functools.wraps(fn)
+    def wrapper(self, *args, **kwargs):
+        with Fn.precision(self.precision):
+            return fn(self, *args, **kwargs)
+    return wrapper
+
+
 class LightningSurface(nn.Module):
     """The slice of pl.LightningModule the reference models use."""
 
     current_epoch = 0
+    precision = "32"
+
+    def set_precision(self, precision):
+        """'32' (fp32 arithmetic) or 'bf16' / 'bf16-mixed' (bf16 GEMM operands, fp32 accumulation)."""
+        if precision not in Fn.PRECISIONS:
+            raise ValueError(f"unsupported precision {precision!r}")
+        self.precision = precision
+        return self
 
     def log(self, name, value, **kw):
         pass
@@ -118,6 +142,7 @@ class Metaformer(LightningSurface):
         super().__init__()
         model, optim, metrics = as_attr(model), as_attr(optim), as_attr(metrics)
         self.model, self.optim, self.metrics = model, optim, metrics
+        self.set_precision(model.get("precision", "32"))
         self.max_epochs = model.max_epochs
         self.use_scheduled_sampling = model.use_scheduled_sampling
         _loss_type_of(model)
@@ -192,6 +217,7 @@ class Metaformer(LightningSurface):
         self.delta_order = metrics.delta_order
         self.target_dict = gen_target_dict(metrics)
 
+    @_in_precision
     def forward(self, acoustic_partner, motion_partner, motion_self, leading_acoustic_partner,
                 leading_motion_partner, leading_motion_self, hxs=None):
         dev = self.device
@@ -218,6 +244,7 @@ class Metaformer(LightningSurface):
         return Fn.masked_loss(y, target.to(y.device), lead, self.model.loss_type, self.huber_delta,
                               self.smoothl1_beta, True, self.delta_order, self.delta_loss_scale)
 
+    @_in_precision
     def training_step(self, batch: List, *args, sampling_mask=None):
         if self.use_scheduled_sampling:
             self.log("scheduled_sampling_rate", self.current_epoch / self.max_epochs, logger=True)
@@ -236,6 +263,7 @@ class Metaformer(LightningSurface):
         self.log("train_loss", loss, prog_bar=True, logger=True)
         return {"loss": loss}
 
+    @_in_precision
     def validation_step(self, batch: List, *args):
         lead = batch[4][0].shape[1]
         y, _ = self.forward(*batch[:-1])
@@ -245,6 +273,7 @@ class Metaformer(LightningSurface):
         gen_loss = self.generation_step(batch)["loss"]
         return {"loss": loss, "gen_loss": gen_loss}
 
+    @_in_precision
     def generation_step(self, batch: List, sampling_mask=None):
         """genrt_loss (lstmformer.py:410-424): teacher-forced generation, loss over the broadcast
         [T, B, T, F] target of prediction (Q9), no scaler."""
@@ -255,6 +284,7 @@ class Metaformer(LightningSurface):
         return {"loss": loss}
 
     # ---------------- autoregressive generation (lstmformer.py:426-559)
+    @_in_precision
     def prediction(self, batch: List, use_scheduled_sampling: bool = False, full_generation: bool = False,
                    sampling_mask=None):
         """Stateless step-by-step generation (the reference never carries state, Q1).
@@ -314,6 +344,7 @@ class LSTMwithSample(LightningSurface):
         super().__init__()
         model, optim, metrics = as_attr(model), as_attr(optim), as_attr(metrics)
         self.model, self.optim, self.metrics = model, optim, metrics
+        self.set_precision(model.get("precision", "32"))
         self.max_epochs = model.max_epochs
         self.use_scheduled_sampling = model.use_scheduled_sampling
         _loss_type_of(model)
@@ -345,6 +376,7 @@ class LSTMwithSample(LightningSurface):
         self.delta_order = metrics.delta_order
         self.target_dict = gen_target_dict(metrics)
 
+    @_in_precision
     def forward(self, acoustic_partner, motion_partner, motion_self, leading_acoustic_partner,
                 leading_motion_partner, leading_motion_self, cell_state=None):
         dev = self.device
@@ -370,6 +402,7 @@ class LSTMwithSample(LightningSurface):
     def configure_optimizers(self):
         return self._optimizers(self.optim)
 
+    @_in_precision
     def training_step(self, batch: List, *args, sampling_mask=None):
         if self.use_scheduled_sampling:
             self.log("scheduled_sampling_rate", self.current_epoch / self.max_epochs, logger=True)
@@ -383,6 +416,7 @@ class LSTMwithSample(LightningSurface):
         self.log("train_loss", loss, prog_bar=True, logger=True)
         return {"loss": loss}
 
+    @_in_precision
     def validation_step(self, batch: List, *args):
         y, (lead, _, _), _ = self.forward(*batch[:-1])
         loss = Fn.masked_loss(y, batch[-1][0].to(y.device), lead, self.model.loss_type, self.huber_delta,
@@ -392,6 +426,7 @@ class LSTMwithSample(LightningSurface):
         gen_loss = Fn.masked_loss(pred, target, 0, self.model.loss_type, self.huber_delta, self.smoothl1_beta, True)
         return {"loss": loss, "gen_loss": gen_loss}
 
+    @_in_precision
     def prediction(self, batch: List, use_scheduled_sampling: bool = False, full_generation: bool = False,
                    sampling_mask=None):
         """Autoregressive decode (lstm_with_sample.py:339-433).
@@ -501,6 +536,7 @@ class SimpleLSTM(LightningSurface):
         super().__init__()
         cfg, optim, metrics = as_attr(cfg), as_attr(optim), as_attr(metrics)
         self.cfg, self.optim, self.metrics = cfg, optim, metrics
+        self.set_precision(cfg.get("precision", "32"))
         self.acoustic_encoder = AcousticEncoder(cfg)
         self.motion_encoder = MotionEncoder(cfg)
         self.multimodal_att = MultimodalAttention(
@@ -514,6 +550,7 @@ class SimpleLSTM(LightningSurface):
         self.all_static = cfg.get("all_static", False)
         self.delta_order = metrics.delta_order
 
+    @_in_precision
     def forward(self, acoustic_feature, motion_feature):
         ae = self.acoustic_encoder(acoustic_feature)
         me = self.motion_encoder(motion_feature)
@@ -536,6 +573,7 @@ class SimpleLSTM(LightningSurface):
             return torch.cat([_y, v], dim=-1)
         return torch.cat([_y, v, v - x[:, -1:, :].split(size, dim=-1)[1]], dim=-1)
 
+    @_in_precision
     def training_step(self, batch, *args):
         a, m, target = batch
         dev = self.device
@@ -547,6 +585,7 @@ class SimpleLSTM(LightningSurface):
         self.log("train_loss", loss, prog_bar=True, logger=True)
         return {"loss": loss}
 
+    @_in_precision
     def validation_step(self, batch, *args):
         a, m, target = batch
         dev = self.device

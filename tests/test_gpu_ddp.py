@@ -1,0 +1,72 @@
+"""The data-parallel path with the real kernels: 2 ranks sharing the one GPU of the box (gloo carries
+the gradient exchange; RCCL refuses two ranks on one device), each training on half of the golden
+batch.  GradReducer(overlap=True) issues bucketed all-reduces DURING backward from the library's
+gradient-ready points (ddp.py); after a census step, the averaged gradients must equal the
+reference's full-batch gradients (tests/golden/metaformer_small_r1.npz) and agree across ranks."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from tests.golden_util import load, config, batch_from, prefixed, rel_err
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.cuda.set_device(0)
+    from multimodalreactiongeneration_amd.ddp import init_from_env, GradReducer
+    from multimodalreactiongeneration_amd.model import Metaformer
+    from multimodalreactiongeneration_amd import functional as Fn
+    init_from_env(backend="gloo")
+    d = load("metaformer_small_r1")
+    cfg = config(d)
+    m = Metaformer(cfg["model"], cfg["optim"], cfg["metrics"])
+    m.load_state_dict(prefixed(d, "param/"))
+    m = m.to("cuda:0")
+    opt = m.configure_optimizers()["optimizer"]
+    red = GradReducer(opt.flat_grad, params=opt.plist, overlap=True, bucket_bytes=64 << 10)
+    batch = batch_from(d)
+    per = batch[0][0].shape[0] // world
+    shard = [(x[rank * per:(rank + 1) * per].to("cuda:0"), n[rank * per:(rank + 1) * per]) for x, n in batch]
+    for step in range(2):   # census, then overlapped
+        opt.zero_grad()
+        m.training_step([(x.clone(), n) for x, n in shard])["loss"].backward()
+        red.finish()
+    torch.cuda.synchronize()
+    Fn.check_errors()
+    assert len(red.order) == len(red.buckets) > 2
+    np.save(os.path.join(out_dir, f"g{rank}.npy"), opt.flat_grad.cpu().numpy())
+    red.close()
+    dist.destroy_process_group()
+
+
+def test_two_ranks_overlapped_allreduce_equals_full_batch_gradient():
+    d = load("metaformer_small_r1")
+    out = tempfile.mkdtemp(prefix="mrg_gpu_ddp_")
+    mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    g0, g1 = np.load(os.path.join(out, "g0.npy")), np.load(os.path.join(out, "g1.npy"))
+    assert np.array_equal(g0, g1), "ranks disagree after the all-reduce"
+    off, worst = 0, 0.0
+    for k, v in prefixed(d, "param/").items():
+        n = v.numel()
+        ref = d["grad/" + k]
+        if np.abs(ref).max() > 1e-6:
+            worst = max(worst, rel_err(torch.from_numpy(g0[off:off + n].reshape(ref.shape)), ref))
+        off += n
+    assert off == g0.size
+    assert worst < TOL, worst

@@ -74,10 +74,11 @@ def run_shape(M, N, K, ta, tb, wgrad, iters=20):
 def main():
     from multimodalreactiongeneration_amd import _lib
     modes = [int(m) for m in sys.argv[1].split(",")] if len(sys.argv) > 1 else [1, 0]
-    for mode in modes:
-        _lib.check(_lib.load().mrg_gemm_set_mode(mode), "mode")
-        print(f"=== GEMM mode {mode} ({'x6 bf16 split' if mode == 1 else 'exact f32 MFMA'})")
-        one_mode()
+    for mode in modes:   # 2 = bf16 operands (mrg_gemm_bf16_ex, models' precision "bf16")
+        _lib.check(_lib.load().mrg_gemm_set_mode(1 if mode == 2 else mode), "mode")
+        print(f"=== GEMM mode {mode} ({ {0: 'exact f32 MFMA', 1: 'x6 bf16 split', 2: 'bf16 operands'}[mode] })")
+        with Fn.precision("bf16" if mode == 2 else "32"):
+            one_mode()
 
 
 def one_mode():
