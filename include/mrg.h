@@ -161,6 +161,58 @@ int mrg_gru_cell_bwd(int B, int H, const float* gates, long g_ld, const float* g
  * LSTM launches into buf ([T][8] u64); null disables.  Never in timed runs. */
 int mrg_lstm_debug_stamps(void* buf);
 
+/* ---------------------------------------------------------------- scheduled-sampling decode
+ * The per-frame kernels of lstm_with_sampling's autoregressive training step
+ * (LSTMwithSample.head_motion_generation / generate_one_step, lstm_with_sample.py:379-433), whose
+ * layered LSTM restarts from zero state every frame.  Host side: decode.py.  All
+ * per-frame tensors are [B, ...] row-major slabs; H <= 256 and H % 4 == 0, HB <= 64, FO <= 8.
+ * mrg_ssd_gate_cell_fwd: one zero-state LSTM layer of one frame for B rows; its input X [B, H]
+ *   is mode 0: xin, mode 1: LayerNorm(hp + rp) of the previous layer (gamma, beta; its mean /
+ *   rstd written).  X goes to xout (unless it is xin); gates [B, 4H] (i, f, g, o), c, h [B, H].
+ * mrg_ssd_feat_gate_cell_fwd: the same for layer 1 of frame t, whose input is the frame's features
+ *   X = p + ms_in W_ms^T (p = P(t): the projection of the sampler / partner columns; wms_t =
+ *   W_ms^T [FO, H]) with ms_in = ms[:, 0] at t = 0 and, for t > 0, ms_in = mask[t-1] ? y(t-1) :
+ *   ms[:, t-1] where y(t-1) = z(t-1) W2^T + b2 is written to y[b * y_bs + o]; ms_in goes to
+ *   xf_ms[b * F + o] and X to xout.
+ * mrg_ssd_ffn_z_fwd: u = LayerNorm(hp + rp) of the last layer (mean / rstd written),
+ *   z = relu(u W1^T + b1) [B, HB].
+ * mrg_ssd_y_fwd: y = z W2^T + b2 -> y[b * y_bs + o] (the last frame's; earlier frames' come from
+ *   mrg_ssd_feat_gate_cell_fwd of the next frame).
+ * mrg_ssd_ffn_bwd: last layer of frame t: dy_total = dy(t) + mask[t] (dfeat_next W_ms) -> dyt
+ *   [B, FO]; dz [B, HB]; du = dz W1 [B, H]; LayerNorm backward g = d(h + x) (its row sums through
+ *   v = [W1 gamma | W1 beta] [HB, 2]); zero-state cell backward -> dG [B, 4H].
+ * mrg_ssd_ln_cell_bwd: a lower layer: LayerNorm backward of upstream du, then the cell -> g, dG.
+ * mrg_ssd_dx: dx [B, H] = dG [B, 4H] W_ih + g, with W_ih given transposed (w_t [H, 4H]).       */
+int mrg_ssd_gate_cell_fwd(int B, int H, int mode, const float* xin, const float* hp, const float* rp,
+                          const float* gamma, const float* beta, float eps, float* xout, float* mean,
+                          float* rstd, const float* w_ih, const float* b_ih, const float* b_hh, float* gates,
+                          float* c, float* h, hipStream_t stream);
+int mrg_ssd_feat_gate_cell_fwd(int B, int H, int HB, int FO, int F, int t, const float* p, const float* z,
+                               const float* w2, const float* b2, const unsigned char* mask, const float* ms,
+                               long ms_bs, long ms_ts, const float* wms_t, float* y, long y_bs, float* xf_ms,
+                               float* xout, const float* w_ih, const float* b_ih, const float* b_hh,
+                               float* gates, float* c, float* h, hipStream_t stream);
+/* Timing experiments only: mrg_ssd_gate_cell_fwd (mode 1) with parts removed (dbg 1: no input
+ * prologue, 2: no gate GEMM, 3: neither); H = 256.  Outputs are not meaningful for dbg != 0. */
+int mrg_ssd_gate_cell_fwd_dbg(int dbg, int B, int H, int mode, const float* xin, const float* hp,
+                              const float* rp, const float* gamma, const float* beta, float eps, float* xout,
+                              float* mean, float* rstd, const float* w_ih, const float* b_ih,
+                              const float* b_hh, float* gates, float* c, float* h, hipStream_t stream);
+int mrg_ssd_ffn_z_fwd(int B, int H, int HB, const float* hp, const float* rp, const float* gamma,
+                      const float* beta, float eps, float* u, float* mean, float* rstd, const float* w1,
+                      const float* b1, float* z, hipStream_t stream);
+int mrg_ssd_y_fwd(int B, int HB, int FO, const float* z, const float* w2, const float* b2, float* y, long y_bs,
+                  hipStream_t stream);
+int mrg_ssd_ffn_bwd(int B, int H, int HB, int FO, int t, const float* dy, long dy_bs, const float* dfeat_next,
+                    const float* wms_t, const unsigned char* mask, const float* w1, const float* w2,
+                    const float* b1, const float* v, const float* z, float* dyt, float* dz, float* du,
+                    const float* h, const float* x, const float* gamma, const float* mean, const float* rstd,
+                    float* g, const float* gates, const float* c, float* dG, hipStream_t stream);
+int mrg_ssd_ln_cell_bwd(int B, int H, const float* du, const float* h, const float* x, const float* gamma,
+                        const float* mean, const float* rstd, float* g, const float* gates, const float* c,
+                        float* dG, hipStream_t stream);
+int mrg_ssd_dx(int B, int H, const float* dG, const float* w_t, const float* g, float* dx, hipStream_t stream);
+
 /* ---------------------------------------------------------------- attention
  * Scaled-dot-product core of nn.MultiheadAttention as the reference calls it
  * (MHAforSequentail.forward, for_sequential.py:42-51;

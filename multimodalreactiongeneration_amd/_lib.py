@@ -93,6 +93,17 @@ SIGNATURES = {
                                        c_float, c_float, c_int, c_float, P, P, P]),
     "mrg_broadcast_loss_bwd": (c_int, [c_int, c_int, c_int, P, c_long, P, P, c_long, c_long, c_int, c_int,
                                        c_float, c_float, c_int, c_float, P, P, P, P]),
+    "mrg_ssd_gate_cell_fwd": (c_int, [c_int, c_int, c_int, P, P, P, P, P, c_float, P, P, P, P, P, P, P, P, P, P]),
+    "mrg_ssd_gate_cell_fwd_dbg": (c_int, [c_int, c_int, c_int, c_int, P, P, P, P, P, c_float, P, P, P, P, P, P, P,
+                                          P, P, P]),
+    "mrg_ssd_feat_gate_cell_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, P, P, P, c_long, c_long,
+                                           P, P, c_long, P, P, P, P, P, P, P, P, P]),
+    "mrg_ssd_dx": (c_int, [c_int, c_int, P, P, P, P, P]),
+    "mrg_ssd_ffn_z_fwd": (c_int, [c_int, c_int, c_int, P, P, P, P, c_float, P, P, P, P, P, P, P]),
+    "mrg_ssd_y_fwd": (c_int, [c_int, c_int, c_int, P, P, P, P, c_long, P]),
+    "mrg_ssd_ffn_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_long, P, P, P, P, P, P, P, P, P, P, P,
+                                P, P, P, P, P, P, P, P, P, P]),
+    "mrg_ssd_ln_cell_bwd": (c_int, [c_int, c_int, P, P, P, P, P, P, P, P, P, P, P]),
     "mrg_adamw_step": (c_int, [P, P, P, P, c_long, P, c_float, c_float, c_float, c_float, P, P]),
     "mrg_lstm_debug_inject": (c_int, [c_int]),
 }

@@ -52,6 +52,8 @@ struct GemmArgs {
   float* asum_out;
   float* asum_out2;
   float asum_beta;
+  // few-row kernel: byte extent of A and B from their base pointers (buffer-load range checks)
+  int a_bytes, b_bytes;
 };
 
 #ifndef MRG_GEMM_COUNTERS
@@ -871,6 +873,13 @@ static void launch_tile_x6(GemmArgs a, int ta, int tb, bool va, bool vb, int spl
 // quarters and each wave's 4 lane groups contiguous sub-ranges of those (operands load as runs),
 // all loads of a chunk are in flight at once, and the 4 partial blocks are summed in LDS in a
 // fixed order before the epilogue.  Arithmetic: fp32 FMA chains (no bf16 split needed).
+typedef unsigned int u32x4r __attribute__((ext_vector_type(4)));
+static constexpr int ROWS_OOB = 0x7fffff00;  // masked-off lanes load past every range (hardware zero)
+
+// Operand loads are range-checked buffer loads with the out-of-range lanes pointed past the
+// descriptor (cdna_hip_programming.md T8): no branch per load, so a lane's whole chunk of loads is
+// in flight at once.  (Guarded plain loads compiled to a branch + vmcnt(0) per 4 elements: one L2
+// round trip per load, 9 us for a 64 x 256 x 1024 product.)
 template <int TA, int TB, int CH>
 __global__ __launch_bounds__(256) void gemm_rows_kernel(GemmArgs a) {
   __shared__ float red[4][16][17];
@@ -883,39 +892,41 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(GemmArgs a) {
   const int ke = min(a.K, kb + KQ);
   const int m = m0 + l16, n = n0 + l16;
   const bool mv = m < a.M, nv = n < a.N;
-  // A(m, k): row m of A (TA = 0) or element m of row k (TA = 1, A stored k-major)
-  const float* ap = a.A + (TA ? m : (mv ? a.amap.off(m) : 0));
-  const float* bp = a.B + (TB ? (nv ? a.bmap.off(n) : 0) : n);
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.A), (short)0, a.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.B), (short)0, a.b_bytes, 0x00020000);
+  // element offsets of this lane's row (A, TA = 0) / column (B, TB = 1); the other forms walk rows of k
+  const long arow = (!TA && mv) ? a.amap.off(m) : 0;
+  const long bcol = (TB && nv) ? a.bmap.off(n) : 0;
   const bool sums = TA && a.asum_out && blockIdx.x == 0;
   f32x4v acc = f32x4v{0.f, 0.f, 0.f, 0.f};
   float rs = 0.0f;
-  // k-contiguous operands (A when TA = 0, B when TB = 1) load as float4 when this lane's run is
-  // 16-B aligned: a quarter of the load instructions
-  const bool va = !TA && (KQ & 3) == 0 && (((uintptr_t)(ap + kb)) & 15) == 0;
-  const bool vb = TB && (KQ & 3) == 0 && (((uintptr_t)(bp + kb)) & 15) == 0;
   for (int k0 = kb; k0 < ke; k0 += CH) {
     float av[CH], bv[CH];
 #pragma unroll
     for (int s = 0; s < CH; s += 4) {
       const int k = k0 + s;
-      if (va && k + 3 < ke) {
-        const float4 v = mv ? *reinterpret_cast<const float4*>(ap + k) : make_float4(0.f, 0.f, 0.f, 0.f);
-        av[s] = v.x; av[s + 1] = v.y; av[s + 2] = v.z; av[s + 3] = v.w;
+      if (!TA) {  // 4 consecutive k of row m: one 16-B load, the k >= ke tail zeroed by select
+        const int off = (mv && k < ke) ? (int)((arow + k) * 4) : ROWS_OOB;
+        const float4 v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0));
+        av[s] = v.x; av[s + 1] = k + 1 < ke ? v.y : 0.0f; av[s + 2] = k + 2 < ke ? v.z : 0.0f;
+        av[s + 3] = k + 3 < ke ? v.w : 0.0f;
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const bool ok = k + e < ke;
-          av[s + e] = (ok && mv) ? (TA ? ap[a.amap.off(k + e)] : ap[k + e]) : 0.0f;
+          const int off = (mv && k + e < ke) ? (int)((a.amap.off(k + e) + m) * 4) : ROWS_OOB;
+          av[s + e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ra, off, 0, 0));
         }
       }
-      if (vb && k + 3 < ke) {
-        const float4 v = nv ? *reinterpret_cast<const float4*>(bp + k) : make_float4(0.f, 0.f, 0.f, 0.f);
-        bv[s] = v.x; bv[s + 1] = v.y; bv[s + 2] = v.z; bv[s + 3] = v.w;
+      if (TB) {
+        const int off = (nv && k < ke) ? (int)((bcol + k) * 4) : ROWS_OOB;
+        const float4 v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rb, off, 0, 0));
+        bv[s] = v.x; bv[s + 1] = k + 1 < ke ? v.y : 0.0f; bv[s + 2] = k + 2 < ke ? v.z : 0.0f;
+        bv[s + 3] = k + 3 < ke ? v.w : 0.0f;
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const bool ok = k + e < ke;
-          bv[s + e] = (ok && nv) ? (TB ? bp[k + e] : bp[a.bmap.off(k + e)]) : 0.0f;
+          const int off = (nv && k + e < ke) ? (int)((a.bmap.off(k + e) + n) * 4) : ROWS_OOB;
+          bv[s + e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, off, 0, 0));
         }
       }
     }
@@ -1097,9 +1108,15 @@ static int gemm_ex(int mode, int M, int N, int K, float alpha,
            (!aux || (ldaux & 3) == 0) && (!a.ws || (N & 3) == 0)) ? 1 : 0;
   // few-row products (x6 mode): exact f32 MFMA from registers, no split, no LDS staging: M <= 64
   // rows of activations, or a weight gradient over <= 64 rows (K), its bias sums fused
-  if (mx && splits == 1 && ((!transA && M <= 64 && !asum_out) || (transA && K <= 64))) {
+  // (its buffer-load range checks need both operands' extents below 2 GB)
+  const long a_ext = transA ? a.amap.off(K > 0 ? K - 1 : 0) + M : a.amap.off(M > 0 ? M - 1 : 0) + K;
+  const long b_ext = transB ? a.bmap.off(N > 0 ? N - 1 : 0) + K : a.bmap.off(K > 0 ? K - 1 : 0) + N;
+  const bool rows_ok = a_ext * 4 < ROWS_OOB && b_ext * 4 < ROWS_OOB && K > 0;
+  if (mx && splits == 1 && rows_ok && ((!transA && M <= 64 && !asum_out) || (transA && K <= 64))) {
     a.transA = transA ? 1 : 0;
     a.transB = transB ? 1 : 0;
+    a.a_bytes = (int)(a_ext * 4);
+    a.b_bytes = (int)(b_ext * 4);
     launch_rows(a, stream);
     return check_launch("gemm_rows_kernel");
   }

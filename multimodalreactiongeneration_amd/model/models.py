@@ -32,7 +32,7 @@ from torch import nn
 from .. import functional as Fn
 from ..configs import as_attr
 from ..optim import FusedAdamW
-from .layers import Linear, LSTMSampler, LSTMLayerd, MultimodalAttention, run_sequential_ffn
+from .layers import Linear, LSTMSampler, LSTMLayerd, MultimodalAttention, ResidualConnection, run_sequential_ffn
 from .masks import gen_attention_mask
 from .metaformer import MultiModalMetaformer
 from .mixers import mixer_layerd_argments_select, feedforward_block_argments
@@ -439,19 +439,21 @@ class LSTMwithSample(LightningSurface):
         dev = self.device
         (fb, lf), (mp, lp), (ms, ls) = batch[0], batch[1], batch[2]
         T, B = mp.shape[1], mp.shape[0]
-        # time-major copies made once: every per-frame slice below is then contiguous, so the
-        # ops of the T single-frame forwards run on it in place (no per-frame layout copies)
-        fb = fb.to(dev).view(B, T, self.ratio, fb.shape[-1]).transpose(0, 1).contiguous()
-        mp = mp.to(dev).transpose(0, 1).unsqueeze(2).contiguous()
-        ms = ms.to(dev).transpose(0, 1).unsqueeze(2).contiguous()
         target = batch[-1][0].to(dev)
-        empty = [(torch.empty(x.shape[0], 0, x.shape[2], device=dev), n) for x, n in batch]
-        _, _, cell = self.forward(*empty[:3], *batch[3:6], cell_state=None)
         if sampling_mask is None:
             if use_scheduled_sampling:
                 sampling_mask = torch.rand(T) < (self.current_epoch / self.max_epochs)
             else:
                 sampling_mask = (torch.ones if full_generation else torch.zeros)(T, dtype=torch.bool)
+        if self.use_fused_decode and self._fused_params() is not None:
+            return self._fused_prediction(batch, sampling_mask), target
+        # time-major copies made once: every per-frame slice below is then contiguous, so the
+        # ops of the T single-frame forwards run on it in place (no per-frame layout copies)
+        fb = fb.to(dev).view(B, T, self.ratio, fb.shape[-1]).transpose(0, 1).contiguous()
+        mp = mp.to(dev).transpose(0, 1).unsqueeze(2).contiguous()
+        ms = ms.to(dev).transpose(0, 1).unsqueeze(2).contiguous()
+        empty = [(torch.empty(x.shape[0], 0, x.shape[2], device=dev), n) for x, n in batch]
+        _, _, cell = self.forward(*empty[:3], *batch[3:6], cell_state=None)
         y = ms[0]
         preds = []
         ones = torch.ones(B, dtype=torch.long)
@@ -466,6 +468,56 @@ class LSTMwithSample(LightningSurface):
             else:
                 y = y if bool(sampling_mask[step]) else ms[step]
         return torch.cat(preds, dim=1), target
+
+    # ---------------- fused decode (decode.py / decode.hip)
+    use_fused_decode = True
+
+    def _fused_params(self):
+        """Parameters of the fused decode, or None when this configuration is outside it (the
+        per-frame path above then runs): layered blocks = residual LN around a 1-layer
+        unidirectional LSTM without mixing or feed-forward, FFN = Linear -> ReLU -> Linear."""
+        try:
+            layers = []
+            for blk in self.layerd_lstm.lstm_layered:
+                rc = blk.lstm_module
+                if blk.use_feed_forward or not isinstance(rc, ResidualConnection) or rc.layer_norm is None:
+                    return None
+                mod = rc.module
+                if mod.mixer is not None:
+                    return None
+                lstm = mod.lstm_module
+                if lstm.num_layers != 1 or lstm.bidirectional:
+                    return None
+                ln = rc.layer_norm
+                layers.append((*lstm.direction_params(0), ln.weight, ln.bias))
+            ff = list(self.feed_forward.children())
+            if len(ff) != 3 or not isinstance(ff[1], nn.ReLU):
+                return None
+            H = self.feature_projection.weight.shape[0]
+            if not (4 <= H <= 256 and H % 4 == 0 and ff[0].weight.shape[0] <= 64 and ff[2].weight.shape[0] <= 8):
+                return None
+            if any(p[4].shape[0] != H or abs(rc.layer_norm.eps - 1e-5) > 0 for p in layers):
+                return None
+            return layers, (ff[0].weight, ff[0].bias, ff[2].weight, ff[2].bias)
+        except AttributeError:
+            return None
+
+    def _fused_prediction(self, batch, sampling_mask):
+        """head_motion_generation with the sampler over the whole audio sequence in one pass and the
+        per-frame chain in the fused kernels (decode.py).  Equivalent to the per-frame path: the
+        sampler state the reference carries (warm-up over the lead, then frame by frame) is the
+        state of one LSTM pass over [lead audio | frame audio]."""
+        from ..decode import scheduled_sampling_decode
+        dev = self.device
+        a = _cat_lead(batch[3][0].to(dev), batch[0][0].to(dev))
+        a, _ = self.sampling_lstm(self.acoustic_projection(a), None)
+        lead, T = batch[4][0].shape[1], batch[1][0].shape[1]
+        if a.shape[1] != lead + T:
+            raise RuntimeError(f"acoustic: {a.shape} motion frames: {lead} + {T} ratio: {self.ratio}")
+        layers, ffn = self._fused_params()
+        return scheduled_sampling_decode(a[:, lead:], batch[1][0], batch[2][0], sampling_mask,
+                                         self.feature_projection.weight, self.feature_projection.bias,
+                                         layers, ffn, eps=self.layerd_lstm.lstm_layered[0].lstm_module.layer_norm.eps)
 
 
 class AcousticEncoder(nn.Module):

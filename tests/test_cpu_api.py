@@ -168,3 +168,14 @@ def test_checkpoint_round_trip_through_load_model(tmp_path, model_type):
     assert all(torch.equal(got2.state_dict()[k], sd[k]) for k in sd)
     with pytest.raises(ValueError):
         M.load_model("gru_former", str(path), cfg)
+
+
+def test_ctypes_signatures_match_header_arity():
+    """Every binding in _lib.SIGNATURES declares as many arguments as include/mrg.h gives the entry."""
+    from multimodalreactiongeneration_amd import _lib
+    h = open(os.path.join(ROOT, "include", "mrg.h")).read()
+    for name, (_res, args) in _lib.SIGNATURES.items():
+        m = re.search(r"^(?:const\s+)?\w+\s*\**\s*" + name + r"\s*\(([^;]*?)\);", h, re.S | re.M)
+        assert m, name
+        params = [x for x in m.group(1).split(",") if x.strip() and x.strip() != "void"]
+        assert len(params) == len(args), (name, len(params), len(args))
