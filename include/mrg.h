@@ -213,6 +213,14 @@ int mrg_ssd_ln_cell_bwd(int B, int H, const float* du, const float* h, const flo
                         float* dG, hipStream_t stream);
 int mrg_ssd_dx(int B, int H, const float* dG, const float* w_t, const float* g, float* dx, hipStream_t stream);
 
+/* One step (T = 1) of an LSTM direction with a carried state (the generation loops' mixers,
+ * lstmformer.py:466-521): gates = [x | h0] [W_ih | W_hh]^T + b_ih + b_hh (i, f, g, o) -> gates
+ * [B, 4H], c = f c0 + i g [B, H], h -> y[b * ldy + u] and hT [B, H] (nullable); h0 / c0 nullable
+ * (zero state).  In, H multiples of 4, In + H <= 512.  Replaces two GEMMs + mrg_lstm_cell_fwd. */
+int mrg_lstm_step_fwd(int B, int H, int In, const float* x, const float* h0, const float* c0,
+                      const float* w_ih, const float* w_hh, const float* b_ih, const float* b_hh,
+                      float* gates, float* c, float* y, long ldy, float* hT, hipStream_t stream);
+
 /* ---------------------------------------------------------------- attention
  * Scaled-dot-product core of nn.MultiheadAttention as the reference calls it
  * (MHAforSequentail.forward, for_sequential.py:42-51;

@@ -99,6 +99,7 @@ SIGNATURES = {
     "mrg_ssd_feat_gate_cell_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, P, P, P, c_long, c_long,
                                            P, P, c_long, P, P, P, P, P, P, P, P, P]),
     "mrg_ssd_dx": (c_int, [c_int, c_int, P, P, P, P, P]),
+    "mrg_lstm_step_fwd": (c_int, [c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, c_long, P, P]),
     "mrg_ssd_ffn_z_fwd": (c_int, [c_int, c_int, c_int, P, P, P, P, c_float, P, P, P, P, P, P, P]),
     "mrg_ssd_y_fwd": (c_int, [c_int, c_int, c_int, P, P, P, P, c_long, P]),
     "mrg_ssd_ffn_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_long, P, P, P, P, P, P, P, P, P, P, P,

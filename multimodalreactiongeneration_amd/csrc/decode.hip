@@ -620,6 +620,107 @@ __global__ __launch_bounds__(256) void ssd_ln_cell_bwd_kernel(int H, const float
   d[3 * H] = gv * tc * og * (1.0f - og);
 }
 
+
+// One step (T = 1) of an LSTM with a carried state: the per-frame forward of the autoregressive
+// generation loops (Metaformer.prediction's generate_one_step, lstmformer.py:466-521, whose mixer
+// LSTMs carry (h, c) from frame to frame).  gates = [x | h0] [W_ih | W_hh]^T + b_ih + b_hh and the
+// cell in ONE launch (it was two GEMMs and a cell kernel): the same 16 rows x 4 units MFMA tile as
+// ssd_gate_cell_fwd_kernel over the concatenated K = In + H (zero-padded to KMAX), the operands
+// loaded branch-free from both sources (the other source's lane reads out of range, i.e. 0).
+struct LstmStepArgs {
+  int B, H, In;
+  const float* x;    // [B][In]
+  const float* h0;   // [B][H] or null (zero state)
+  const float* c0;   // [B][H] or null
+  const float* w_ih;  // [4H][In]
+  const float* w_hh;  // [4H][H]
+  const float* b_ih;
+  const float* b_hh;
+  float* gates;      // [B][4H] i, f, g, o (post-activation)
+  float* c;          // [B][H]
+  float* y;          // y[b * ldy + u]
+  long ldy;
+  float* hT;         // [B][H] or null
+};
+
+template <int KMAX>
+__global__ __launch_bounds__(256) void lstm_step_fwd_kernel(LstmStepArgs a) {
+  constexpr int LDK = KMAX + 2;
+  constexpr int C4 = KMAX / 4;                      // float4 slots a row
+  constexpr int NX = SSD_R * C4 / 256;              // float4 per thread per operand
+  __shared__ __attribute__((aligned(16))) float Xs[SSD_R * LDK];
+  __shared__ __attribute__((aligned(16))) float Ws[16 * LDK];
+  __shared__ float red[4][16][17];
+  __shared__ float bias[16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int H = a.H, In = a.In;
+  const int KA = In, KT = In + (a.h0 ? H : 0);
+  const int r0 = blockIdx.y * SSD_R, u0 = blockIdx.x * SSD_U;
+  float4 xv[NX], wv[NX];
+#pragma unroll
+  for (int i = 0; i < NX; ++i) {
+    const int e = tid + i * 256, rr = e / C4, k = 4 * (e % C4);
+    const int q = rr >> 2, uu = rr & 3, b = r0 + rr, wrow = q * H + u0 + uu;
+    const bool inx = k < KA, inh = k >= KA && k < KT;
+    const float4 x1 = ld4_or0(a.x, (long)b * In + k, inx && b < a.B);
+    const float4 x2 = ld4_or0(a.h0, (long)b * H + (k - KA), inh && b < a.B);
+    const float4 w1 = ld4_or0(a.w_ih, (long)wrow * In + k, inx);
+    const float4 w2 = ld4_or0(a.w_hh, (long)wrow * H + (k - KA), inh);
+    xv[i] = make_float4(x1.x + x2.x, x1.y + x2.y, x1.z + x2.z, x1.w + x2.w);
+    wv[i] = make_float4(w1.x + w2.x, w1.y + w2.y, w1.z + w2.z, w1.w + w2.w);
+  }
+  float cprev = 0.0f;
+  {
+    const int rr = tid >> 2, uu = tid & 3, b = r0 + rr;
+    if (tid < SSD_R * SSD_U) cprev = ld_or0(a.c0, (long)b * H + u0 + uu, a.c0 && b < a.B);
+  }
+  if (tid < 16) {
+    const int q = tid >> 2, uu = tid & 3;
+    bias[tid] = ld_or0(a.b_ih, q * H + u0 + uu, true) + ld_or0(a.b_hh, q * H + u0 + uu, true);
+  }
+#pragma unroll
+  for (int i = 0; i < NX; ++i) {
+    const int e = tid + i * 256, rr = e / C4, k = 4 * (e % C4);
+    float2* xd = reinterpret_cast<float2*>(&Xs[rr * LDK + k]);
+    xd[0] = make_float2(xv[i].x, xv[i].y);
+    xd[1] = make_float2(xv[i].z, xv[i].w);
+    float2* wd = reinterpret_cast<float2*>(&Ws[rr * LDK + k]);
+    wd[0] = make_float2(wv[i].x, wv[i].y);
+    wd[1] = make_float2(wv[i].z, wv[i].w);
+  }
+  __syncthreads();
+  // the 4 waves take K quarters of roundup(KT, 32)
+  const int l16 = lane & 15, kg = lane >> 4;
+  const int kq = ((KT + 31) / 32) * 8, kb = wave * kq;
+  ssd_f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  for (int k = kb; k < kb + kq; k += 8) {
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Xs[l16 * LDK + k + kg], Ws[l16 * LDK + k + kg], acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Xs[l16 * LDK + k + 4 + kg], Ws[l16 * LDK + k + 4 + kg], acc1, 0, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) red[wave][4 * kg + i][l16] = acc0[i] + acc1[i];
+  __syncthreads();
+  if (tid < SSD_R * SSD_U) {
+    const int rr = tid >> 2, uu = tid & 3, b = r0 + rr, u = u0 + uu;
+    if (b < a.B && u < H) {
+      float z[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int cc = q * 4 + uu;
+        z[q] = ((red[0][rr][cc] + red[1][rr][cc]) + (red[2][rr][cc] + red[3][rr][cc])) + bias[cc];
+      }
+      const float ig = sigmoidf_(z[0]), fg = sigmoidf_(z[1]), gg = tanhf_(z[2]), og = sigmoidf_(z[3]);
+      const float cn = fg * cprev + ig * gg;
+      float* gs = a.gates + (long)b * 4 * H + u;
+      gs[0] = ig; gs[H] = fg; gs[2 * H] = gg; gs[3 * H] = og;
+      a.c[(long)b * H + u] = cn;
+      const float hv = og * tanhf_(cn);
+      a.y[(long)b * a.ldy + u] = hv;
+      if (a.hT) a.hT[(long)b * H + u] = hv;
+    }
+  }
+}
+
 }  // namespace mrg
 
 using namespace mrg;
@@ -750,4 +851,22 @@ MRG_API int mrg_ssd_ln_cell_bwd(int B, int H, const float* du, const float* h, c
   if (B == 0) return 0;
   ssd_ln_cell_bwd_kernel<<<B, 256, 0, stream>>>(H, du, h, x, gamma, mean, rstd, g, gates, c, dG);
   return check_launch("ssd_ln_cell_bwd_kernel");
+}
+
+MRG_API int mrg_lstm_step_fwd(int B, int H, int In, const float* x, const float* h0, const float* c0,
+                              const float* w_ih, const float* w_hh, const float* b_ih, const float* b_hh,
+                              float* gates, float* c, float* y, long ldy, float* hT, hipStream_t stream) {
+  MRG_REQUIRE(H >= 4 && H % 4 == 0 && In >= 4 && In % 4 == 0 && In + H <= 512,
+              "mrg_lstm_step_fwd: H=%d In=%d (multiples of 4, In + H <= 512)", H, In);
+  MRG_REQUIRE((((uintptr_t)x | (uintptr_t)w_ih | (uintptr_t)(h0 ? h0 : x) | (uintptr_t)w_hh) & 15) == 0,
+              "mrg_lstm_step_fwd: x, h0, w_ih, w_hh must be 16-B aligned");
+  if (B == 0) return 0;
+  LstmStepArgs a;
+  a.B = B; a.H = H; a.In = In; a.x = x; a.h0 = h0; a.c0 = c0; a.w_ih = w_ih; a.w_hh = w_hh; a.b_ih = b_ih;
+  a.b_hh = b_hh; a.gates = gates; a.c = c; a.y = y; a.ldy = ldy; a.hT = hT;
+  const dim3 grid(H / SSD_U, (B + SSD_R - 1) / SSD_R);
+  const int kt = In + (h0 ? H : 0);
+  if (kt <= 256) lstm_step_fwd_kernel<256><<<grid, 256, 0, stream>>>(a);
+  else lstm_step_fwd_kernel<512><<<grid, 256, 0, stream>>>(a);
+  return check_launch("lstm_step_fwd_kernel");
 }

@@ -801,18 +801,24 @@ class _LSTMCellFn(Function):
         H = w_hh.shape[1]
         lib = _lib.load()
         x2 = x.reshape(B, In).contiguous()
-        pre = torch.empty(B, 4 * H, device=dev, dtype=torch.float32)
-        gemm(B, 4 * H, In, _ptr(x2), 0, In, _ptr(w_ih), 1, In, _ptr(pre), 4 * H, bias=_ptr(b_ih), device=dev)
         h0c = None if h0 is None else h0.contiguous()
         c0c = None if c0 is None else c0.contiguous()
-        if h0c is not None:
-            gemm(B, 4 * H, H, _ptr(h0c), 0, H, _ptr(w_hh), 1, H, _ptr(pre), 4 * H, beta=1.0, device=dev)
         gates = torch.empty(B, 4 * H, device=dev, dtype=torch.float32)
         c = torch.empty(B, H, device=dev, dtype=torch.float32)
         y = torch.empty(B, 1, H, device=dev, dtype=torch.float32)
         hT = torch.empty(B, H, device=dev, dtype=torch.float32)
-        _lib.check(lib.mrg_lstm_cell_fwd(B, H, _ptr(pre), 4 * H, _ptr(b_hh), _ptr(c0c), _ptr(gates), _ptr(c),
-                                         _ptr(y), H, _ptr(hT), _stream()), "lstm cell fwd")
+        if _ARITH[0] is None and In % 4 == 0 and H % 4 == 0 and In + H <= 512:
+            # gates GEMMs + cell in one launch (decode.hip lstm_step_fwd_kernel)
+            _lib.check(lib.mrg_lstm_step_fwd(B, H, In, _ptr(x2), _ptr(h0c), _ptr(c0c), _ptr(w_ih), _ptr(w_hh),
+                                             _ptr(b_ih), _ptr(b_hh), _ptr(gates), _ptr(c), _ptr(y), H, _ptr(hT),
+                                             _stream()), "lstm step fwd")
+        else:
+            pre = torch.empty(B, 4 * H, device=dev, dtype=torch.float32)
+            gemm(B, 4 * H, In, _ptr(x2), 0, In, _ptr(w_ih), 1, In, _ptr(pre), 4 * H, bias=_ptr(b_ih), device=dev)
+            if h0c is not None:
+                gemm(B, 4 * H, H, _ptr(h0c), 0, H, _ptr(w_hh), 1, H, _ptr(pre), 4 * H, beta=1.0, device=dev)
+            _lib.check(lib.mrg_lstm_cell_fwd(B, H, _ptr(pre), 4 * H, _ptr(b_hh), _ptr(c0c), _ptr(gates), _ptr(c),
+                                             _ptr(y), H, _ptr(hT), _stream()), "lstm cell fwd")
         ctx.save_for_backward(x2, w_ih, w_hh, b_ih, b_hh, h0c, c0c, gates, c)
         ctx.set_materialize_grads(False)  # an unused final state costs no zero-filled gradient
         return y, hT, c
