@@ -160,6 +160,9 @@ int mrg_gru_cell_bwd(int B, int H, const float* gates, long g_ld, const float* g
 /* Diagnostics only: record per-step phase clocks (s_memtime) of block 0 of the next
  * LSTM launches into buf ([T][8] u64); null disables.  Never in timed runs. */
 int mrg_lstm_debug_stamps(void* buf);
+/* Hand-off granule stores at workgroup scope (1, default; the line stays in the XCD's L2 where the
+ * group's agent-scope polls read it) or agent scope (0).  Env MRG_LSTM_LOCAL=0 starts with 0. */
+int mrg_lstm_set_local_handoff(int on);
 
 /* ---------------------------------------------------------------- scheduled-sampling decode
  * The per-frame kernels of lstm_with_sampling's autoregressive training step

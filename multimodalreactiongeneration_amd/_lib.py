@@ -70,6 +70,7 @@ SIGNATURES = {
     "mrg_feature_delta": (c_int, [c_int, c_int, c_int, P, c_long, c_int, P, P]),
     "mrg_pad_sequences": (c_int, [c_int, c_int, c_int, P, P, c_float, P, P]),
     "mrg_lstm_debug_stamps": (c_int, [P]),
+    "mrg_lstm_set_local_handoff": (c_int, [c_int]),
     "mrg_attention_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int,
                                   P, c_long, c_long, P, c_long, c_long, P, c_long, c_long,
                                   P, c_long, c_long, P, P, P, c_int, c_float, P]),

@@ -351,6 +351,37 @@ def test_lstm_batched_problems_and_forced_tiling(bs):
         assert rel_err(y, r) < TOL
 
 
+@pytest.mark.parametrize("H,B", [(256, 64), (256, 24), (128, 16), (32, 5)])
+def test_lstm_local_handoff_is_bitwise_the_agent_one(H, B):
+    """The hand-off store flavour (workgroup scope for groups verified on one XCD, agent scope
+    otherwise; lstm.hip put_granule / group_on_one_xcd) changes no arithmetic: forward outputs,
+    final states and every gradient are bitwise those of the agent-scope hand-offs."""
+    from multimodalreactiongeneration_amd import _lib
+    from multimodalreactiongeneration_amd import functional as Fn
+    lib = _lib.load()
+    T = 37
+    g = torch.Generator().manual_seed(H + B)
+    w = [torch.randn(4 * H, H, generator=g) * 0.06 for _ in range(2)]
+    bb = [torch.randn(4 * H, generator=g) * 0.06 for _ in range(2)]
+    x = torch.randn(B, T, H, generator=g)
+    h0, c0 = torch.randn(B, H, generator=g), torch.randn(B, H, generator=g)
+    outs = []
+    try:
+        for local in (1, 0):
+            _lib.check(lib.mrg_lstm_set_local_handoff(local), "local")
+            ps = [_param(t) for t in (w[0], w[1], bb[0], bb[1])]
+            xx = x.to(DEV).requires_grad_(True)
+            y, hT, cT = Fn.lstm_layer(xx, *ps, h0.to(DEV), c0.to(DEV))
+            (y.square().sum() + hT.sum() + cT.sum()).backward()
+            torch.cuda.synchronize()
+            Fn.check_errors()
+            outs.append([y.detach(), hT.detach(), cT.detach(), xx.grad] + [p.grad for p in ps])
+    finally:
+        lib.mrg_lstm_set_local_handoff(1)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("case", [0, 1, 2])
 def test_mha_with_reference_mask_golden(case):
     from multimodalreactiongeneration_amd.model.layers import MultiheadAttention
