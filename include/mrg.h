@@ -181,10 +181,13 @@ int mrg_lstm_set_local_handoff(int on);
  *   z = relu(u W1^T + b1) [B, HB].
  * mrg_ssd_y_fwd: y = z W2^T + b2 -> y[b * y_bs + o] (the last frame's; earlier frames' come from
  *   mrg_ssd_feat_gate_cell_fwd of the next frame).
- * mrg_ssd_ffn_bwd: last layer of frame t: dy_total = dy(t) + mask[t] (dfeat_next W_ms) -> dyt
+ * mrg_ssd_ffn_bwd: last layer of frame t: dy_total = dy(t) + mask[t] (dfeat_next W_ms, or dyx_next
+ *   when the next frame's bottom layer formed that product already) -> dyt
  *   [B, FO]; dz [B, HB]; du = dz W1 [B, H]; LayerNorm backward g = d(h + x) (its row sums through
  *   v = [W1 gamma | W1 beta] [HB, 2]); zero-state cell backward -> dG [B, 4H].
- * mrg_ssd_ln_cell_bwd: a lower layer: LayerNorm backward of upstream du, then the cell -> g, dG.
+ * mrg_ssd_ln_cell_bwd: a lower layer: LayerNorm backward of upstream du, then the cell -> g, dG;
+ *   with dyx (the bottom layer): dyx [B, FM] = (dG W_ih + g) W_ms as dG vt^T + g wms_t^T
+ *   (vt = W_ms^T W_ih [FM, 4H]), the prediction gradient the select passes to frame t - 1.
  * mrg_ssd_dx: dx [B, H] = dG [B, 4H] W_ih + g, with W_ih given transposed (w_t [H, 4H]).       */
 int mrg_ssd_gate_cell_fwd(int B, int H, int mode, const float* xin, const float* hp, const float* rp,
                           const float* gamma, const float* beta, float eps, float* xout, float* mean,
@@ -207,13 +210,14 @@ int mrg_ssd_ffn_z_fwd(int B, int H, int HB, const float* hp, const float* rp, co
 int mrg_ssd_y_fwd(int B, int HB, int FO, const float* z, const float* w2, const float* b2, float* y, long y_bs,
                   hipStream_t stream);
 int mrg_ssd_ffn_bwd(int B, int H, int HB, int FO, int t, const float* dy, long dy_bs, const float* dfeat_next,
-                    const float* wms_t, const unsigned char* mask, const float* w1, const float* w2,
+                    const float* dyx_next, const float* wms_t, const unsigned char* mask, const float* w1,
+                    const float* w2,
                     const float* b1, const float* v, const float* z, float* dyt, float* dz, float* du,
                     const float* h, const float* x, const float* gamma, const float* mean, const float* rstd,
                     float* g, const float* gates, const float* c, float* dG, hipStream_t stream);
 int mrg_ssd_ln_cell_bwd(int B, int H, const float* du, const float* h, const float* x, const float* gamma,
                         const float* mean, const float* rstd, float* g, const float* gates, const float* c,
-                        float* dG, hipStream_t stream);
+                        float* dG, int FM, const float* vt, const float* wms_t, float* dyx, hipStream_t stream);
 int mrg_ssd_dx(int B, int H, const float* dG, const float* w_t, const float* g, float* dx, hipStream_t stream);
 
 /* One step (T = 1) of an LSTM direction with a carried state (the generation loops' mixers,

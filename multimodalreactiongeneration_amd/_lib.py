@@ -104,8 +104,8 @@ SIGNATURES = {
     "mrg_ssd_ffn_z_fwd": (c_int, [c_int, c_int, c_int, P, P, P, P, c_float, P, P, P, P, P, P, P]),
     "mrg_ssd_y_fwd": (c_int, [c_int, c_int, c_int, P, P, P, P, c_long, P]),
     "mrg_ssd_ffn_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_long, P, P, P, P, P, P, P, P, P, P, P,
-                                P, P, P, P, P, P, P, P, P, P]),
-    "mrg_ssd_ln_cell_bwd": (c_int, [c_int, c_int, P, P, P, P, P, P, P, P, P, P, P]),
+                                P, P, P, P, P, P, P, P, P, P, P]),
+    "mrg_ssd_ln_cell_bwd": (c_int, [c_int, c_int, P, P, P, P, P, P, P, P, P, P, c_int, P, P, P, P]),
     "mrg_adamw_step": (c_int, [P, P, P, P, c_long, P, c_float, c_float, c_float, c_float, P, P]),
     "mrg_lstm_debug_inject": (c_int, [c_int]),
 }

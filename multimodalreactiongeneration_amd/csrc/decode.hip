@@ -422,8 +422,9 @@ struct SsdFfnBwdArgs {
   int B, H, HB, FO, t;
   const float* dy;          // dy(t)[b * dy_bs + o]
   long dy_bs;
-  const float* dfeat_next;  // dfeat(t + 1) [B][H] (null at the last frame)
+  const float* dfeat_next;  // dfeat(t + 1) [B][H] (null at the last frame, or when dyx_next is given)
   const float* wms;         // W_ms^T [FO][H]
+  const float* dyx_next;    // dfeat(t + 1) W_ms [B][FO], from frame t + 1's bottom layer (nullable)
   const unsigned char* mask;
   const float* w1;          // [HB][H]
   const float* w2;          // [FO][HB]
@@ -479,7 +480,9 @@ __global__ __launch_bounds__(256) void ssd_ffn_bwd_kernel(SsdFfnBwdArgs a) {
     v2[i] = ld_or0(a.v, 2 * j + 1, j < a.HB);
     b1v[i] = ld_or0(a.b1, j, j < a.HB);
   }
-  const float dyv = ld_or0(a.dy, (long)ba * a.dy_bs + (pa & 7), pa < 8 && pa < a.FO && ba < a.B);
+  const bool fed2 = a.dyx_next != nullptr && a.mask[a.t] != 0;
+  const float dyv = ld_or0(a.dy, (long)ba * a.dy_bs + (pa & 7), pa < 8 && pa < a.FO && ba < a.B) +
+                    ld_or0(a.dyx_next, (long)ba * a.FO + (pa & 7), fed2 && pa < 8 && pa < a.FO && ba < a.B);
   // W1 columns k0..k0+7 of all HB rows -> LDS (thread = (row j, half))
   {
     const int j = tid >> 1, hf = tid & 1;
@@ -585,14 +588,22 @@ __device__ __forceinline__ void block_sums256(float (&v)[N], float (*sh)[4]) {
   __syncthreads();
 }
 
+// With dyx given (the bottom layer of a frame): also the frame's contribution to the previous
+// frame's prediction gradient through the sampling select, dyx[b][o] = dfeat[b] . W_ms[:, o] with
+// dfeat = dG W_ih + g, taken as dG . vt[o] + g . wms_t[o] (vt = W_ms^T W_ih, [FM][4H], formed once
+// per backward), so the frame needs no dX product of its own (decode.py forms every frame's dfeat
+// in one GEMM after the loop).
 __global__ __launch_bounds__(256) void ssd_ln_cell_bwd_kernel(int H, const float* __restrict__ du_in,
                                                               const float* __restrict__ h, const float* __restrict__ x,
                                                               const float* __restrict__ gamma,
                                                               const float* __restrict__ mean,
                                                               const float* __restrict__ rstd, float* __restrict__ g,
                                                               const float* __restrict__ gates,
-                                                              const float* __restrict__ c, float* __restrict__ dG) {
-  __shared__ float sh[2][4];
+                                                              const float* __restrict__ c, float* __restrict__ dG,
+                                                              int FM, const float* __restrict__ vt,
+                                                              const float* __restrict__ wms_t,
+                                                              float* __restrict__ dyx) {
+  __shared__ float sh[8][4];
   const int b = blockIdx.x, k = threadIdx.x;
   const bool kv = k < H;
   const float mn = ld_or0(mean, b, true), rs = ld_or0(rstd, b, true);
@@ -603,23 +614,49 @@ __global__ __launch_bounds__(256) void ssd_ln_cell_bwd_kernel(int H, const float
   const float gg = ld_or0(gates, (long)b * 4 * H + 2 * H + k, kv);
   const float og = ld_or0(gates, (long)b * 4 * H + 3 * H + k, kv);
   const float du = ld_or0(du_in, (long)b * H + k, kv);
+  const bool ext = dyx != nullptr;
+  float vi[8], vg[8], vo[8], wm[8];
+#pragma unroll
+  for (int o = 0; o < 8; ++o) {
+    const bool ok = ext && kv && o < FM;
+    vi[o] = ld_or0(vt, (long)o * 4 * H + k, ok);
+    vg[o] = ld_or0(vt, (long)o * 4 * H + 2 * H + k, ok);
+    vo[o] = ld_or0(vt, (long)o * 4 * H + 3 * H + k, ok);
+    wm[o] = ld_or0(wms_t, (long)o * H + k, ok);
+  }
   // LayerNorm backward: g = rstd (gd - mean(gd) - xh mean(gd xh)), gd = du * gamma
   const float xh = kv ? (hx - mn) * rs : 0.0f;
   const float gd = du * gam;
   float m[2] = {gd, gd * xh};
   block_sums256<2>(m, sh);
-  if (!kv) return;
   const float gv = rs * (gd - m[0] / (float)H - xh * (m[1] / (float)H));
-  g[(long)b * H + k] = gv;
   const float tc = tanhf_(cc);
   const float dc = gv * og * (1.0f - tc * tc);
-  float* d = dG + (long)b * 4 * H + k;
-  d[0] = dc * gg * ig * (1.0f - ig);
-  d[H] = 0.0f;
-  d[2 * H] = dc * ig * (1.0f - gg * gg);
-  d[3 * H] = gv * tc * og * (1.0f - og);
+  const float d_i = dc * gg * ig * (1.0f - ig);
+  const float d_g = dc * ig * (1.0f - gg * gg);
+  const float d_o = gv * tc * og * (1.0f - og);
+  if (kv) {
+    g[(long)b * H + k] = gv;
+    float* d = dG + (long)b * 4 * H + k;
+    d[0] = d_i;
+    d[H] = 0.0f;
+    d[2 * H] = d_g;
+    d[3 * H] = d_o;
+  }
+  if (!ext) return;  // uniform
+  float p[8];
+#pragma unroll
+  for (int o = 0; o < 8; ++o) {
+    p[o] = kv ? fmaf(d_i, vi[o], fmaf(d_g, vg[o], fmaf(d_o, vo[o], gv * wm[o]))) : 0.0f;
+  }
+  block_sums256<8>(p, sh);
+  if (k < FM) {
+    float v = 0.0f;
+#pragma unroll
+    for (int o = 0; o < 8; ++o) v = (k == o) ? p[o] : v;
+    dyx[(long)b * FM + k] = v;
+  }
 }
-
 
 // One step (T = 1) of an LSTM with a carried state: the per-frame forward of the autoregressive
 // generation loops (Metaformer.prediction's generate_one_step, lstmformer.py:466-521, whose mixer
@@ -827,7 +864,8 @@ MRG_API int mrg_ssd_y_fwd(int B, int HB, int FO, const float* z, const float* w2
 }
 
 MRG_API int mrg_ssd_ffn_bwd(int B, int H, int HB, int FO, int t, const float* dy, long dy_bs, const float* dfeat_next,
-                            const float* wms_t, const unsigned char* mask, const float* w1, const float* w2,
+                            const float* dyx_next, const float* wms_t, const unsigned char* mask, const float* w1,
+                            const float* w2,
                             const float* b1, const float* v, const float* z, float* dyt, float* dz, float* du,
                             const float* h, const float* x, const float* gamma, const float* mean, const float* rstd,
                             float* g, const float* gates, const float* c, float* dG, hipStream_t stream) {
@@ -837,7 +875,9 @@ MRG_API int mrg_ssd_ffn_bwd(int B, int H, int HB, int FO, int t, const float* dy
               "mrg_ssd_ffn_bwd: w1, wms_t, dfeat_next must be 16-B aligned");
   if (B == 0) return 0;
   SsdFfnBwdArgs a;
+  MRG_REQUIRE(!(dfeat_next && dyx_next), "mrg_ssd_ffn_bwd: dfeat_next or dyx_next, not both");
   a.B = B; a.H = H; a.HB = HB; a.FO = FO; a.t = t; a.dy = dy; a.dy_bs = dy_bs; a.dfeat_next = dfeat_next;
+  a.dyx_next = dyx_next;
   a.wms = wms_t; a.mask = mask; a.w1 = w1; a.w2 = w2; a.b1 = b1; a.v = v; a.z = z; a.dyt = dyt; a.dz = dz; a.du = du;
   a.h = h; a.x = x; a.gamma = gamma; a.mean = mean; a.rstd = rstd; a.g = g; a.gates = gates; a.c = c; a.dG = dG;
   ssd_ffn_bwd_kernel<<<dim3((H + 7) / 8, (B + 7) / 8), 256, 0, stream>>>(a);
@@ -846,10 +886,12 @@ MRG_API int mrg_ssd_ffn_bwd(int B, int H, int HB, int FO, int t, const float* dy
 
 MRG_API int mrg_ssd_ln_cell_bwd(int B, int H, const float* du, const float* h, const float* x, const float* gamma,
                                 const float* mean, const float* rstd, float* g, const float* gates, const float* c,
-                                float* dG, hipStream_t stream) {
-  MRG_REQUIRE(H >= 1 && H <= 256, "mrg_ssd_ln_cell_bwd: H=%d (1..256)", H);
+                                float* dG, int FM, const float* vt, const float* wms_t, float* dyx,
+                                hipStream_t stream) {
+  MRG_REQUIRE(H >= 1 && H <= 256 && FM >= 0 && FM <= 8, "mrg_ssd_ln_cell_bwd: H=%d (1..256) FM=%d", H, FM);
+  MRG_REQUIRE(!dyx || (vt && wms_t && FM > 0), "mrg_ssd_ln_cell_bwd: dyx needs vt, wms_t, FM");
   if (B == 0) return 0;
-  ssd_ln_cell_bwd_kernel<<<B, 256, 0, stream>>>(H, du, h, x, gamma, mean, rstd, g, gates, c, dG);
+  ssd_ln_cell_bwd_kernel<<<B, 256, 0, stream>>>(H, du, h, x, gamma, mean, rstd, g, gates, c, dG, FM, vt, wms_t, dyx);
   return check_launch("ssd_ln_cell_bwd_kernel");
 }
 

@@ -130,31 +130,47 @@ class _SSDecodeFn(Function):
         dX = [torch.empty(T, B, H, device=dev, dtype=F32) for _ in range(nl)]  # dX[0] = dfeat
         slab, gslab, zslab = B * H, B * 4 * H, B * HB
         # W_ih^T copies: the per-frame dX = dG W_ih reads both operands k-contiguous (float4)
-        w_t = [lay[0].t().contiguous() for lay in layers]
+        w_t = [None if (nl >= 2 and i == 0) else lay[0].t().contiguous() for i, lay in enumerate(layers)]
         # v = [W1 gamma | W1 beta] [HB, 2] of the last LayerNorm: its row sums through W1 (decode.hip)
         lw, lb = layers[-1][4], layers[-1][5]
         gb = torch.stack([lw.detach(), lb.detach()])
         v = torch.empty(HB, 2, device=dev, dtype=F32)
         gemm(HB, 2, H, _ptr(w1), 0, H, _ptr(gb), 1, H, _ptr(v), 2, device=dev)
+        # the bottom layer forms each frame's y gradient through the select itself (dyx = dfeat W_ms
+        # with vt = W_ms^T W_ih0), so its dX (dfeat) is one GEMM over all frames after the loop
+        ext = nl >= 2
+        if ext:
+            vt = torch.empty(FM, 4 * H, device=dev, dtype=F32)
+            gemm(FM, 4 * H, H, _ptr(wms_t), 0, H, _ptr(layers[0][0]), 1, H, _ptr(vt), 4 * H, device=dev)
+            dyx = torch.empty(T, B, FM, device=dev, dtype=F32)
         for t in range(T - 1, -1, -1):
             for i in range(nl - 1, -1, -1):
-                cell = (_ptr(gs[i], t * slab), _ptr(G[i], t * gslab), _ptr(C[i], t * slab), _ptr(dG[i], t * gslab),
-                        _stream())
+                cell = (_ptr(gs[i], t * slab), _ptr(G[i], t * gslab), _ptr(C[i], t * slab), _ptr(dG[i], t * gslab))
                 if i == nl - 1:
+                    nxt = t + 1 < T
                     _lib.check(lib.mrg_ssd_ffn_bwd(
-                        B, H, HB, FO, t, _ptr(dy, t * FO), T * FO, _ptr(dX[0], (t + 1) * slab) if t + 1 < T else None,
+                        B, H, HB, FO, t, _ptr(dy, t * FO), T * FO,
+                        _ptr(dX[0], (t + 1) * slab) if (nxt and not ext) else None,
+                        _ptr(dyx, (t + 1) * B * FM) if (nxt and ext) else None,
                         _ptr(wms_t), _ptr(mask), _ptr(w1), _ptr(w2), _ptr(b1), _ptr(v), _ptr(Z, t * zslab),
                         _ptr(dyt, t * B * FO), _ptr(dz, t * zslab), _ptr(duL, t * slab), _ptr(Hs[i], t * slab),
-                        _ptr(X[i], t * slab), _ptr(lw), _ptr(stats[i][0], t * B), _ptr(stats[i][1], t * B), *cell),
-                        "ssd ffn bwd")
+                        _ptr(X[i], t * slab), _ptr(lw), _ptr(stats[i][0], t * B), _ptr(stats[i][1], t * B), *cell,
+                        _stream()), "ssd ffn bwd")
                 else:
+                    bottom = ext and i == 0
                     _lib.check(lib.mrg_ssd_ln_cell_bwd(
                         B, H, _ptr(dX[i + 1], t * slab), _ptr(Hs[i], t * slab), _ptr(X[i], t * slab),
-                        _ptr(layers[i][4]), _ptr(stats[i][0], t * B), _ptr(stats[i][1], t * B), *cell),
-                        "ssd ln/cell bwd")
+                        _ptr(layers[i][4]), _ptr(stats[i][0], t * B), _ptr(stats[i][1], t * B), *cell, FM,
+                        _ptr(vt) if bottom else None, _ptr(wms_t) if bottom else None,
+                        _ptr(dyx, t * B * FM) if bottom else None, _stream()), "ssd ln/cell bwd")
+                    if bottom:
+                        continue
                 # dX = dG W_ih + g (g: the LayerNorm's residual branch)
                 _lib.check(lib.mrg_ssd_dx(B, H, _ptr(dG[i], t * gslab), _ptr(w_t[i]), _ptr(gs[i], t * slab),
                                           _ptr(dX[i], t * slab), _stream()), "ssd dx")
+        if ext:  # every frame's dfeat = dG0 W_ih0 + g0 in one GEMM
+            gemm(T * B, H, 4 * H, _ptr(dG[0]), 0, 4 * H, _ptr(layers[0][0]), 0, H, _ptr(dX[0]), H, epi=3,
+                 aux=_ptr(gs[0]), ldaux=H, device=dev)
         # weight gradients over all T * B rows
         for i, (w_ih, w_hh, b_ih, b_hh, lw, lb) in enumerate(layers):
             _wgrad(_ptr(dG[i]), 4 * H, _ptr(X[i]), H, rows, 4 * H, H, _gbuf(w_ih), dev, gb=_gbuf(b_ih),

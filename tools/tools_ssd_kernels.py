@@ -77,10 +77,14 @@ def main():
     out["ssd_y_fwd"] = timed(lambda: lib.mrg_ssd_y_fwd(B, HB, FO, P(z), P(w2), P(b2), P(yb), T * FO, S()))
     v = r(HB, 2)
     out["ssd_ffn_bwd"] = timed(lambda: lib.mrg_ssd_ffn_bwd(
-        B, H, HB, FO, 1, P(dy), T * FO, P(dfn), P(wms_t), P(mask), P(w1), P(w2), P(b1), P(v), P(z), P(dyt), P(dz),
+        B, H, HB, FO, 1, P(dy), T * FO, P(dfn), None, P(wms_t), P(mask), P(w1), P(w2), P(b1), P(v), P(z), P(dyt), P(dz),
         P(duo), P(hp), P(rp), P(gm), P(mean), P(rstd), P(g), P(gates), P(c), P(dG), S()))
     out["ssd_ln_cell_bwd"] = timed(lambda: lib.mrg_ssd_ln_cell_bwd(
-        B, H, P(du), P(hp), P(rp), P(gm), P(mean), P(rstd), P(g), P(gates), P(c), P(dG), S()))
+        B, H, P(du), P(hp), P(rp), P(gm), P(mean), P(rstd), P(g), P(gates), P(c), P(dG), FM, None, None, None, S()))
+    vt, dyxb = r(FM, 4 * H), r(B, FM)
+    out["ssd_ln_cell_bwd + dyx"] = timed(lambda: lib.mrg_ssd_ln_cell_bwd(
+        B, H, P(du), P(hp), P(rp), P(gm), P(mean), P(rstd), P(g), P(gates), P(c), P(dG), FM, P(vt), P(wms_t),
+        P(dyxb), S()))
     out["ssd_dx"] = timed(lambda: lib.mrg_ssd_dx(B, H, P(dG), P(w_t), P(g), P(dX), S()))
     out["dX gemm rows TB=1 (W_ih^T)"] = timed(lambda: Fn.gemm(B, H, 4 * H, P(dG), 0, 4 * H, P(w_t), 1, 4 * H, P(dX), H,
                                                            epi=3, aux=P(g), ldaux=H, device=dev))
