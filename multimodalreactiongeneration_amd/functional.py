@@ -1115,11 +1115,84 @@ class _MHAFn(Function):
         return None, dq_in, dkv_in, None, None, None, None, None, None, None, None
 
 
+class _MHAOneKeyFn(Function):
+    """nn.MultiheadAttention when every query sees exactly one key (Tq = Tk = 1: a frame of the
+    generation loops attending to one partner / audio frame, lstmformer.py:498-521).  Softmax over a
+    single visible key is exactly 1, so the attention output IS the value projection (bitwise the
+    SDPA result: P = exp(s - s) / 1 = 1, O = 1 * V); the query / key projections and the attention
+    kernel are skipped.  A row the mask rules hide entirely (query AND key padding) is NaN, as the
+    softmax over an all -inf row is.  Gradients: dV = dO; the query and key projections get none
+    (the reference's dS = P (dP - rowsum(dO O)) is 0 up to rounding there)."""
+
+    @staticmethod
+    @_keeps_precision
+    def forward(ctx, eps, q_in, kv_in, in_w, in_b, out_w, out_b, qpad, kpad, gamma=None, beta=None):
+        _lib.require_device(q_in)
+        dev = q_in.device
+        B, _, E = q_in.shape
+        q2 = q_in.reshape(B, E).contiguous()
+        kv2 = kv_in.reshape(B, E).contiguous()
+        V = torch.empty(B, E, device=dev, dtype=torch.float32)
+        gemm(B, E, E, _ptr(kv2), 0, E, _ptr(in_w, 2 * E * E), 1, E, _ptr(V), E, bias=_ptr(in_b, 2 * E), device=dev)
+        hide = None
+        O = V
+        if qpad is not None and kpad is not None:
+            hide = (qpad.reshape(B, 1) & kpad.reshape(B, 1)).bool()
+            O = torch.where(hide, torch.full_like(V, float("nan")), V)
+        out = torch.empty(B, E, device=dev, dtype=torch.float32)
+        gemm(B, E, E, _ptr(O), 0, E, _ptr(out_w), 1, E, _ptr(out), E, bias=_ptr(out_b), device=dev)
+        res = out
+        extra = []
+        if eps is not None:
+            u, mean, rstd = _resln_fwd(out, q2, gamma, beta, eps)
+            res = u
+            extra = [out, gamma, beta, mean, rstd]
+        ctx.save_for_backward(q2, kv2, O, in_w, in_b, out_w, out_b, *extra)
+        ctx.hide = hide
+        ctx.resln = eps is not None
+        return res.view(B, 1, E)
+
+    @staticmethod
+    @_keeps_precision
+    def backward(ctx, dout):
+        saved = ctx.saved_tensors
+        q2, kv2, O, in_w, in_b, out_w, out_b = saved[:7]
+        B, E = q2.shape
+        dev = dout.device
+        g = None
+        if ctx.resln:
+            out, gamma, beta, mean, rstd = saved[7:]
+            g = _resln_bwd(dout.reshape(B, E).contiguous(), out, q2, gamma, beta, mean, rstd)
+            do2 = g
+        else:
+            do2 = dout.reshape(B, E).contiguous()
+        dO = torch.empty(B, E, device=dev, dtype=torch.float32)
+        gemm(B, E, E, _ptr(do2), 0, E, _ptr(out_w), 0, E, _ptr(dO), E, device=dev)
+        _wgrad(_ptr(do2), E, _ptr(O), E, B, E, E, _gbuf(out_w), dev, gb=_gbuf(out_b), keep=(do2, O))
+        if ctx.hide is not None:  # hidden rows: O is the constant NaN, nothing flows to V
+            dO = torch.where(ctx.hide, torch.zeros_like(dO), dO)
+        gw, gb = _gbuf(in_w), _gbuf(in_b)
+        _wgrad(_ptr(dO), E, _ptr(kv2), E, B, E, E, None if gw is None else gw[2 * E:], dev,
+               gb=None if gb is None else gb[2 * E:], keep=(dO, kv2))
+        dkv = None
+        if ctx.needs_input_grad[2]:
+            dkv = torch.empty(B, 1, E, device=dev, dtype=torch.float32)
+            gemm(B, E, E, _ptr(dO), 0, E, _ptr(in_w, 2 * E * E), 0, E, _ptr(dkv), E, device=dev)
+        dq = g.view(B, 1, E) if (g is not None and ctx.needs_input_grad[1]) else None
+        return None, dq, dkv, None, None, None, None, None, None, None, None
+
+
+def _one_key(q, kv):
+    return q.dim() == 3 and q.shape[1] == 1 and kv.shape[1] == 1 and kv.shape[-1] == q.shape[-1]
+
+
 def mha(q, kv, in_proj_weight, in_proj_bias, out_weight, out_bias, heads, causal=False,
         qpad=None, kpad=None):
     """nn.MultiheadAttention(batch_first, kdim=vdim=E)(q, kv, kv) with the reference mask rules."""
     if in_proj_weight.shape[0] != 3 * q.shape[-1]:
         raise ValueError("in_proj_weight must be [3E, E]")
+    if _one_key(q, kv):
+        return _MHAOneKeyFn.apply(None, q, kv, in_proj_weight, in_proj_bias, out_weight, out_bias, qpad, kpad)
     return _MHAFn.apply((heads, bool(causal), None), q, kv, in_proj_weight, in_proj_bias, out_weight,
                         out_bias, qpad, kpad)
 
@@ -1130,6 +1203,9 @@ def mha_residual_layernorm(q, kv, in_proj_weight, in_proj_bias, out_weight, out_
     projection's input-gradient GEMM takes the residual gradient in its epilogue."""
     if in_proj_weight.shape[0] != 3 * q.shape[-1]:
         raise ValueError("in_proj_weight must be [3E, E]")
+    if _one_key(q, kv):
+        return _MHAOneKeyFn.apply(float(eps), q, kv, in_proj_weight, in_proj_bias, out_weight, out_bias, qpad, kpad,
+                                  gamma, beta)
     return _MHAFn.apply((heads, bool(causal), float(eps)), q, kv, in_proj_weight, in_proj_bias, out_weight,
                         out_bias, qpad, kpad, gamma, beta)
 
