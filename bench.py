@@ -32,7 +32,7 @@ METRIC = "training frames/sec/GPU, lstmformer T=300 B=64; 1→8 GPU scaling"
 FP32_MFMA_PEAK_TF = 157.3   # MI355X_MICROARCH.md chip table (f32 matrix, dense)
 BF16_MFMA_PEAK_TF = 2500.0  # MI355X_MICROARCH.md chip table (bf16 matrix, dense)
 HBM_PEAK_GBS = 8000.0
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_pmc_summary.json")
 
 # probe name (functional._probe) -> kernels it brackets; FLOPs are algorithmic
 FAMILIES = {
@@ -88,6 +88,8 @@ def parse():
     ap.add_argument("--secondary", type=int, default=1, help="time the other 1-GPU BASELINE configs (N=1 only)")
     ap.add_argument("--wgrad-stream", type=int, default=1,
                     help="weight-gradient GEMMs on a side stream (functional._side); 0 = one stream")
+    ap.add_argument("--comm", default="torch", choices=["torch", "native"],
+                    help="N>1 gradient all-reduce: torch.distributed (RCCL) or libmrg's mrg_comm_* RCCL communicator")
     ap.add_argument("--lstm-group", type=int, default=0, help="workgroups per LSTM row group at H=256 (8|16; 0 = library default)")
     return ap.parse_args()
 
@@ -428,7 +430,7 @@ def main():
     from multimodalreactiongeneration_amd import configs as C
     from multimodalreactiongeneration_amd import functional as Fn
     from multimodalreactiongeneration_amd.graphs import capture
-    from multimodalreactiongeneration_amd.ddp import init_from_env, broadcast_parameters, GradReducer
+    from multimodalreactiongeneration_amd.ddp import init_from_env, broadcast_parameters, GradReducer, NativeComm
     from multimodalreactiongeneration_amd.model import Metaformer
     from multimodalreactiongeneration_amd.synthetic import make_batch
 
@@ -445,7 +447,8 @@ def main():
     model = Metaformer(mc, oc, me).to(dev)
     broadcast_parameters(model)
     opt = model.configure_optimizers()["optimizer"]
-    reducer = GradReducer(opt.flat_grad)
+    comm = NativeComm() if (args.comm == "native" and world > 1) else None
+    reducer = GradReducer(opt.flat_grad, comm=comm)
     batch = make_batch(B=args.batch, T=args.seq, ratio=args.ratio, seed=1234 + rank, device=dev)
 
     def fwd_bwd():
@@ -522,6 +525,8 @@ def main():
                    "model": "lstmformer H=256 blocks=5 enc_layers=5 heads=4 bottleneck=64 (13,052,678 params)",
                    "global_batch": args.batch * world, "seq_len": args.seq, "audio_ratio": args.ratio,
                    "parallelism": f"dp{world}", "hip_graph": bool(args.graph),
+                   "allreduce": ("mrg_comm (libmrg RCCL)" if comm is not None else "torch.distributed RCCL")
+                   if world > 1 else None,
                    "wgrad_side_stream": bool(args.wgrad_stream)},
         "whole_step_roofline": {"bound": "mfma", "algorithmic_tflop_per_step": round(step_flop / 1e12, 4),
                                 "achieved_tflops": round(step_flop / (ms / 1000.0) / 1e12, 3),
@@ -542,6 +547,8 @@ def main():
         out["speedup_vs_cpu_baseline"] = round(out["value"] / out["cpu_baseline"]["value"], 1)
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
 

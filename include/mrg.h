@@ -332,6 +332,23 @@ int mrg_feature_delta(int nclip, int T, int C, const float* x, long ldx, int ord
 int mrg_pad_sequences(int B, int Tmax, int F, const float* const* seqs, const int* lens, float pad,
                       float* out, hipStream_t stream);
 
+/* ---------------------------------------------------------------- RCCL gradient exchange
+ * The data-parallel step's one exchange: Lightning `strategy: ddp`
+ * (mr_gen/model/lstmformer/config.yaml:127) averages the gradients across ranks after backward;
+ * here an in-place fp32 all-reduce of spans of the flat gradient buffer over RCCL (xGMI).
+ * librccl.so.1 is resolved at run time (the copy torch already mapped); mrg_comm_available()
+ * says whether one was found.  Rank 0 calls mrg_comm_unique_id, the host moves the
+ * mrg_comm_id_bytes() bytes to every rank, each rank (its GPU already selected) calls
+ * mrg_comm_init.  mrg_comm_allreduce_f32 issues the spans [offsets[i], offsets[i] + counts[i])
+ * of buf as one RCCL group on `stream`; op 0 = sum, 1 = mean.                               */
+int mrg_comm_available(void);
+size_t mrg_comm_id_bytes(void);
+int mrg_comm_unique_id(void* id_out);
+int mrg_comm_init(void** comm_out, int nranks, const void* id, int rank);
+int mrg_comm_allreduce_f32(void* comm, float* buf, const long* offsets, const long* counts, int nbuckets,
+                           int op, hipStream_t stream);
+int mrg_comm_destroy(void* comm);
+
 #ifdef __cplusplus
 }
 #endif

@@ -108,6 +108,12 @@ SIGNATURES = {
     "mrg_ssd_ln_cell_bwd": (c_int, [c_int, c_int, P, P, P, P, P, P, P, P, P, P, c_int, P, P, P, P]),
     "mrg_adamw_step": (c_int, [P, P, P, P, c_long, P, c_float, c_float, c_float, c_float, P, P]),
     "mrg_lstm_debug_inject": (c_int, [c_int]),
+    "mrg_comm_available": (c_int, []),
+    "mrg_comm_id_bytes": (c_size, []),
+    "mrg_comm_unique_id": (c_int, [P]),
+    "mrg_comm_init": (c_int, [ctypes.POINTER(ctypes.c_void_p), c_int, P, c_int]),
+    "mrg_comm_allreduce_f32": (c_int, [P, P, PL, PL, c_int, c_int, P]),
+    "mrg_comm_destroy": (c_int, [P]),
 }
 
 _lock = threading.Lock()

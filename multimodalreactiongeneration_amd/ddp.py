@@ -47,13 +47,66 @@ def broadcast_parameters(module: torch.nn.Module, src: int = 0):
             dist.broadcast(p.data, src)
 
 
+class NativeComm:
+    """An RCCL communicator owned by libmrg's C-ABI (``mrg_comm_*``, include/mrg.h).
+
+    The 128-byte unique id made by rank 0 travels to the other ranks over torch.distributed
+    (any backend: it is host bytes); each rank must have selected its GPU first.  ``allreduce``
+    issues the given spans of a flat fp32 buffer as one RCCL group on the caller's current
+    stream (op "mean" = ncclAvg, the DDP gradient mean; "sum").
+    """
+
+    def __init__(self, rank: int = None, world: int = None):
+        import ctypes
+        from . import _lib
+        self._lib = _lib.load()
+        if not self._lib.mrg_comm_available():
+            raise RuntimeError("NativeComm: no librccl.so.1 in this process")
+        self.rank = dist.get_rank() if rank is None else rank
+        self.world = dist.get_world_size() if world is None else world
+        nbytes = self._lib.mrg_comm_id_bytes()
+        uid = (ctypes.c_char * nbytes)()
+        if self.rank == 0:
+            _lib.check(self._lib.mrg_comm_unique_id(uid), "mrg_comm_unique_id")
+        if self.world > 1:
+            obj = [bytes(uid)]
+            dist.broadcast_object_list(obj, src=0)
+            ctypes.memmove(uid, obj[0], nbytes)
+        self._handle = ctypes.c_void_p()
+        _lib.check(self._lib.mrg_comm_init(ctypes.byref(self._handle), self.world, uid, self.rank), "mrg_comm_init")
+
+    def allreduce(self, buf: torch.Tensor, spans=None, op: str = "mean"):
+        import ctypes
+        from . import _lib
+        _lib.require_device(buf)
+        if buf.dtype != torch.float32 or not buf.is_contiguous():
+            raise ValueError("NativeComm.allreduce: contiguous float32 buffer required")
+        spans = [(0, buf.numel())] if spans is None else list(spans)
+        offs = (ctypes.c_long * len(spans))(*[s for s, _ in spans])
+        cnts = (ctypes.c_long * len(spans))(*[e - s for s, e in spans])
+        stream = torch.cuda.current_stream(buf.device).cuda_stream
+        _lib.check(self._lib.mrg_comm_allreduce_f32(self._handle, ctypes.c_void_p(buf.data_ptr()), offs, cnts,
+                                                    len(spans), 1 if op == "mean" else 0,
+                                                    ctypes.c_void_p(stream)), "mrg_comm_allreduce_f32")
+
+    def close(self):
+        if getattr(self, "_handle", None) is not None and self._handle.value:
+            from . import _lib
+            _lib.check(self._lib.mrg_comm_destroy(self._handle), "mrg_comm_destroy")
+            self._handle = None
+
+
 class GradReducer:
-    """Average a flat gradient buffer across ranks, in buckets, on a side stream."""
+    """Average a flat gradient buffer across ranks, in buckets, on a side stream.
+
+    ``comm``: None = torch.distributed (backend "nccl" is RCCL), or a ``NativeComm`` (libmrg's
+    own RCCL communicator, the ``mrg_comm_*`` C-ABI)."""
 
     def __init__(self, flat_grad: torch.Tensor, bucket_elems: int = 0, params=None, overlap: bool = False,
-                 bucket_bytes: int = 8 << 20):
+                 bucket_bytes: int = 8 << 20, comm: "NativeComm" = None):
         self.flat_grad = flat_grad
-        self.world = dist.get_world_size() if dist.is_initialized() else 1
+        self.comm = comm
+        self.world = comm.world if comm is not None else (dist.get_world_size() if dist.is_initialized() else 1)
         self.backend = dist.get_backend() if dist.is_initialized() else None
         n = flat_grad.numel()
         self.overlap = bool(overlap) and params is not None and self.world > 1
@@ -147,6 +200,9 @@ class GradReducer:
             if side is not None:
                 self.stream.wait_stream(side)
             with torch.cuda.stream(self.stream):
+                if self.comm is not None:
+                    self.comm.allreduce(self.flat_grad, [(s, e)], "mean")
+                    return
                 dist.all_reduce(self.flat_grad[s:e], op=op)
                 if scale != 1.0:
                     self.flat_grad[s:e].mul_(scale)
@@ -181,6 +237,13 @@ class GradReducer:
         if self.overlap:
             return self.finish()
         op, scale = self._op()
+        if self.comm is not None:
+            cur = torch.cuda.current_stream(self.flat_grad.device)
+            self.stream.wait_stream(cur)
+            with torch.cuda.stream(self.stream):
+                self.comm.allreduce(self.flat_grad, self.buckets, "mean")
+            cur.wait_stream(self.stream)
+            return
         if self.stream is not None:
             cur = torch.cuda.current_stream(self.flat_grad.device)
             self.stream.wait_stream(cur)

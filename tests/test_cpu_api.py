@@ -179,3 +179,13 @@ def test_ctypes_signatures_match_header_arity():
         assert m, name
         params = [x for x in m.group(1).split(",") if x.strip() and x.strip() != "void"]
         assert len(params) == len(args), (name, len(params), len(args))
+
+
+def test_comm_entry_points_load_without_a_gpu():
+    """The RCCL C-ABI resolves librccl at run time: the library loads and reports the 128-byte id
+    size with no GPU and no communicator."""
+    from multimodalreactiongeneration_amd import _lib
+    lib = _lib.load()
+    assert lib.mrg_comm_id_bytes() == 128
+    assert lib.mrg_comm_available() in (0, 1)
+    assert lib.mrg_comm_destroy(None) == 0

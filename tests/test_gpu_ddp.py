@@ -70,3 +70,20 @@ def test_two_ranks_overlapped_allreduce_equals_full_batch_gradient():
         off += n
     assert off == g0.size
     assert worst < TOL, worst
+
+
+def test_native_rccl_communicator_one_rank():
+    """libmrg's own RCCL communicator (mrg_comm_* C-ABI) on the box's one GPU: a 1-rank group's mean
+    and sum of bucketed spans leave the buffer bit-identical, spans outside the list untouched."""
+    from multimodalreactiongeneration_amd.ddp import NativeComm
+    torch.cuda.set_device(0)
+    comm = NativeComm(rank=0, world=1)
+    try:
+        x = torch.randn(1 << 20, device="cuda:0")
+        ref = x.clone()
+        comm.allreduce(x, [(0, 1000), (4096, 300000), (600000, 1 << 20)], "mean")
+        comm.allreduce(x, None, "sum")
+        torch.cuda.synchronize()
+        assert torch.equal(x, ref)
+    finally:
+        comm.close()
