@@ -88,6 +88,8 @@ def parse():
     ap.add_argument("--secondary", type=int, default=1, help="time the other 1-GPU BASELINE configs (N=1 only)")
     ap.add_argument("--wgrad-stream", type=int, default=1,
                     help="weight-gradient GEMMs on a side stream (functional._side); 0 = one stream")
+    ap.add_argument("--wgrad-defer", type=int, default=0,
+                    help="queue side-stream weight gradients to run beside the next backward recurrence")
     ap.add_argument("--comm", default="torch", choices=["torch", "native"],
                     help="N>1 gradient all-reduce: torch.distributed (RCCL) or libmrg's mrg_comm_* RCCL communicator")
     ap.add_argument("--lstm-group", type=int, default=0, help="workgroups per LSTM row group at H=256 (8|16; 0 = library default)")
@@ -443,6 +445,7 @@ def main():
         from multimodalreactiongeneration_amd import _lib
         _lib.check(_lib.load().mrg_lstm_config(args.lstm_group), "mrg_lstm_config")
     Fn.set_wgrad_stream(bool(args.wgrad_stream))
+    Fn.set_wgrad_defer(bool(args.wgrad_defer))
     torch.manual_seed(0)
     model = Metaformer(mc, oc, me).to(dev)
     broadcast_parameters(model)
@@ -527,7 +530,8 @@ def main():
                    "parallelism": f"dp{world}", "hip_graph": bool(args.graph),
                    "allreduce": ("mrg_comm (libmrg RCCL)" if comm is not None else "torch.distributed RCCL")
                    if world > 1 else None,
-                   "wgrad_side_stream": bool(args.wgrad_stream)},
+                   "wgrad_side_stream": bool(args.wgrad_stream),
+                   "wgrad_beside_recurrence": bool(args.wgrad_stream and args.wgrad_defer)},
         "whole_step_roofline": {"bound": "mfma", "algorithmic_tflop_per_step": round(step_flop / 1e12, 4),
                                 "achieved_tflops": round(step_flop / (ms / 1000.0) / 1e12, 3),
                                 "peak": FP32_MFMA_PEAK_TF,

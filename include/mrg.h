@@ -48,6 +48,18 @@ size_t mrg_gemm_workspace_bytes(int M, int N, int splits);
  * 0 = exact f32 MFMA (a k-ordered fmaf chain).  Env MRG_GEMM_EXACT=1 -> 0.  */
 int mrg_gemm_set_mode(int mode);
 int mrg_gemm_get_mode(void);
+/* Cap on resident blocks per CU of the following GEMM launches (0 = HW occupancy); returns the
+ * previous cap.  Host-side state read at launch (and graph-capture) time.                       */
+int mrg_gemm_set_blocks_per_cu(int n);
+/* LDS-DMA pipelined x6 kernel for k-contiguous products (transA 0, transB 1, K % 32 == 0, unsplit,
+ * >= 2048 rows, >= 256 columns): ring depth 2..4 (0 = off; default 2, MRG_GEMM_GLDS) and column
+ * tile (64 forces 64-wide tiles, 128 = by shape).                                               */
+int mrg_gemm_set_glds(int depth, int bn);
+/* dst_i [cols_i][rows_i] = src_i [rows_i][cols_i]^T for n row-major fp32 matrices (host arrays of
+ * device pointers and sizes), one launch per 32 matrices: the [in][out] weight copies that let the
+ * input-gradient products dY W run k-contiguous (nn.Linear / LSTM backward, mixer_block.py:63-74).*/
+int mrg_transpose_batched(int n, const float* const* src, float* const* dst, const int* rows, const int* cols,
+                          hipStream_t stream);
 /* Tuning only: force the tile shape (0: 128x128, 1: 128x64, 2: 64x64), -1 = heuristic. */
 int mrg_gemm_force_tile(int tile);
 /* Tuning only: structural variants of the x6 kernel (0 product, 1 split + one MFMA, 2 plane-0 +
@@ -133,6 +145,9 @@ int mrg_lstm_debug_inject(int mode);
 /* Tuning knob: number of workgroups that share one batch row group at H = 256
  * (8 or 16; default 8).  Process-wide; set before capture, not during. */
 int mrg_lstm_config(int group256);
+/* Backward recurrences pick the smallest batch tile whose grid fits n workgroups per CU (0 = HW
+ * occupancy), leaving CU room for weight-gradient GEMMs issued beside them; returns the old cap. */
+int mrg_lstm_set_blocks_per_cu(int n);
 /* Single-step cell (T = 1), e.g. the per-frame decode of lstm_with_sampling's scheduled-sampling
  * training (lstm_with_sample.py:410-433): pre [B, 4H] = x W_ih^T + b_ih (+ h0 W_hh^T) from the
  * GEMMs; fwd adds b_hh and writes gates [B, 4H], c [B, H], h (row stride h_ld) and a dense copy

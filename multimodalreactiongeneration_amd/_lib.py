@@ -34,6 +34,10 @@ SIGNATURES = {
     "mrg_gemm_set_mode": (c_int, [c_int]),
     "mrg_gemm_get_mode": (c_int, []),
     "mrg_gemm_force_tile": (c_int, [c_int]),
+    "mrg_gemm_set_blocks_per_cu": (c_int, [c_int]),
+    "mrg_gemm_set_glds": (c_int, [c_int, c_int]),
+    "mrg_transpose_batched": (c_int, [c_int, PP, PP, PI, PI, P]),
+    "mrg_lstm_set_blocks_per_cu": (c_int, [c_int]),
     "mrg_gemm_x6_variant": (c_int, [c_int, c_int, c_int, c_int, P, P, P, P]),
     "mrg_gemm_f32": (c_int, [c_int, c_int, c_int, c_float,
                              P, c_int, c_long, c_long, c_int,

@@ -188,6 +188,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   const bool qp = pad && qi < a.Tq && a.qpad[(long)b * a.Tq + qi];
   const int kmax = key_bound(a, qi);                    // this lane's query
   const int wmin = key_bound(a, q0 + wave * 16);        // smallest bound in the wave (monotone in i)
+  const int wlim = key_bound(a, q0 + wave * 16 + 15);   // largest: sub-tiles from here on are masked
 
   float qreg[C::KS];
 #pragma unroll
@@ -220,8 +221,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
     for (int sp = 0; sp < TT / 16; sp += 2) {
       const int kb = k0 + sp * 16;
-      if (kb >= klim) break;
-      const bool two = kb + 16 < klim;  // wave-uniform: the second sub-tile has visible keys
+      if (kb >= wlim) break;            // every query of this wave masks these keys (no contribution)
+      const bool two = kb + 16 < wlim;  // wave-uniform: the second sub-tile has visible keys
       f32x4 s4[2];
       s4[0] = qk16<D>(Ks, sp * 16, qreg, lq, lg);
       s4[1] = two ? qk16<D>(Ks, sp * 16 + 16, qreg, lq, lg) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -308,6 +309,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
   const bool qp = pad && qv && a.qpad[(long)b * a.Tq + qi];
   const int kmax = key_bound(a, qi);
   const int wmin = key_bound(a, q0 + wave * 16);
+  const int wlim = key_bound(a, q0 + wave * 16 + 15);  // sub-tiles from here on: dS = 0 for the wave
   float qreg[C::KS], dreg[C::KS];
   float dsum = 0.0f;
 #pragma unroll
@@ -346,7 +348,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
     for (int sub = 0; sub < TT / 16; ++sub) {
       const int kb = k0 + sub * 16;
-      if (kb >= klim) break;
+      if (kb >= wlim) break;
       f32x4 s4 = f32x4{0.f, 0.f, 0.f, 0.f};
       f32x4 dp4 = f32x4{0.f, 0.f, 0.f, 0.f};
       {
@@ -410,6 +412,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
   const bool kp = pad && kv && a.kpad[(long)b * a.Tk + kj];
   const int qmin = query_start(a, kj);                       // first query seeing this lane's key
   const int wmax = query_start(a, min(kb0 + wave * 16 + 15, a.Tk - 1));  // largest in the wave
+  const int wq0 = query_start(a, min(kb0 + wave * 16, a.Tk - 1));        // smallest in the wave
   float kreg[C::KS], vreg[C::KS];
 #pragma unroll
   for (int s = 0; s < C::KS; ++s) {
@@ -450,6 +453,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
     for (int sub = 0; sub < TT / 16; ++sub) {
       const int qb = qt0 + sub * 16;
       if (qb >= a.Tq) break;
+      if (qb + 16 <= wq0) continue;  // no query of this sub-tile sees a key of this wave (P = dS = 0)
       f32x4 s4 = f32x4{0.f, 0.f, 0.f, 0.f};
       f32x4 dp4 = f32x4{0.f, 0.f, 0.f, 0.f};
       {

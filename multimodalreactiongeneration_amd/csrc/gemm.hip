@@ -15,101 +15,10 @@
 // the per-lane fragment reads (lane -> row l&31, k-pair l>>5) are
 // bank-conflict free; global loads for the next K tile are issued before the
 // MFMAs of the current one (register prefetch).
-#include "mrg_common.h"
+#include "gemm_common.h"
 #include <cstdlib>
 
 namespace mrg {
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-struct GemmArgs {
-  int M, N, K;
-  float alpha, beta;
-  const float* A;
-  RowMap amap;
-  int transA;
-  const float* B;
-  RowMap bmap;
-  int transB;
-  float* C;
-  long ldc;
-  const float* bias;
-  int epi;  // 0 none, 1 relu, 2 multiply by (aux > 0), 3 add aux (residual gradient)
-  const float* aux;
-  long ldaux;
-  float* ws;  // split-K slabs [splits][M][N] (nullptr when splits == 1)
-  int kchunk;
-  int tiles_n, tiles_mn, ntiles;  // output tiles (x splits), walked by a persistent grid
-  int nsplit;                     // K slices per tile (ntiles / tiles_mn)
-  // in-launch split-K combine (x6 path, small outputs): per-tile tickets, zero between launches;
-  // null -> the slabs are reduced by splitk_reduce*_kernel
-  unsigned* cnt;
-  int vec;                        // C / bias / aux / slab rows 16-B aligned: vector epilogue
-  // fused row sums of op(A) (bias gradients of a weight-gradient GEMM, TA = 1, x6 path):
-  // per-(split, m) partials in asum [splits][M], reduced in a fixed order into
-  // asum_out[m] = asum_beta * asum_out[m] + sum (and asum_out2, nullable)
-  float* asum;
-  float* asum_out;
-  float* asum_out2;
-  float asum_beta;
-  // few-row kernel: byte extent of A and B from their base pointers (buffer-load range checks)
-  int a_bytes, b_bytes;
-};
-
-#ifndef MRG_GEMM_COUNTERS
-#define MRG_GEMM_COUNTERS 4096  // tickets the caller provides (include/mrg.h)
-#endif
-
-static constexpr int BK = 32;  // K tile (64 measured no faster here: 2 blocks/CU instead of 3)
-static constexpr int NT = 256;
-
-__device__ __forceinline__ float apply_epi(const GemmArgs& a, float v, int m, int n) {
-  v *= a.alpha;
-  if (a.beta != 0.0f) v += a.beta * a.C[(long)m * a.ldc + n];
-  if (a.bias) v += a.bias[n];
-  if (a.epi == 1) v = fmaxf(v, 0.0f);
-  else if (a.epi == 2) v = (a.aux[(long)m * a.ldaux + n] > 0.0f) ? v : 0.0f;
-  else if (a.epi == 3) v += a.aux[(long)m * a.ldaux + n];
-  return v;
-}
-
-// C[m, n..n+3] (or the split-K slab row) from four accumulators: one 16-B access per operand when
-// the rows are 16-B aligned (a.vec), element-wise at the N edge or for unaligned operands.
-__device__ __forceinline__ void store4(const GemmArgs& a, int z, int m, int n, float4 v) {
-  if (a.ws) {
-    float* p = a.ws + ((long)z * a.M + m) * a.N + n;
-    if (a.vec && n + 3 < a.N) { *reinterpret_cast<float4*>(p) = v; return; }
-    const float e[4] = {v.x, v.y, v.z, v.w};
-    for (int q = 0; q < 4 && n + q < a.N; ++q) p[q] = e[q];
-    return;
-  }
-  if (a.vec && n + 3 < a.N) {
-    float* pc = a.C + (long)m * a.ldc + n;
-    float4 o = make_float4(v.x * a.alpha, v.y * a.alpha, v.z * a.alpha, v.w * a.alpha);
-    if (a.beta != 0.0f) {
-      const float4 c = *reinterpret_cast<const float4*>(pc);
-      o.x += a.beta * c.x; o.y += a.beta * c.y; o.z += a.beta * c.z; o.w += a.beta * c.w;
-    }
-    if (a.bias) {
-      const float4 b = *reinterpret_cast<const float4*>(a.bias + n);
-      o.x += b.x; o.y += b.y; o.z += b.z; o.w += b.w;
-    }
-    if (a.epi == 1) {
-      o.x = fmaxf(o.x, 0.0f); o.y = fmaxf(o.y, 0.0f); o.z = fmaxf(o.z, 0.0f); o.w = fmaxf(o.w, 0.0f);
-    } else if (a.epi == 2) {
-      const float4 x = *reinterpret_cast<const float4*>(a.aux + (long)m * a.ldaux + n);
-      o.x = x.x > 0.0f ? o.x : 0.0f; o.y = x.y > 0.0f ? o.y : 0.0f;
-      o.z = x.z > 0.0f ? o.z : 0.0f; o.w = x.w > 0.0f ? o.w : 0.0f;
-    } else if (a.epi == 3) {
-      const float4 x = *reinterpret_cast<const float4*>(a.aux + (long)m * a.ldaux + n);
-      o.x += x.x; o.y += x.y; o.z += x.z; o.w += x.w;
-    }
-    *reinterpret_cast<float4*>(pc) = o;
-    return;
-  }
-  const float e[4] = {v.x, v.y, v.z, v.w};
-  for (int q = 0; q < 4 && n + q < a.N; ++q) a.C[(long)m * a.ldc + n + q] = apply_epi(a, e[q], m, n + q);
-}
 
 // One operand tile (rows of the MFMA M or N dimension x BK) staged k-major in LDS:
 // S[k][x], x = m (or n).  TR says which index is contiguous in memory:
@@ -301,32 +210,6 @@ __device__ __forceinline__ int x6_off(int x, int c) {
 }
 
 
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-
-// two floats -> packed bf16 pair (RNE), one v_cvt_pk_bf16_f32
-__device__ __forceinline__ unsigned pk_bf16(float a, float b) {
-  const f32x2 v = {a, b};
-  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2));
-}
-
-// two values -> three planes of 2 bf16: 3 cvt_pk + 2 x (and, shift, packed sub) per pair
-__device__ __forceinline__ void split2(float a, float b, unsigned& p0, unsigned& p1, unsigned& p2) {
-  p0 = pk_bf16(a, b);
-  a -= __uint_as_float(p0 << 16);
-  b -= __uint_as_float(p0 & 0xffff0000u);
-  p1 = pk_bf16(a, b);
-  a -= __uint_as_float(p1 << 16);
-  b -= __uint_as_float(p1 & 0xffff0000u);
-  p2 = pk_bf16(a, b);
-}
-
-// four consecutive-k values -> three planes of 4 bf16 (8 B each)
-__device__ __forceinline__ void split4(float v0, float v1, float v2, float v3, uint2& p0, uint2& p1, uint2& p2) {
-  split2(v0, v1, p0.x, p1.x, p2.x);
-  split2(v2, v3, p0.y, p1.y, p2.y);
-}
-
 // One operand tile (X rows of the MFMA M or N dimension x XBK) for the x6 kernel.
 //   TR = 0 : memory row = x, contiguous along k: thread loads float4 (x, 4 k), 8 threads per row
 //   TR = 1 : memory row = k, contiguous along x: thread loads a 4 k x 4 x block (4 float4) and
@@ -432,7 +315,6 @@ struct TileX6 {
   }
 };
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 // In-launch split-K combine (cdna_hip_programming.md, "Projection GEMM at M = 256", item 2):
 // every K slice stores its fp32 slab and draws a ticket for its tile; the workgroup that draws
@@ -665,6 +547,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_x6_kernel(GemmArgs a) {
   }
 }
 
+
 __global__ void splitk_reduce_kernel(GemmArgs a, int splits) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   long total = (long)a.M * a.N;
@@ -793,6 +676,11 @@ __global__ __launch_bounds__(1024) void colsum_final_kernel(const float* part, i
 
 // blocks per CU the hardware admits for a kernel (cached per kernel FUNCTION: every instantiation
 // has the same C++ type, so the cache is keyed by its address), x CUs of the current device
+// Host-side cap on resident blocks per CU for the persistent tile walks (0 = the occupancy the HW
+// reports).  The weight-gradient products issued beside a latency-bound recurrence run with 1, so
+// they take the CU room the recurrence leaves instead of queueing whole waves of tiles ahead of it.
+static int g_blocks_per_cu = 0;
+
 template <typename K>
 static int resident_blocks(K kernel) {
   static const void* keys[256];
@@ -809,6 +697,7 @@ static int resident_blocks(K kernel) {
     per_cu = n;
     if (nkeys < 256) { keys[nkeys] = key; vals[nkeys] = n; ++nkeys; }
   }
+  if (g_blocks_per_cu > 0 && per_cu > g_blocks_per_cu) per_cu = g_blocks_per_cu;
   int dev = 0;
   (void)hipGetDevice(&dev);
   if (dev < 0 || dev >= 16) dev = 0;
@@ -972,6 +861,17 @@ static void launch_rows(const GemmArgs& a, hipStream_t s) {
 }
 
 static int g_tile_override = -1;
+// LDS-DMA x6 kernel for k-contiguous products (gemm_x6g_kernel): 0 = off, else ring depth (2..4);
+// MRG_GEMM_GLDS overrides; g_glds_bn = column tile (128 or 64)
+static int g_glds = [] {
+  const char* e = getenv("MRG_GEMM_GLDS");
+  return e ? atoi(e) : 2;
+}();
+static int g_glds_bn = [] {  // 64 forces 64-wide column tiles (tuning); 128 = by shape
+  const char* e = getenv("MRG_GEMM_GLDS_BN");
+  return e ? atoi(e) : 128;
+}();
+
 
 // GEMM arithmetic: 1 = x6 bf16 split on the bf16 matrix cores (default), 0 = exact f32 MFMA
 static int g_gemm_mode = [] {
@@ -1020,6 +920,46 @@ MRG_API int mrg_gemm_set_mode(int mode) {
   return 0;
 }
 MRG_API int mrg_gemm_get_mode(void) { return g_gemm_mode; }
+
+// LDS-DMA x6 kernel for k-contiguous products: ring depth 2..4 (0 = off) and column tile (64 forces
+// 64-wide tiles; 128 = the shape heuristic).
+MRG_API int mrg_gemm_set_glds(int depth, int bn) {
+  MRG_REQUIRE(depth == 0 || (depth >= 2 && depth <= 4), "mrg_gemm_set_glds: depth must be 0 or 2..4");
+  MRG_REQUIRE(bn == 64 || bn == 128, "mrg_gemm_set_glds: column tile must be 64 or 128");
+  g_glds = depth;
+  g_glds_bn = bn;
+  return 0;
+}
+
+// Cap on resident blocks per CU of the following GEMM launches (0 = none); returns the previous cap.
+// dst_i [cols_i][rows_i] = src_i [rows_i][cols_i]^T for n matrices, one launch per 32 of them.
+MRG_API int mrg_transpose_batched(int n, const float* const* src, float* const* dst, const int* rows, const int* cols,
+                                  hipStream_t stream) {
+  MRG_REQUIRE(n >= 0 && (n == 0 || (src && dst && rows && cols)), "mrg_transpose_batched: bad arguments");
+  for (int b0 = 0; b0 < n; b0 += MRG_TP_MAX) {
+    TransposeBatch tb;
+    memset(&tb, 0, sizeof(tb));
+    tb.n = n - b0 < MRG_TP_MAX ? n - b0 : MRG_TP_MAX;
+    int blocks = 0;
+    for (int i = 0; i < tb.n; ++i) {
+      MRG_REQUIRE(rows[b0 + i] >= 0 && cols[b0 + i] >= 0, "mrg_transpose_batched: negative size");
+      tb.src[i] = src[b0 + i]; tb.dst[i] = dst[b0 + i]; tb.rows[i] = rows[b0 + i]; tb.cols[i] = cols[b0 + i];
+      tb.first[i] = blocks;
+      blocks += ((rows[b0 + i] + 31) / 32) * ((cols[b0 + i] + 31) / 32);
+    }
+    tb.first[tb.n] = blocks;
+    if (blocks == 0) continue;
+    transpose_batched_kernel<<<blocks, 256, 0, stream>>>(tb);
+    if (check_launch("transpose_batched_kernel")) return 1;
+  }
+  return 0;
+}
+
+MRG_API int mrg_gemm_set_blocks_per_cu(int n) {
+  const int prev = g_blocks_per_cu;
+  g_blocks_per_cu = n > 0 ? n : 0;
+  return prev;
+}
 
 // Tuning only: the x6 kernel's structural variants (see gemm_x6_kernel VAR) on C = A B^T,
 // A [M][K], B [N][K] row-major, 128x128 tiles, no split-K.  Results are NOT C for var != 0.
@@ -1119,6 +1059,18 @@ static int gemm_ex(int mode, int M, int N, int K, float alpha,
     a.b_bytes = (int)(b_ext * 4);
     launch_rows(a, stream);
     return check_launch("gemm_rows_kernel");
+  }
+  // LDS-DMA pipelined x6 kernel: k-contiguous A and B, whole 32-deep k-tiles, unsplit
+  // (tile by shape, measured with tools/tools_gemm_bench.py: 128 x 128 for N >= 1024, 64 x 64 for
+  // N = K = 256, else 64 x 128; ring depth 2 = two workgroups per CU)
+  if (mode == 1 && g_glds > 0 && !transA && transB && splits == 1 && !asum_out && K > 0 && (K % 32) == 0 && va &&
+      vb && M >= 2048 && N >= 256) {
+    int bm = 64, bn = 128;
+    if (N >= 1024) bm = 128;
+    else if (N == 256 && K <= 256) bn = 64;
+    if (g_glds_bn == 64) bn = 64;
+    launch_x6g(a, g_glds, bm, bn, stream);
+    return check_launch("gemm_x6g_kernel");
   }
   int tile;  // 0: 128x128, 1: 128x64, 2: 64x64
   if (mx) {

@@ -1,0 +1,249 @@
+// x6 GEMM with LDS-DMA staging (gfx950 global_load_lds_dwordx4): see the comment below.
+#include "gemm_common.h"
+#include <cstdlib>
+
+namespace mrg {
+
+
+// ----------------------------------------------------------------------------------------------
+// x6 GEMM with LDS-DMA staging for k-contiguous operands (transA = 0, transB = 1: X W^T, and dY W
+// through a transposed weight copy).  The register-staged kernel above keeps ONE k-tile of loads
+// in flight per workgroup; on the step's short-K products (K = 256..1024, 300..1200 tiles, about
+// one workgroup per CU) each k-tile then waits out a full HBM round trip (33 us for a
+// 19200 x 256 x 256 product whose MFMA work is ~6 us).  Here the fp32 tiles arrive by
+// global_load_lds_dwordx4 into an NS-deep LDS ring (no VGPRs held by loads in flight), NS - 1
+// k-tiles ahead, and each wave splits its own fragments into the three bf16 planes as it reads
+// them (cdna_hip_programming.md §5, "Async global->LDS copy", "Pipelining across barriers").
+//   ring slot: A [BM rows][32 k] fp32 then B [BN rows][32 k] fp32, 128-B rows in 1-KB groups of 8;
+//   a DMA wave-instruction fills one group lane-linearly: lane L -> row 8g + L/8, 16-B slot L%8,
+//   which holds k-chunk (L%8) ^ f(row), f(row) = (row >> 1) & 7 (source-address swizzle; the
+//   fragment reads apply the same XOR: 16 lanes reading rows r0..r0+15 at one chunk hit 16
+//   distinct 16-B bank groups).
+//   per k-tile: counted s_waitcnt vmcnt (the later stages stay in flight) -> raw s_barrier ->
+//   issue k-tile kt + NS - 1 into the slot read in the previous k-tile -> fragments, split, MFMAs.
+__device__ __forceinline__ int glds_off(int row, int c) {
+  return ((row >> 3) << 10) + ((row & 7) << 7) + ((c ^ ((row >> 1) & 7)) << 4);
+}
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+typedef float f32x4v_ __attribute__((ext_vector_type(4)));
+
+// 16-B LDS read the compiler does not track (see gemm_x6g_kernel); the caller waits lgkmcnt
+__device__ __forceinline__ f32x4v_ lds_read16(unsigned addr) {
+  f32x4v_ v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr) : "memory");
+  return v;
+}
+
+// 8 consecutive-k fp32 -> three bf16x8 planes (v = p0 + p1 + p2 + r, |r| <= 2^-24 |v|)
+__device__ __forceinline__ void split8(f32x4v_ v0, f32x4v_ v1, bf16x8 (&f)[3]) {
+  unsigned a0, a1, a2, b0, b1, b2, c0, c1, c2, d0, d1, d2;
+  split2(v0.x, v0.y, a0, a1, a2);
+  split2(v0.z, v0.w, b0, b1, b2);
+  split2(v1.x, v1.y, c0, c1, c2);
+  split2(v1.z, v1.w, d0, d1, d2);
+  const u32x4 p0 = {a0, b0, c0, d0}, p1 = {a1, b1, c1, d1}, p2 = {a2, b2, c2, d2};
+  f[0] = __builtin_bit_cast(bf16x8, p0);
+  f[1] = __builtin_bit_cast(bf16x8, p1);
+  f[2] = __builtin_bit_cast(bf16x8, p2);
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN, int NS>
+__global__ __launch_bounds__(NT, 1) void gemm_x6g_kernel(GemmArgs a) {
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int SA = BM * 128, SS = SA + BN * 128;  // bytes of one ring slot
+  constexpr int GA = BM / 32, GB = BN / 32;         // DMA wave-instructions per wave per k-tile
+  constexpr int GT = GA + GB;
+  static_assert(NS >= 2 && NS <= 4 && (BM == 64 || BM == 128) && (BN == 64 || BN == 128), "gemm_x6g tile");
+  __shared__ __attribute__((aligned(16))) unsigned char lds[NS * SS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = (wave >> 1) * (BM / 2), wn = (wave & 1) * (BN / 2);
+  const int lr = lane & 31, lh = lane >> 5;
+  // XCD-aware bijective remap: the blocks that share an XCD (b % 8) take consecutive tiles, so the
+  // column tiles of one row block (the same A rows) meet in one L2
+  const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int m0 = (t / a.tiles_n) * BM, n0 = (t % a.tiles_n) * BN;
+  const int nk = a.K / 32;
+
+  const float* src[GT];
+#pragma unroll
+  for (int g = 0; g < GT; ++g) {
+    const bool isa = g < GA;
+    const int row = 8 * (wave * (isa ? GA : GB) + (isa ? g : g - GA)) + (lane >> 3);
+    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+    src[g] = isa ? a.A + a.amap.off(min(m0 + row, a.M - 1)) + 4 * chunk
+                 : a.B + a.bmap.off(min(n0 + row, a.N - 1)) + 4 * chunk;
+  }
+  const unsigned lds_base = (unsigned)(uintptr_t)((__attribute__((address_space(3))) unsigned char*)lds);
+  auto issue = [&](int kt, int slot) {
+#pragma unroll
+    for (int g = 0; g < GT; ++g) {
+      const int grp = g < GA ? wave * GA + g : wave * GB + (g - GA);
+      unsigned char* dst = lds + slot * SS + (g < GA ? 0 : SA) + (grp << 10);
+      __builtin_amdgcn_global_load_lds((const void*)(src[g] + kt * 32),
+                                       (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+#pragma unroll
+  for (int st = 0; st < NS - 1; ++st)
+    if (st < nk) issue(st, st);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int ahead = min(NS - 2, nk - 1 - kt);  // k-tiles issued after kt, left in flight
+    if (ahead >= 2) vm_wait<2 * GT>();
+    else if (ahead == 1) vm_wait<GT>();
+    else vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    if (kt + NS - 1 < nk) issue(kt + NS - 1, (kt + NS - 1) % NS);
+    const unsigned sa = lds_base + (kt % NS) * SS;
+    const unsigned sb = sa + SA;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int c0 = 4 * s + 2 * lh;
+      // fragment reads in inline asm: hipcc would put s_waitcnt vmcnt(0) before any ds_read it
+      // sees while an LDS-DMA is in flight (draining the ring every k-tile); the counted vmcnt and
+      // the barrier above already order these reads after the DMA of this k-tile
+      f32x4v_ ra[TM][2], rb[TN][2];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm + 32 * i + lr;
+        ra[i][0] = lds_read16(sa + glds_off(row, c0));
+        ra[i][1] = lds_read16(sa + glds_off(row, c0 + 1));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn + 32 * j + lr;
+        rb[j][0] = lds_read16(sb + glds_off(row, c0));
+        rb[j][1] = lds_read16(sb + glds_off(row, c0 + 1));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      bf16x8 fa[TM][3], fb[TN][3];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) split8(ra[i][0], ra[i][1], fa[i]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) split8(rb[j][0], rb[j][1], fb[j]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {  // small terms first; (B, A) operand order -> C^T per lane
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][2], fa[i][0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][1], fa[i][1], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][0], fa[i][2], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][1], fa[i][0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][0], fa[i][1], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][0], fa[i][0], acc[i][j], 0, 0, 0);
+        }
+    }
+  }
+  __syncthreads();  // every wave's last fragment reads are done: the ring becomes the epilogue stage
+  if constexpr (BN >= 128) {
+    constexpr int WC = TN * 32, PITCH = WC + 4, C4 = WC / 4;
+    float* stg = reinterpret_cast<float*>(lds) + wave * 32 * PITCH;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4)
+          *reinterpret_cast<float4*>(stg + lr * PITCH + j * 32 + 8 * r4 + 4 * lh) =
+              make_float4(acc[i][j][4 * r4], acc[i][j][4 * r4 + 1], acc[i][j][4 * r4 + 2], acc[i][j][4 * r4 + 3]);
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int it = 0; it < 32 * C4 / 64; ++it) {
+        const int qq = lane + 64 * it, row = qq / C4, c4 = qq % C4;
+        const float4 v = *reinterpret_cast<const float4*>(stg + row * PITCH + 4 * c4);
+        const int m = m0 + wm + i * 32 + row;
+        if (m < a.M) store4(a, 0, m, n0 + wn + 4 * c4, v);
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wm + i * 32 + lr;
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) {
+          const int n = n0 + wn + j * 32 + 8 * r4 + 4 * lh;
+          const float4 v = make_float4(acc[i][j][4 * r4], acc[i][j][4 * r4 + 1], acc[i][j][4 * r4 + 2],
+                                       acc[i][j][4 * r4 + 3]);
+          if (m < a.M) store4(a, 0, m, n, v);
+        }
+    }
+  }
+}
+
+template <int BM, int BN>
+static void launch_tiles(GemmArgs a, int ns, hipStream_t s) {
+  a.tiles_n = (a.N + BN - 1) / BN;
+  a.tiles_mn = a.tiles_n * ((a.M + BM - 1) / BM);
+  a.ntiles = a.tiles_mn;
+  a.nsplit = 1;
+  a.ws = nullptr;
+  const unsigned grid = (unsigned)a.tiles_mn;
+  switch (ns) {
+    case 2: gemm_x6g_kernel<BM, BN, 2><<<grid, NT, 0, s>>>(a); break;
+    case 4: gemm_x6g_kernel<BM, BN, 4><<<grid, NT, 0, s>>>(a); break;
+    default: gemm_x6g_kernel<BM, BN, 3><<<grid, NT, 0, s>>>(a); break;
+  }
+}
+
+void launch_x6g(GemmArgs a, int ns, int bm, int bn, hipStream_t s) {
+  if (bm == 64) {
+    if (bn == 64) launch_tiles<64, 64>(a, ns, s);
+    else launch_tiles<64, 128>(a, ns, s);
+  } else if (bn == 64) {
+    launch_tiles<128, 64>(a, ns, s);
+  } else {
+    launch_tiles<128, 128>(a, ns, s);
+  }
+}
+
+// ----------------------------------------------------------------------------------------------
+// Batched transpose: dst_i [cols_i][rows_i] = src_i [rows_i][cols_i]^T for up to MRG_TP_MAX
+// matrices in one launch (the weights' [in][out] copies that let the input-gradient products
+// dY W run as k-contiguous products on the kernel above).  32 x 32 tiles through LDS.
+__global__ __launch_bounds__(256) void transpose_batched_kernel(TransposeBatch tb) {
+  __shared__ float tile[32][33];
+  int blk = blockIdx.x, i = 0;
+  while (i + 1 < tb.n && blk >= tb.first[i + 1]) ++i;
+  const int local = blk - tb.first[i];
+  const int R = tb.rows[i], C = tb.cols[i];
+  const int tc = (C + 31) / 32;
+  const int r0 = (local / tc) * 32, c0 = (local % tc) * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const float* src = tb.src[i];
+  float* dst = tb.dst[i];
+#pragma unroll
+  for (int k = 0; k < 32; k += 8) {
+    const int r = r0 + ty + k, c = c0 + tx;
+    if (r < R && c < C) tile[ty + k][tx] = src[(long)r * C + c];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 32; k += 8) {
+    const int c = c0 + ty + k, r = r0 + tx;
+    if (r < R && c < C) dst[(long)c * R + r] = tile[tx][ty + k];
+  }
+}
+
+}  // namespace mrg

@@ -634,12 +634,15 @@ static int launch_fwd(const LstmFwdArgs& a, int force_bs, int cus, hipStream_t s
   return 4;
 }
 
+static int g_bwd_blocks_per_cu = 0;  // cap on resident workgroups per CU (mrg_lstm_set_blocks_per_cu)
+
 template <int H, int G>
 static int launch_bwd(const LstmBwdArgs& a, int force_bs, int cus, hipStream_t s) {
   constexpr int NT = LstmNT<H, G>::value;
   for (int bs = 1; bs <= 8; bs *= 2) {
     if (force_bs > 0 && bs != force_bs) continue;
     long nblk = (long)a.nprob * ((a.B + bs - 1) / bs) * G;
+    if (force_bs <= 0 && g_bwd_blocks_per_cu > 0 && bs < 8 && nblk > (long)g_bwd_blocks_per_cu * cus) continue;
     bool ok;
     switch (bs) {
       case 1: ok = fits(lstm_bwd_kernel<H, G, 1>, NT, nblk, cus); if (ok) lstm_bwd_kernel<H, G, 1><<<nblk, NT, 0, s>>>(a); break;
@@ -716,6 +719,15 @@ MRG_API size_t mrg_lstm_bwd_xbuf_bytes(int B, int H) {
 }
 
 MRG_API int mrg_lstm_supported_hidden(int H) { return group_size(H) > 0; }
+
+// Backward recurrences take the smallest batch tile whose grid fits `n` workgroups per CU (0 = the
+// HW occupancy), leaving the rest of each CU to weight-gradient GEMMs issued beside them.  Returns
+// the previous cap.
+MRG_API int mrg_lstm_set_blocks_per_cu(int n) {
+  const int prev = g_bwd_blocks_per_cu;
+  g_bwd_blocks_per_cu = n > 0 ? n : 0;
+  return prev;
+}
 
 // Tuning: workgroups per recurrence group at H = 256 (8 or 16).  Affects the bwd xbuf size.
 MRG_API int mrg_lstm_config(int group256) {

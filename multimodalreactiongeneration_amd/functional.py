@@ -282,6 +282,102 @@ def set_wgrad_stream(on: bool) -> bool:
     return prev
 
 
+# Deferred weight gradients (MRG_WGRAD_DEFER=1; off by default: measured neutral): a side-stream product is not issued
+# when its operands are ready but queued until the backward reaches its next persistent recurrence
+# (_LSTMFn.backward calls flush_beside_recurrence right before mrg_lstm_bwd), then issued on the
+# side stream with the GEMM grids capped at one block per CU while the recurrence runs at one
+# workgroup per CU (mrg_lstm_set_blocks_per_cu): the latency-bound recurrence leaves most of each
+# CU idle, and the dW products fill it instead of running beside the dX chain's GEMMs (which
+# already fill the GPU).  The end-of-backward join issues whatever is still queued.  Queue order is
+# side-stream order, so the writes into each gradient buffer keep their order; a write issued on the
+# current stream (fewer than _SIDE_MIN_ROWS rows) first flushes the queue.  Not used while a
+# gradient-ready listener (DDP bucket overlap) needs each write issued when it is reported.
+_DEFER = [os.environ.get("MRG_WGRAD_DEFER", "0") == "1"]
+_PENDING = {}
+
+
+def set_wgrad_defer(on: bool) -> bool:
+    """Enable / disable deferring side-stream weight gradients to the next recurrence; returns the old value."""
+    prev = _DEFER[0]
+    _DEFER[0] = bool(on)
+    return prev
+
+
+def _ensure_join(key, cur, s, task):
+    if key not in _JOIN_PENDING:
+        def join(cur=cur, s=s, key=key):
+            _flush_deferred(key, cur.device)
+            cur.wait_stream(s)
+            _JOIN_PENDING.pop(key, None)
+        torch.autograd.Variable._execution_engine.queue_callback(join)
+        _JOIN_PENDING[key] = task
+
+
+def _defers(device, rows) -> bool:
+    return (_WGRAD_SIDE[0] and _DEFER[0] and rows >= _SIDE_MIN_ROWS and _GRAD_LISTENER[0] is None
+            and torch._C._current_graph_task_id() >= 0)
+
+
+def _flush_deferred(key, device, cap=0):
+    """Issue the queued weight-gradient products on the side stream (GEMM grids capped at `cap`
+    blocks per CU while they run beside a recurrence)."""
+    items = _PENDING.pop(key, None)
+    if not items:
+        return
+    dev = torch.device(device)
+    cur = torch.cuda.current_stream(dev)
+    s = _SIDE[key]
+    s.wait_stream(cur)
+    lib = _lib.load()
+    prev = lib.mrg_gemm_set_blocks_per_cu(cap) if cap else None
+    try:
+        with torch.cuda.stream(s):
+            for fn, keep, arith in items:
+                for t in keep:
+                    if t is not None:
+                        t.record_stream(s)
+                old = _ARITH[0]
+                _ARITH[0] = arith
+                try:
+                    fn()
+                finally:
+                    _ARITH[0] = old
+    finally:
+        if cap:
+            lib.mrg_gemm_set_blocks_per_cu(prev)
+
+
+def flush_beside_recurrence(device) -> int:
+    """Called right before a backward recurrence launch: issues the queued weight-gradient products so
+    they run beside it; returns the recurrence's workgroups-per-CU cap (1 when deferring, else 0)."""
+    if not (_WGRAD_SIDE[0] and _DEFER[0] and _GRAD_LISTENER[0] is None):
+        return 0
+    key = torch.device(device).index or 0
+    _flush_deferred(key, device, cap=1)
+    return 1
+
+
+def _on_side(device, rows, keep, fn):
+    """Run fn() (weight-gradient launches) on the side stream now, or queue it (see _DEFER)."""
+    if not _defers(device, rows):
+        with _side(device, rows, keep):
+            fn()
+        return
+    dev = torch.device(device)
+    key = dev.index or 0
+    cur = torch.cuda.current_stream(dev)
+    task = torch._C._current_graph_task_id()
+    if key in _JOIN_PENDING and _JOIN_PENDING[key] != task:
+        _flush_deferred(key, dev)
+        cur.wait_stream(_SIDE[key])
+        del _JOIN_PENDING[key]
+    s = _SIDE.get(key)
+    if s is None:
+        s = _SIDE[key] = torch.cuda.Stream(device=dev)
+    _ensure_join(key, cur, s, task)
+    _PENDING.setdefault(key, []).append((fn, tuple(keep), _ARITH[0]))
+
+
 class _side:
     """Issue the enclosed launches on the device's weight-gradient stream (see above)."""
     __slots__ = ("dev", "rows", "keep", "ctx")
@@ -299,22 +395,19 @@ class _side:
         s = _SIDE.get(key)
         if key in _JOIN_PENDING and _JOIN_PENDING[key] != task:
             # left over from a backward that did not finish: order after its side-stream work
+            _flush_deferred(key, dev)
             cur.wait_stream(s)
             del _JOIN_PENDING[key]
         if self.rows < _SIDE_MIN_ROWS:
             if key in _JOIN_PENDING:  # order this write after the side stream's pending ones
+                _flush_deferred(key, dev)
                 cur.wait_stream(s)
             return self
         if task < 0:  # not inside a backward pass: stay on the current stream
             return self
         if s is None:
             s = _SIDE[key] = torch.cuda.Stream(device=dev)
-        if key not in _JOIN_PENDING:
-            def join(cur=cur, s=s, key=key):
-                cur.wait_stream(s)
-                _JOIN_PENDING.pop(key, None)
-            torch.autograd.Variable._execution_engine.queue_callback(join)
-            _JOIN_PENDING[key] = task
+        _ensure_join(key, cur, s, task)
         s.wait_stream(cur)
         for t in self.keep:
             if t is not None:
@@ -334,7 +427,7 @@ def _wgrad(dY, ldy, X, ldx, rows, Nout, Nin, gw, device, *, dy_hi=0, dy_div=0, x
     """gw[Nout, Nin] += sum_rows dY[row, :]^T X[row, :]; gb (and gb2) += sum_rows dY[row, :] (fused).
 
     keep: the tensors behind the dY / X pointers (side-stream lifetime, see _side)."""
-    with _side(device, rows, keep):
+    def issue():
         if gw is None:
             if gb is not None:
                 colsum(rows, Nout, dY, ldy, _ptr(gb), out2=_ptr(gb2), ld_hi=dy_hi, rdiv=dy_div, device=device)
@@ -342,6 +435,72 @@ def _wgrad(dY, ldy, X, ldx, rows, Nout, Nin, gw, device, *, dy_hi=0, dy_div=0, x
         gemm(Nout, Nin, rows, dY, 1, ldy, X, 0, ldx, _ptr(gw), Nin, beta=1.0, a_hi=dy_hi, a_div=dy_div,
              b_hi=x_hi, b_div=x_div, splits=wgrad_splits(Nout, Nin, rows), device=device,
              asum_out=_ptr(gb), asum_out2=_ptr(gb2))
+    _on_side(device, rows, keep, issue)
+
+
+# --- [in][out] weight copies for the input-gradient products.  dX = dY W reads W [out][in] along
+# n (not k): the product runs as a k-contiguous one, dY (W^T)^T, on the LDS-DMA x6 kernel
+# (gemm_glds.hip) when the weight's transposed copy exists.  The forwards note the weights of their
+# large products (>= _WT_MIN_ROWS rows, >= 256 inputs); the backward's first use transposes every
+# noted weight in ONE launch (mrg_transpose_batched) and later uses hit the cache.  A weight noted
+# again (the next step's forward: the optimizer has rewritten it in place) drops its stale copy.
+# MRG_DX_TRANSPOSED=0 keeps the [out][in] operand (the register-staged kernel's n-contiguous path).
+_WT_ON = [os.environ.get("MRG_DX_TRANSPOSED", "1") != "0"]
+_WT_MIN_ROWS = 2048
+_WT_PENDING = {}
+_WT_CACHE = {}
+
+
+def set_dx_transposed(on: bool) -> bool:
+    prev = _WT_ON[0]
+    _WT_ON[0] = bool(on)
+    return prev
+
+
+def _wt_key(w):
+    return (w.data_ptr(), tuple(w.shape))
+
+
+def _wt_note(w, rows, need=True):
+    """Forward side (inside autograd Function.forward: pass ctx.needs_input_grad of the input): w
+    [out][in] (a contiguous 2-D view) will serve a dX product over `rows` rows."""
+    if not (need and _WT_ON[0] and rows >= _WT_MIN_ROWS and w.shape[1] >= 256 and w.shape[0] % 32 == 0
+            and w.is_contiguous()):
+        return
+    k = _wt_key(w)
+    _WT_CACHE.pop(k, None)
+    _WT_PENDING[k] = w
+
+
+def _wt(w):
+    """Backward side: the [in][out] copy of w, or None when w was not noted in this step's forward."""
+    k = _wt_key(w)
+    t = _WT_CACHE.get(k)
+    if t is not None:
+        return t
+    if k not in _WT_PENDING:
+        return None
+    items = list(_WT_PENDING.values())
+    _WT_PENDING.clear()
+    outs = [torch.empty(x.shape[1], x.shape[0], device=x.device, dtype=torch.float32) for x in items]
+    n = len(items)
+    VP = ctypes.c_void_p
+    _lib.check(_lib.load().mrg_transpose_batched(
+        n, (VP * n)(*[_ptr(x) for x in items]), (VP * n)(*[_ptr(o) for o in outs]),
+        (ctypes.c_int * n)(*[x.shape[0] for x in items]), (ctypes.c_int * n)(*[x.shape[1] for x in items]),
+        _stream()), "transpose")
+    for x, o in zip(items, outs):
+        _WT_CACHE[_wt_key(x)] = o
+    return _WT_CACHE[k]
+
+
+def _dx_gemm(M, In, N, dY, ldy, w, dx, ldx, **kw):
+    """dx[M, In] = epi(dY[M, N] w[N, In] ...): through w's [in][out] copy when one exists."""
+    wt = _wt(w) if M >= _WT_MIN_ROWS else None
+    if wt is not None:
+        gemm(M, In, N, dY, 0, ldy, _ptr(wt), 1, N, dx, ldx, **kw)
+    else:
+        gemm(M, In, N, dY, 0, ldy, _ptr(w), 0, In, dx, ldx, **kw)
 
 
 # ------------------------------------------------------------------ Linear
@@ -355,6 +514,7 @@ class _LinearFn(Function):
         M = x2.shape[0]
         y = torch.empty(M, N, device=x.device, dtype=torch.float32)
         gemm(M, N, In, _ptr(x2), 0, In, _ptr(w), 1, In, _ptr(y), N, bias=_ptr(b), device=x.device)
+        _wt_note(w, M, ctx.needs_input_grad[0])
         ctx.save_for_backward(x2, w, b)
         ctx.xshape = x.shape
         return y.view(*x.shape[:-1], N)
@@ -371,7 +531,7 @@ class _LinearFn(Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(M, In, device=dev, dtype=torch.float32)
-            gemm(M, In, N, _ptr(dy2), 0, N, _ptr(w), 0, In, _ptr(dx), In, device=dev)
+            _dx_gemm(M, In, N, _ptr(dy2), N, w, _ptr(dx), In, device=dev)
             dx = dx.view(ctx.xshape)
         return dx, None, None
 
@@ -394,6 +554,7 @@ class _FFNFn(Function):
         gemm(M, Hb, In, _ptr(x2), 0, In, _ptr(w1), 1, In, _ptr(h), Hb, bias=_ptr(b1), epi=1, device=dev)
         z = torch.empty(M, N, device=dev, dtype=torch.float32)
         gemm(M, N, Hb, _ptr(h), 0, Hb, _ptr(w2), 1, Hb, _ptr(z), N, bias=_ptr(b2), device=dev)
+        _wt_note(w1, M, ctx.needs_input_grad[0])
         ctx.save_for_backward(x2, h, w1, b1, w2, b2)
         ctx.xshape = x.shape
         return z.view(*x.shape[:-1], N)
@@ -416,7 +577,7 @@ class _FFNFn(Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(M, In, device=dev, dtype=torch.float32)
-            gemm(M, In, Hb, _ptr(dh), 0, Hb, _ptr(w1), 0, In, _ptr(dx), In, device=dev)
+            _dx_gemm(M, In, Hb, _ptr(dh), Hb, w1, _ptr(dx), In, device=dev)
             dx = dx.view(ctx.xshape)
         return dx, None, None, None, None
 
@@ -485,13 +646,14 @@ def _resln_bwd(dy2, a2, b2, gamma, beta, mean, rstd):
         None, None, 1, _ptr(ws), _stream()), "layernorm bwd")
     if gg is not None or gb is not None:
         # dgamma / dbeta from the per-block partials: parameter gradients, off the critical path
-        with _side(dev, rows, (ws,)):
+        def reduce():
             scratch = None
             if gg is None or gb is None:
                 scratch = torch.empty(2, E, device=dev, dtype=torch.float32)
             _lib.check(lib.mrg_residual_layernorm_param_reduce(
                 rows, E, _ptr(ws), _ptr(gg if gg is not None else scratch[0]),
                 _ptr(gb if gb is not None else scratch[1]), 1, _stream()), "layernorm param reduce")
+        _on_side(dev, rows, (ws,), reduce)
     return g
 
 
@@ -510,6 +672,7 @@ class _LinResLNFn(Function):
         M = x2.shape[0]
         z = torch.empty(M, E, device=x.device, dtype=torch.float32)
         gemm(M, E, E, _ptr(x2), 0, E, _ptr(w), 1, E, _ptr(z), E, bias=_ptr(b), device=x.device)
+        _wt_note(w, M, ctx.needs_input_grad[0])
         y, mean, rstd = _resln_fwd(z, x2, gamma, beta, eps)
         ctx.save_for_backward(x2, w, b, z, gamma, beta, mean, rstd)
         ctx.xshape = x.shape
@@ -526,7 +689,7 @@ class _LinResLNFn(Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(M, E, device=dev, dtype=torch.float32)
-            gemm(M, E, E, _ptr(g), 0, E, _ptr(w), 0, E, _ptr(dx), E, epi=3, aux=_ptr(g), ldaux=E, device=dev)
+            _dx_gemm(M, E, E, _ptr(g), E, w, _ptr(dx), E, epi=3, aux=_ptr(g), ldaux=E, device=dev)
             dx = dx.view(ctx.xshape)
         return dx, None, None, None, None, None
 
@@ -550,6 +713,7 @@ class _FFNResLNFn(Function):
         gemm(M, Hb, E, _ptr(x2), 0, E, _ptr(w1), 1, E, _ptr(h), Hb, bias=_ptr(b1), epi=1, device=dev)
         z = torch.empty(M, E, device=dev, dtype=torch.float32)
         gemm(M, E, Hb, _ptr(h), 0, Hb, _ptr(w2), 1, Hb, _ptr(z), E, bias=_ptr(b2), device=dev)
+        _wt_note(w1, M, ctx.needs_input_grad[0])
         y, mean, rstd = _resln_fwd(z, x2, gamma, beta, eps)
         ctx.save_for_backward(x2, h, z, w1, b1, w2, b2, gamma, beta, mean, rstd)
         ctx.xshape = x.shape
@@ -570,7 +734,7 @@ class _FFNResLNFn(Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(M, E, device=dev, dtype=torch.float32)
-            gemm(M, E, Hb, _ptr(dh), 0, Hb, _ptr(w1), 0, E, _ptr(dx), E, epi=3, aux=_ptr(g), ldaux=E, device=dev)
+            _dx_gemm(M, E, Hb, _ptr(dh), Hb, w1, _ptr(dx), E, epi=3, aux=_ptr(g), ldaux=E, device=dev)
             dx = dx.view(ctx.xshape)
         return dx, None, None, None, None, None, None, None
 
@@ -614,6 +778,7 @@ class _LSTMFn(Function):
             gx = torch.empty(B, T, 4 * H, device=dev, dtype=torch.float32)
             gemm(B * T, 4 * H, In_i, _ptr(x), 0, In_i, _ptr(w_ih), 1, In_i, _ptr(gx), 4 * H,
                  bias=_ptr(b_ih), device=dev)
+            _wt_note(w_ih, B * T, ctx.needs_input_grad[1 + K * i])
             gxs.append(gx)
             if concat:
                 y_ptrs.append(_ptr(ycat, i * H))
@@ -728,6 +893,7 @@ class _LSTMFn(Function):
         def arr(ctype, vals):
             return (ctype * nprob)(*vals)
         VP = ctypes.c_void_p
+        lib.mrg_lstm_set_blocks_per_cu(flush_beside_recurrence(dev))
         pr = _probe("lstm_bwd", 8.0 * H * H * B * T * nprob).__enter__()  # dG W_hh FLOPs
         rc = lib.mrg_lstm_bwd(
             nprob, B, T, H,
@@ -760,9 +926,9 @@ class _LSTMFn(Function):
                        dy_hi=T * 4 * H, dy_div=T - 1, x_hi=y_bs[i], x_div=T - 1, keep=(g, yb))
             if gw is not None and h0 is not None:
                 t0 = T - 1 if reverse[i] else 0
-                with _side(dev, B * T, (g, h0)):
-                    gemm(4 * H, H, B, _ptr(g, t0 * 4 * H), 1, T * 4 * H, _ptr(h0), 0, H, _ptr(gw), H,
-                         beta=1.0, device=dev)
+                _on_side(dev, B * T, (g, h0),
+                         lambda g=g, h0=h0, gw=gw, t0=t0: gemm(4 * H, H, B, _ptr(g, t0 * 4 * H), 1, T * 4 * H,
+                                                               _ptr(h0), 0, H, _ptr(gw), H, beta=1.0, device=dev))
             gbi, gbh = _gbuf(b_ih), _gbuf(b_hh)
             first = gbi if gbi is not None else gbh
             second = gbh if gbi is not None else None
@@ -771,15 +937,14 @@ class _LSTMFn(Function):
             dx = None
             if need[1 + K * i]:
                 if ctx.shared_x[i] and dx_first is not None:
-                    gemm(rows, In, 4 * H, _ptr(g), 0, 4 * H, _ptr(w_ih), 0, In, _ptr(dx_first), In,
-                         beta=1.0, device=dev)
+                    _dx_gemm(rows, In, 4 * H, _ptr(g), 4 * H, w_ih, _ptr(dx_first), In, beta=1.0, device=dev)
                 else:
                     dx = torch.empty(B, T, In, device=dev, dtype=torch.float32)
                     if res[i] is not None:  # dx = dG W_ih + g (residual branch in the epilogue)
-                        gemm(rows, In, 4 * H, _ptr(g), 0, 4 * H, _ptr(w_ih), 0, In, _ptr(dx), In, epi=3,
-                             aux=_ptr(res[i]), ldaux=In, device=dev)
+                        _dx_gemm(rows, In, 4 * H, _ptr(g), 4 * H, w_ih, _ptr(dx), In, epi=3, aux=_ptr(res[i]),
+                                 ldaux=In, device=dev)
                     else:
-                        gemm(rows, In, 4 * H, _ptr(g), 0, 4 * H, _ptr(w_ih), 0, In, _ptr(dx), In, device=dev)
+                        _dx_gemm(rows, In, 4 * H, _ptr(g), 4 * H, w_ih, _ptr(dx), In, device=dev)
                     if dx_first is None:
                         dx_first = dx
             out += [dx, None, None, None, None, dh0[i], dc0[i]] + ([None, None] if resln else [])
@@ -993,12 +1158,12 @@ class _GRUFn(Function):
                    dy_hi=T * H3, dy_div=T - 1, x_hi=T * H, x_div=T - 1, keep=(dGH, y))
         if gw is not None and h0c is not None:
             t0 = T - 1 if reverse else 0
-            with _side(dev, B * T, (dGH, h0c)):
-                gemm(H3, H, B, _ptr(dGH, t0 * H3), 1, T * H3, _ptr(h0c), 0, H, _ptr(gw), H, beta=1.0, device=dev)
+            _on_side(dev, B * T, (dGH, h0c),
+                     lambda: gemm(H3, H, B, _ptr(dGH, t0 * H3), 1, T * H3, _ptr(h0c), 0, H, _ptr(gw), H, beta=1.0,
+                                  device=dev))
         gbh = _gbuf(b_hh)
         if gbh is not None:
-            with _side(dev, B * T, (dGH,)):
-                colsum(B * T, H3, _ptr(dGH), H3, _ptr(gbh), device=dev)
+            _on_side(dev, B * T, (dGH,), lambda: colsum(B * T, H3, _ptr(dGH), H3, _ptr(gbh), device=dev))
         dx = None
         if need[1]:
             dx = torch.empty(B, T, In, device=dev, dtype=torch.float32)
@@ -1051,6 +1216,10 @@ class _MHAFn(Function):
         _lib.check(rc, "attention fwd")
         out = torch.empty(B, Tq, E, device=dev, dtype=torch.float32)
         gemm(B * Tq, E, E, _ptr(O), 0, E, _ptr(out_w), 1, E, _ptr(out), E, bias=_ptr(out_b), device=dev)
+        need_in = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
+        _wt_note(out_w, B * Tq, need_in)
+        _wt_note(in_w[:E], B * Tq, ctx.needs_input_grad[1])
+        _wt_note(in_w[E:], B * Tk, ctx.needs_input_grad[2])
         extra = []
         res = out
         if eps is not None:
@@ -1081,7 +1250,7 @@ class _MHAFn(Function):
         else:
             do2 = dout.contiguous()
         dO = torch.empty(B, Tq, E, device=dev, dtype=torch.float32)
-        gemm(B * Tq, E, E, _ptr(do2), 0, E, _ptr(out_w), 0, E, _ptr(dO), E, device=dev)
+        _dx_gemm(B * Tq, E, E, _ptr(do2), E, out_w, _ptr(dO), E, device=dev)
         _wgrad(_ptr(do2), E, _ptr(O), E, B * Tq, E, E, _gbuf(out_w), dev, gb=_gbuf(out_b), keep=(do2, O))
         dQ = torch.empty(B, Tq, E, device=dev, dtype=torch.float32)
         dKV = torch.empty(B, Tk, 2 * E, device=dev, dtype=torch.float32)
@@ -1102,16 +1271,15 @@ class _MHAFn(Function):
         if ctx.needs_input_grad[1]:
             dq_in = torch.empty(B, Tq, E, device=dev, dtype=torch.float32)
             if g is not None:
-                gemm(B * Tq, E, E, _ptr(dQ), 0, E, _ptr(in_w), 0, E, _ptr(dq_in), E, epi=3, aux=_ptr(g), ldaux=E,
-                     device=dev)
+                _dx_gemm(B * Tq, E, E, _ptr(dQ), E, in_w[:E], _ptr(dq_in), E, epi=3, aux=_ptr(g), ldaux=E,
+                         device=dev)
             else:
-                gemm(B * Tq, E, E, _ptr(dQ), 0, E, _ptr(in_w), 0, E, _ptr(dq_in), E, device=dev)
+                _dx_gemm(B * Tq, E, E, _ptr(dQ), E, in_w[:E], _ptr(dq_in), E, device=dev)
         elif g is not None:
             dq_in = None
         if ctx.needs_input_grad[2]:
             dkv_in = torch.empty(B, Tk, E, device=dev, dtype=torch.float32)
-            gemm(B * Tk, E, 2 * E, _ptr(dKV), 0, 2 * E, _ptr(in_w, E * E), 0, E, _ptr(dkv_in), E,
-                 device=dev)
+            _dx_gemm(B * Tk, E, 2 * E, _ptr(dKV), 2 * E, in_w[E:], _ptr(dkv_in), E, device=dev)
         return None, dq_in, dkv_in, None, None, None, None, None, None, None, None
 
 

@@ -254,9 +254,12 @@ def test_metaformer_generation_benchmark_width_vs_oracle():
     assert rel_err(pred, ref) < TOL
 
 
-def test_wgrad_side_stream_bitwise():
+@pytest.mark.parametrize("defer,B", [(False, 8), (True, 64)])
+def test_wgrad_side_stream_bitwise(defer, B):
     """Weight gradients on the side stream (functional._side), eager and graph-replayed, give the
-    bit-identical gradients of the single-stream schedule (every kernel is deterministic)."""
+    bit-identical gradients of the single-stream schedule (every kernel is deterministic).  With
+    deferral the products run beside the next backward recurrence, which then takes one workgroup
+    per CU (batch tile 4 instead of 2 at B = 64): the gradients are still bitwise the same."""
     from multimodalreactiongeneration_amd import configs as C
     from multimodalreactiongeneration_amd import functional as Fn
     from multimodalreactiongeneration_amd.graphs import capture
@@ -266,13 +269,14 @@ def test_wgrad_side_stream_bitwise():
     torch.manual_seed(0)
     m = Metaformer(mc, oc, me).to(DEV)
     opt = m.configure_optimizers()["optimizer"]
-    batch = make_batch(B=8, T=300, ratio=1, seed=5, device=DEV)
+    batch = make_batch(B=B, T=300, ratio=1, seed=5, device=DEV)
 
     def step():
         opt.zero_grad()
         m.training_step(list(batch))["loss"].backward()
 
     prev = Fn.set_wgrad_stream(False)
+    prev_defer = Fn.set_wgrad_defer(defer)
     try:
         step()
         torch.cuda.synchronize()
@@ -286,8 +290,10 @@ def test_wgrad_side_stream_bitwise():
         replay()
         torch.cuda.synchronize()
         assert torch.equal(opt.flat_grad, ref)
+        Fn.check_errors()
     finally:
         Fn.set_wgrad_stream(prev)
+        Fn.set_wgrad_defer(prev_defer)
 
 
 def test_metaformer_q9_broadcast_losses_golden():

@@ -101,6 +101,54 @@ def test_few_row_gemms(M, N, K, epi, split):
     assert int(Fn._counters(DEV).abs().sum()) == 0
 
 
+@pytest.mark.parametrize("depth,bn", [(2, 128), (3, 128), (3, 64), (4, 128)])
+@pytest.mark.parametrize("M,N,K,epi,rowmap", [
+    (19200, 1024, 256, 0, False), (19200, 256, 256, 3, False), (1000, 192, 96, 1, False), (300, 64, 32, 0, False),
+    (64 * 300, 256, 512, 0, True)])
+def test_glds_gemm_vs_fp64(M, N, K, epi, rowmap, depth, bn):
+    """The LDS-DMA pipelined x6 kernel (gemm_x6g_kernel: k-contiguous A and B, DMA ring of `depth`
+    k-tiles, fragments split into bf16 planes as they are read) against fp64: M and N edges
+    (clamped rows, masked stores), bias / beta / ReLU / residual epilogues, and an A read through a
+    RowMap ([B, T] rows of a [B, T + 12, K] view: the [:, lead:] slice).  Bitwise repeatable."""
+    from multimodalreactiongeneration_amd import functional as Fn
+    from multimodalreactiongeneration_amd import _lib as L
+    lib = L.load()
+    g = torch.Generator().manual_seed(M + 7 * N + K + depth)
+    if rowmap:
+        B_, T_ = 64, M // 64
+        full = torch.randn(B_, T_ + 12, K, generator=g)
+        a = full[:, 12:].reshape(M, K)
+        ad = full.to(DEV)
+        a_ptr, lda, a_hi, a_div = Fn._ptr(ad, 12 * K), K, (T_ + 12) * K, T_
+    else:
+        a = torch.randn(M, K, generator=g)
+        ad = a.to(DEV)
+        a_ptr, lda, a_hi, a_div = Fn._ptr(ad), K, 0, 0
+    w = torch.randn(N, K, generator=g) / math.sqrt(K)
+    bias = torch.randn(N, generator=g)
+    c0 = torch.randn(M, N, generator=g)
+    aux = torch.randn(M, N, generator=g)
+    wd, bd, auxd = w.to(DEV), bias.to(DEV), aux.to(DEV)
+    L.check(lib.mrg_gemm_set_glds(depth, bn), "glds")
+    try:
+        outs = []
+        for _ in range(2):
+            c = c0.to(DEV)
+            Fn.gemm(M, N, K, a_ptr, 0, lda, Fn._ptr(wd), 1, K, Fn._ptr(c), N, beta=0.5, bias=Fn._ptr(bd), epi=epi,
+                    aux=Fn._ptr(auxd) if epi >= 2 else None, ldaux=N, a_hi=a_hi, a_div=a_div, device=DEV)
+            outs.append(c)
+        torch.cuda.synchronize()
+    finally:
+        L.check(lib.mrg_gemm_set_glds(0, 128), "glds")
+    ref = a.double() @ w.double().t() + 0.5 * c0.double() + bias.double()
+    if epi == 1:
+        ref = ref.clamp_min(0)
+    elif epi == 3:
+        ref = ref + aux.double()
+    assert rel_err(outs[0], ref) < 2e-6
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("M,N,K,transB,a_off", [
     (64, 256, 1024, 0, 0), (64, 128, 512, 1, 0), (37, 96, 516, 0, 0), (64, 256, 1024, 1, 1), (50, 40, 64, 1, 3)])
 def test_few_row_gemm_operand_layouts(M, N, K, transB, a_off):

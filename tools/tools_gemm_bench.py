@@ -34,6 +34,8 @@ PROBES = [
     ("square TN 4096^3", 4096, 4096, 4096, 1, 0, 0, False),
     ("4096x4096 K=256 NT", 4096, 4096, 256, 0, 1, 0, False),
     ("19200x1024 K=1024 NT", R, 1024, 1024, 0, 1, 0, False),
+    ("lstm dX as NT (W_ih^T copy)", R, 256, 1024, 0, 1, 0, False),
+    ("kv512 dX as NT", R, 256, 512, 0, 1, 0, False),
     ("odd NN 1000x70x45", 1000, 70, 45, 0, 0, 0, False),
     ("odd NT 333x129x97", 333, 129, 97, 0, 1, 0, False),
     ("odd TN 130x66x1001", 130, 66, 1001, 1, 0, 0, False),
