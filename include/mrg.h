@@ -60,6 +60,17 @@ int mrg_gemm_set_glds(int depth, int bn);
  * input-gradient products dY W run k-contiguous (nn.Linear / LSTM backward, mixer_block.py:63-74).*/
 int mrg_transpose_batched(int n, const float* const* src, float* const* dst, const int* rows, const int* cols,
                           hipStream_t stream);
+/* Three bf16 planes (the x6 split: v ~ p0 + p1 + p2) of n row-major fp32 weights, once per optimizer
+ * step: dst_i [3][R'][C'] with (R', C') = (rows_i, cols_i), or (cols_i, rows_i) when transpose_i.   */
+int mrg_split_planes_batched(int n, const float* const* src, void* const* dst, const int* rows, const int* cols,
+                             const int* transpose, hipStream_t stream);
+/* C = epi(alpha A B^T + beta C + bias), B as three bf16 planes (row n of plane p at
+ * Bplanes + p * bplane + n * ldb, bf16 elements), A [M][K] through the RowMap; K % 32 == 0.  The
+ * forward products x W^T and the input-gradient products dY W (B = planes of W^T) of the nn.Linear /
+ * LSTM / MultiheadAttention layers (mixer_block.py:63-74,237-252, for_sequential.py:42-51).      */
+int mrg_gemm_x6_planes(int M, int N, int K, float alpha, const float* A, long lda, long lda_hi, int a_rdiv,
+                       const void* Bplanes, long ldb, long bplane, float beta, float* C, long ldc,
+                       const float* bias, int epilogue, const float* aux, long ldaux, hipStream_t stream);
 /* Tuning only: force the tile shape (0: 128x128, 1: 128x64, 2: 64x64), -1 = heuristic. */
 int mrg_gemm_force_tile(int tile);
 /* Tuning only: structural variants of the x6 kernel (0 product, 1 split + one MFMA, 2 plane-0 +

@@ -37,6 +37,9 @@ SIGNATURES = {
     "mrg_gemm_set_blocks_per_cu": (c_int, [c_int]),
     "mrg_gemm_set_glds": (c_int, [c_int, c_int]),
     "mrg_transpose_batched": (c_int, [c_int, PP, PP, PI, PI, P]),
+    "mrg_split_planes_batched": (c_int, [c_int, PP, PP, PI, PI, PI, P]),
+    "mrg_gemm_x6_planes": (c_int, [c_int, c_int, c_int, c_float, P, c_long, c_long, c_int, P, c_long, c_long,
+                                   c_float, P, c_long, P, c_int, P, c_long, P]),
     "mrg_lstm_set_blocks_per_cu": (c_int, [c_int]),
     "mrg_gemm_x6_variant": (c_int, [c_int, c_int, c_int, c_int, P, P, P, P]),
     "mrg_gemm_f32": (c_int, [c_int, c_int, c_int, c_float,

@@ -54,11 +54,19 @@ __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BM, int BN, int NS>
-__global__ __launch_bounds__(NT, 1) void gemm_x6g_kernel(GemmArgs a) {
+// PB = 1: the B operand arrives pre-split, as three bf16 planes [3][N][ldb] (plane stride bplane
+// elements; mrg_split_planes_batched makes them once per optimizer step for every weight), so only
+// A is split in the loop (half the VALU of the split; the B fragments are three ds_read_b128).
+// B plane rows are 64 B per k-tile: one DMA wave-instruction fills 16 rows (lane L -> row 16g + L/4,
+// 16-B slot L%4 holding 8-k chunk (L%4) ^ ((row >> 2) & 3)).
+template <int BM, int BN, int NS, int PB>
+__global__ __launch_bounds__(NT, 1) void gemm_x6g_kernel(GemmArgs a, long bplane) {
   constexpr int TM = BM / 64, TN = BN / 64;
-  constexpr int SA = BM * 128, SS = SA + BN * 128;  // bytes of one ring slot
-  constexpr int GA = BM / 32, GB = BN / 32;         // DMA wave-instructions per wave per k-tile
+  constexpr int SA = BM * 128;                                   // A: [BM][32] fp32
+  constexpr int SBP = BN * 64;                                   // one B plane: [BN][32] bf16
+  constexpr int SS = SA + (PB ? 3 * SBP : BN * 128);             // bytes of one ring slot
+  constexpr int GA = BM / 32;                                    // DMA wave-instructions per wave per k-tile
+  constexpr int GB = PB ? 3 * BN / 64 : BN / 32;
   constexpr int GT = GA + GB;
   static_assert(NS >= 2 && NS <= 4 && (BM == 64 || BM == 128) && (BN == 64 || BN == 128), "gemm_x6g tile");
   __shared__ __attribute__((aligned(16))) unsigned char lds[NS * SS];
@@ -72,23 +80,40 @@ __global__ __launch_bounds__(NT, 1) void gemm_x6g_kernel(GemmArgs a) {
   const int m0 = (t / a.tiles_n) * BM, n0 = (t % a.tiles_n) * BN;
   const int nk = a.K / 32;
 
-  const float* src[GT];
+  // per-lane DMA source (bytes) and LDS destination offset of each wave-instruction of a k-tile
+  const unsigned char* src[GT];
+  int dsto[GT];
 #pragma unroll
   for (int g = 0; g < GT; ++g) {
-    const bool isa = g < GA;
-    const int row = 8 * (wave * (isa ? GA : GB) + (isa ? g : g - GA)) + (lane >> 3);
-    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
-    src[g] = isa ? a.A + a.amap.off(min(m0 + row, a.M - 1)) + 4 * chunk
-                 : a.B + a.bmap.off(min(n0 + row, a.N - 1)) + 4 * chunk;
+    if (g < GA) {
+      const int grp = wave * GA + g;
+      const int row = 8 * grp + (lane >> 3);
+      const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+      src[g] = reinterpret_cast<const unsigned char*>(a.A + a.amap.off(min(m0 + row, a.M - 1)) + 4 * chunk);
+      dsto[g] = grp << 10;
+    } else if (!PB) {
+      const int grp = wave * GB + (g - GA);
+      const int row = 8 * grp + (lane >> 3);
+      const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+      src[g] = reinterpret_cast<const unsigned char*>(a.B + a.bmap.off(min(n0 + row, a.N - 1)) + 4 * chunk);
+      dsto[g] = SA + (grp << 10);
+    } else {
+      const int G = wave * GB + (g - GA), p = G / (BN / 16), grp = G % (BN / 16);
+      const int row = 16 * grp + (lane >> 2);
+      const int chunk = (lane & 3) ^ ((row >> 2) & 3);
+      const __bf16* pb = reinterpret_cast<const __bf16*>(a.B) + p * bplane;
+      src[g] = reinterpret_cast<const unsigned char*>(pb + (long)min(n0 + row, a.N - 1) * a.bmap.ld_lo + 8 * chunk);
+      dsto[g] = SA + p * SBP + (grp << 10);
+    }
   }
   const unsigned lds_base = (unsigned)(uintptr_t)((__attribute__((address_space(3))) unsigned char*)lds);
   auto issue = [&](int kt, int slot) {
 #pragma unroll
     for (int g = 0; g < GT; ++g) {
-      const int grp = g < GA ? wave * GA + g : wave * GB + (g - GA);
-      unsigned char* dst = lds + slot * SS + (g < GA ? 0 : SA) + (grp << 10);
-      __builtin_amdgcn_global_load_lds((const void*)(src[g] + kt * 32),
-                                       (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+      const int adv = (g < GA || !PB) ? 128 : 64;  // bytes per k-tile along a row
+      __builtin_amdgcn_global_load_lds((const void*)(src[g] + (long)kt * adv),
+                                       (__attribute__((address_space(3))) void*)(lds + slot * SS + dsto[g]), 16, 0,
+                                       0);
     }
   };
 
@@ -125,11 +150,18 @@ __global__ __launch_bounds__(NT, 1) void gemm_x6g_kernel(GemmArgs a) {
         ra[i][0] = lds_read16(sa + glds_off(row, c0));
         ra[i][1] = lds_read16(sa + glds_off(row, c0 + 1));
       }
+      f32x4v_ rp[TN][3];
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int row = wn + 32 * j + lr;
-        rb[j][0] = lds_read16(sb + glds_off(row, c0));
-        rb[j][1] = lds_read16(sb + glds_off(row, c0 + 1));
+        if (PB) {
+          const int c = 2 * s + lh;
+#pragma unroll
+          for (int p = 0; p < 3; ++p) rp[j][p] = lds_read16(sb + p * SBP + row * 64 + ((c ^ ((row >> 2) & 3)) << 4));
+        } else {
+          rb[j][0] = lds_read16(sb + glds_off(row, c0));
+          rb[j][1] = lds_read16(sb + glds_off(row, c0 + 1));
+        }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
@@ -137,7 +169,14 @@ __global__ __launch_bounds__(NT, 1) void gemm_x6g_kernel(GemmArgs a) {
 #pragma unroll
       for (int i = 0; i < TM; ++i) split8(ra[i][0], ra[i][1], fa[i]);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) split8(rb[j][0], rb[j][1], fb[j]);
+      for (int j = 0; j < TN; ++j) {
+        if (PB) {
+#pragma unroll
+          for (int p = 0; p < 3; ++p) fb[j][p] = __builtin_bit_cast(bf16x8, rp[j][p]);
+        } else {
+          split8(rb[j][0], rb[j][1], fb[j]);
+        }
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -192,8 +231,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_x6g_kernel(GemmArgs a) {
   }
 }
 
-template <int BM, int BN>
-static void launch_tiles(GemmArgs a, int ns, hipStream_t s) {
+template <int BM, int BN, int PB>
+static void launch_tiles(GemmArgs a, int ns, long bplane, hipStream_t s) {
   a.tiles_n = (a.N + BN - 1) / BN;
   a.tiles_mn = a.tiles_n * ((a.M + BM - 1) / BM);
   a.ntiles = a.tiles_mn;
@@ -201,22 +240,25 @@ static void launch_tiles(GemmArgs a, int ns, hipStream_t s) {
   a.ws = nullptr;
   const unsigned grid = (unsigned)a.tiles_mn;
   switch (ns) {
-    case 2: gemm_x6g_kernel<BM, BN, 2><<<grid, NT, 0, s>>>(a); break;
-    case 4: gemm_x6g_kernel<BM, BN, 4><<<grid, NT, 0, s>>>(a); break;
-    default: gemm_x6g_kernel<BM, BN, 3><<<grid, NT, 0, s>>>(a); break;
+    case 2: gemm_x6g_kernel<BM, BN, 2, PB><<<grid, NT, 0, s>>>(a, bplane); break;
+    case 4: gemm_x6g_kernel<BM, BN, 4, PB><<<grid, NT, 0, s>>>(a, bplane); break;
+    default: gemm_x6g_kernel<BM, BN, 3, PB><<<grid, NT, 0, s>>>(a, bplane); break;
   }
 }
 
-void launch_x6g(GemmArgs a, int ns, int bm, int bn, hipStream_t s) {
+template <int PB>
+static void launch_shape(GemmArgs a, int ns, int bm, int bn, long bplane, hipStream_t s) {
   if (bm == 64) {
-    if (bn == 64) launch_tiles<64, 64>(a, ns, s);
-    else launch_tiles<64, 128>(a, ns, s);
+    if (bn == 64) launch_tiles<64, 64, PB>(a, ns, bplane, s);
+    else launch_tiles<64, 128, PB>(a, ns, bplane, s);
   } else if (bn == 64) {
-    launch_tiles<128, 64>(a, ns, s);
+    launch_tiles<128, 64, PB>(a, ns, bplane, s);
   } else {
-    launch_tiles<128, 128>(a, ns, s);
+    launch_tiles<128, 128, PB>(a, ns, bplane, s);
   }
 }
+
+void launch_x6g(GemmArgs a, int ns, int bm, int bn, hipStream_t s) { launch_shape<0>(a, ns, bm, bn, 0, s); }
 
 // ----------------------------------------------------------------------------------------------
 // Batched transpose: dst_i [cols_i][rows_i] = src_i [rows_i][cols_i]^T for up to MRG_TP_MAX
@@ -247,3 +289,110 @@ __global__ __launch_bounds__(256) void transpose_batched_kernel(TransposeBatch t
 }
 
 }  // namespace mrg
+
+namespace mrg {
+
+// ----------------------------------------------------------------------------------------------
+// Three bf16 planes of a weight, once per optimizer step: dst [3][R'][C'] (plane stride R' C'),
+// (R', C') = (rows, cols), or (cols, rows) for the transposed copy (the input-gradient products'
+// k-contiguous operand).  32 x 32 tiles through LDS; the split is the x6 one (RNE, v - v0, ...).
+struct PlaneBatch {
+  int n;
+  const float* src[MRG_TP_MAX];
+  __bf16* dst[MRG_TP_MAX];
+  int rows[MRG_TP_MAX], cols[MRG_TP_MAX], tr[MRG_TP_MAX];
+  int first[MRG_TP_MAX + 1];
+};
+
+__global__ __launch_bounds__(256) void split_planes_kernel(PlaneBatch pb) {
+  __shared__ float tile[32][33];
+  int blk = blockIdx.x, i = 0;
+  while (i + 1 < pb.n && blk >= pb.first[i + 1]) ++i;
+  const int local = blk - pb.first[i];
+  const int R = pb.rows[i], C = pb.cols[i];
+  const int tc = (C + 31) / 32;
+  const int r0 = (local / tc) * 32, c0 = (local % tc) * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+#pragma unroll
+  for (int k = 0; k < 32; k += 8) {
+    const int r = r0 + ty + k, c = c0 + tx;
+    tile[ty + k][tx] = (r < R && c < C) ? pb.src[i][(long)r * C + c] : 0.0f;
+  }
+  __syncthreads();
+  const long plane = (long)R * C;
+  unsigned short* d = reinterpret_cast<unsigned short*>(pb.dst[i]);
+#pragma unroll
+  for (int k = 0; k < 32; k += 8) {
+    // output element (orow, ocol) of the [R'][C'] image
+    const int orow = (pb.tr[i] ? c0 : r0) + ty + k, ocol = (pb.tr[i] ? r0 : c0) + tx;
+    const float v = pb.tr[i] ? tile[tx][ty + k] : tile[ty + k][tx];
+    const int OR = pb.tr[i] ? C : R, OC = pb.tr[i] ? R : C;
+    if (orow < OR && ocol < OC) {
+      unsigned p0, p1, p2;
+      split2(v, 0.0f, p0, p1, p2);
+      const long o = (long)orow * OC + ocol;
+      d[o] = (unsigned short)(p0 & 0xffffu);
+      d[plane + o] = (unsigned short)(p1 & 0xffffu);
+      d[2 * plane + o] = (unsigned short)(p2 & 0xffffu);
+    }
+  }
+}
+
+}  // namespace mrg
+
+using namespace mrg;
+
+// planes of n weights (see split_planes_kernel): dst_i holds 3 x rows_i x cols_i bf16
+MRG_API int mrg_split_planes_batched(int n, const float* const* src, void* const* dst, const int* rows, const int* cols,
+                                     const int* transpose, hipStream_t stream) {
+  MRG_REQUIRE(n >= 0 && (n == 0 || (src && dst && rows && cols && transpose)), "mrg_split_planes_batched: bad arguments");
+  for (int b0 = 0; b0 < n; b0 += MRG_TP_MAX) {
+    PlaneBatch pb;
+    memset(&pb, 0, sizeof(pb));
+    pb.n = n - b0 < MRG_TP_MAX ? n - b0 : MRG_TP_MAX;
+    int blocks = 0;
+    for (int i = 0; i < pb.n; ++i) {
+      MRG_REQUIRE(rows[b0 + i] >= 0 && cols[b0 + i] >= 0, "mrg_split_planes_batched: negative size");
+      pb.src[i] = src[b0 + i]; pb.dst[i] = reinterpret_cast<__bf16*>(dst[b0 + i]);
+      pb.rows[i] = rows[b0 + i]; pb.cols[i] = cols[b0 + i]; pb.tr[i] = transpose[b0 + i] ? 1 : 0;
+      pb.first[i] = blocks;
+      blocks += ((rows[b0 + i] + 31) / 32) * ((cols[b0 + i] + 31) / 32);
+    }
+    pb.first[pb.n] = blocks;
+    if (blocks == 0) continue;
+    split_planes_kernel<<<blocks, 256, 0, stream>>>(pb);
+    if (check_launch("split_planes_kernel")) return 1;
+  }
+  return 0;
+}
+
+// C = epi(alpha A B^T + beta C + bias) with B given as three bf16 planes (mrg_split_planes_batched):
+// B plane p row n at Bplanes + p * bplane + n * ldb (bf16 elements).  A [M][K] rows through the
+// RowMap (lda, lda_hi, a_rdiv).  K % 32 == 0; rows 16-B aligned.  The LDS-DMA x6 kernel with only
+// A split in the loop.
+MRG_API int mrg_gemm_x6_planes(int M, int N, int K, float alpha, const float* A, long lda, long lda_hi, int a_rdiv,
+                               const void* Bplanes, long ldb, long bplane, float beta, float* C, long ldc,
+                               const float* bias, int epilogue, const float* aux, long ldaux, hipStream_t stream) {
+  MRG_REQUIRE(M >= 0 && N >= 0 && K >= 0, "mrg_gemm_x6_planes: negative size");
+  MRG_REQUIRE(K % 32 == 0, "mrg_gemm_x6_planes: K %d not a multiple of 32", K);
+  MRG_REQUIRE(epilogue >= 0 && epilogue <= 3 && (epilogue < 2 || aux), "mrg_gemm_x6_planes: bad epilogue");
+  MRG_REQUIRE((((uintptr_t)A) & 15) == 0 && (lda & 3) == 0 && (a_rdiv <= 0 || (lda_hi & 3) == 0),
+              "mrg_gemm_x6_planes: A rows must be 16-B aligned");
+  MRG_REQUIRE((((uintptr_t)Bplanes) & 15) == 0 && (ldb & 7) == 0 && (bplane & 7) == 0,
+              "mrg_gemm_x6_planes: B plane rows must be 16-B aligned");
+  if (M == 0 || N == 0) return 0;
+  GemmArgs a;
+  memset(&a, 0, sizeof(a));
+  a.M = M; a.N = N; a.K = K; a.alpha = alpha; a.beta = beta;
+  a.A = A; a.amap = RowMap{lda, lda_hi, a_rdiv}; a.transA = 0;
+  a.B = reinterpret_cast<const float*>(Bplanes); a.bmap = RowMap{ldb, 0, 0}; a.transB = 1;
+  a.C = C; a.ldc = ldc; a.bias = bias; a.epi = epilogue; a.aux = aux; a.ldaux = ldaux;
+  a.kchunk = K;
+  a.vec = ((((uintptr_t)C | (uintptr_t)bias | (uintptr_t)aux) & 15) == 0 && (ldc & 3) == 0 &&
+           (!aux || (ldaux & 3) == 0)) ? 1 : 0;
+  int bm = 64, bn = 128;  // the fp32-operand kernel's shape rule (gemm.hip)
+  if (N >= 1024) bm = 128;
+  else if (N <= 256 && K <= 256) bn = 64;
+  launch_shape<1>(a, 2, bm, bn, bplane, stream);
+  return check_launch("gemm_x6g_kernel");
+}

@@ -465,7 +465,7 @@ def _wt_note(w, rows, need=True):
     """Forward side (inside autograd Function.forward: pass ctx.needs_input_grad of the input): w
     [out][in] (a contiguous 2-D view) will serve a dX product over `rows` rows."""
     if not (need and _WT_ON[0] and rows >= _WT_MIN_ROWS and w.shape[1] >= 256 and w.shape[0] % 32 == 0
-            and w.is_contiguous()):
+            and w.is_contiguous()) or _plane_operand(w, True) is not None:
         return
     k = _wt_key(w)
     _WT_CACHE.pop(k, None)
@@ -494,8 +494,109 @@ def _wt(w):
     return _WT_CACHE[k]
 
 
+# --- pre-split weights: the three bf16 planes of every weight (and of its transpose), made once per
+# optimizer step in ONE launch (mrg_split_planes_batched) by prepare_weight_planes at the start of a
+# training forward; the forward products x W^T and the input-gradient products dY W then run on the
+# LDS-DMA x6 kernel with only the activation operand split in the loop (mrg_gemm_x6_planes).  Keyed
+# by the weight's storage; a row slice of a prepared weight (the Q / K,V blocks of in_proj_weight)
+# resolves to its parent's planes.  Opt-in (MRG_WEIGHT_PLANES=1 / set_weight_planes): 3-10 % faster
+# per product in isolation, but the step measured 0.9 ms SLOWER with it (every kernel of the step ran
+# ~3 % slower beside the extra plane traffic), so it is off by default.
+_PL_ON = [os.environ.get("MRG_WEIGHT_PLANES", "0") == "1"]
+_PLANES = {}
+
+
+def set_weight_planes(on: bool) -> bool:
+    prev = _PL_ON[0]
+    _PL_ON[0] = bool(on)
+    if not on:
+        _PLANES.clear()
+    return prev
+
+
+def invalidate_weight_planes():
+    """The weights changed (optimizer step): forget their planes until the next prepare."""
+    _PLANES.clear()
+
+
+def prepare_weight_planes(weights):
+    """Split every 2-D fp32 weight (rows and cols multiples of 32... any size) into bf16 planes, both
+    orientations, in one launch.  Called per step before the forward (the optimizer rewrote them)."""
+    _PLANES.clear()
+    if not (_PL_ON[0] and _ARITH[0] is None and _lib.load().mrg_gemm_get_mode() == 1):
+        return
+    ws = [w for w in weights if w.dim() == 2 and w.is_cuda and w.dtype == torch.float32 and w.is_contiguous()
+          and min(w.shape) >= 32]
+    if not ws:
+        return
+    srcs, dsts, rows, cols, trs = [], [], [], [], []
+    for w in ws:
+        O, I = w.shape
+        pw = torch.empty(3, O, I, device=w.device, dtype=torch.int16)
+        pt = torch.empty(3, I, O, device=w.device, dtype=torch.int16)
+        _PLANES[w.data_ptr()] = (w, pw, pt, w._version)
+        for dst, tr in ((pw, 0), (pt, 1)):
+            srcs.append(_ptr(w)); dsts.append(_ptr(dst)); rows.append(O); cols.append(I); trs.append(tr)
+    n = len(srcs)
+    VP, CI = ctypes.c_void_p, ctypes.c_int
+    _lib.check(_lib.load().mrg_split_planes_batched(n, (VP * n)(*srcs), (VP * n)(*dsts), (CI * n)(*rows),
+                                                    (CI * n)(*cols), (CI * n)(*trs), _stream()), "split planes")
+
+
+def _plane_operand(w, transposed):
+    """(pointer, ldb, plane stride) of the planes of w (or of w^T), w a prepared weight or a row slice
+    of one; None when w has no planes."""
+    if not _PLANES:
+        return None
+    ent = _PLANES.get(w.data_ptr())
+    r0 = 0
+    if ent is None or ent[0].shape[1] != w.shape[1]:
+        ent = None
+        for cand in _PLANES.values():
+            par = cand[0]
+            off = w.data_ptr() - par.data_ptr()
+            if par.shape[1] == w.shape[1] and 0 <= off < par.numel() * 4 and off % (4 * par.shape[1]) == 0:
+                ent, r0 = cand, off // (4 * par.shape[1])
+                break
+        if ent is None:
+            return None
+    par, pw, pt, ver = ent
+    if par._version != ver:   # rewritten through torch since the split: stale
+        return None
+    O, I = par.shape
+    if not transposed:   # rows r0.. of W: [rows][I]
+        return ctypes.c_void_p(pw.data_ptr() + 2 * r0 * I), I, O * I
+    return ctypes.c_void_p(pt.data_ptr() + 2 * r0), O, I * O   # columns r0.. of W^T: [I][O]
+
+
+def _planes_gemm(M, N, K, A, lda, planes, C, ldc, *, beta=0.0, bias=None, epi=0, aux=None, ldaux=0, a_hi=0,
+                 a_div=0, device=None):
+    bp, ldb, bplane = planes
+    with _probe("gemm", 2.0 * M * N * K):
+        rc = _lib.load().mrg_gemm_x6_planes(M, N, K, 1.0, A, lda, a_hi, a_div, bp, ldb, bplane, beta, C, ldc, bias,
+                                           epi, aux, ldaux, _stream())
+    _lib.check(rc, "gemm (weight planes)")
+
+
+def _fwd_gemm(M, N, K, A, lda, w, C, ldc, **kw):
+    """C[M, N] = epi(A[M, K] w[N, K]^T ...): on the weight planes when w has them."""
+    pl = _plane_operand(w, False) if (M >= _WT_MIN_ROWS and K % 32 == 0 and _ARITH[0] is None) else None
+    if pl is not None:
+        kw.pop("device", None)
+        _planes_gemm(M, N, K, A, lda, pl, C, ldc, **kw)
+    else:
+        gemm(M, N, K, A, 0, lda, _ptr(w), 1, K, C, ldc, **kw)
+
+
 def _dx_gemm(M, In, N, dY, ldy, w, dx, ldx, **kw):
-    """dx[M, In] = epi(dY[M, N] w[N, In] ...): through w's [in][out] copy when one exists."""
+    """dx[M, In] = epi(dY[M, N] w[N, In] ...): on the planes of w^T, else through w's [in][out] copy
+    when one exists, else reading w along n."""
+    if M >= _WT_MIN_ROWS and N % 32 == 0 and _ARITH[0] is None:
+        pl = _plane_operand(w, True)
+        if pl is not None:
+            kw.pop("device", None)
+            _planes_gemm(M, In, N, dY, ldy, pl, dx, ldx, **kw)
+            return
     wt = _wt(w) if M >= _WT_MIN_ROWS else None
     if wt is not None:
         gemm(M, In, N, dY, 0, ldy, _ptr(wt), 1, N, dx, ldx, **kw)
@@ -513,7 +614,7 @@ class _LinearFn(Function):
         x2 = x.reshape(-1, In).contiguous()
         M = x2.shape[0]
         y = torch.empty(M, N, device=x.device, dtype=torch.float32)
-        gemm(M, N, In, _ptr(x2), 0, In, _ptr(w), 1, In, _ptr(y), N, bias=_ptr(b), device=x.device)
+        _fwd_gemm(M, N, In, _ptr(x2), In, w, _ptr(y), N, bias=_ptr(b), device=x.device)
         _wt_note(w, M, ctx.needs_input_grad[0])
         ctx.save_for_backward(x2, w, b)
         ctx.xshape = x.shape
@@ -553,7 +654,7 @@ class _FFNFn(Function):
         h = torch.empty(M, Hb, device=dev, dtype=torch.float32)
         gemm(M, Hb, In, _ptr(x2), 0, In, _ptr(w1), 1, In, _ptr(h), Hb, bias=_ptr(b1), epi=1, device=dev)
         z = torch.empty(M, N, device=dev, dtype=torch.float32)
-        gemm(M, N, Hb, _ptr(h), 0, Hb, _ptr(w2), 1, Hb, _ptr(z), N, bias=_ptr(b2), device=dev)
+        _fwd_gemm(M, N, Hb, _ptr(h), Hb, w2, _ptr(z), N, bias=_ptr(b2), device=dev)
         _wt_note(w1, M, ctx.needs_input_grad[0])
         ctx.save_for_backward(x2, h, w1, b1, w2, b2)
         ctx.xshape = x.shape
@@ -671,7 +772,7 @@ class _LinResLNFn(Function):
         x2 = x.reshape(-1, E).contiguous()
         M = x2.shape[0]
         z = torch.empty(M, E, device=x.device, dtype=torch.float32)
-        gemm(M, E, E, _ptr(x2), 0, E, _ptr(w), 1, E, _ptr(z), E, bias=_ptr(b), device=x.device)
+        _fwd_gemm(M, E, E, _ptr(x2), E, w, _ptr(z), E, bias=_ptr(b), device=x.device)
         _wt_note(w, M, ctx.needs_input_grad[0])
         y, mean, rstd = _resln_fwd(z, x2, gamma, beta, eps)
         ctx.save_for_backward(x2, w, b, z, gamma, beta, mean, rstd)
@@ -712,7 +813,7 @@ class _FFNResLNFn(Function):
         h = torch.empty(M, Hb, device=dev, dtype=torch.float32)
         gemm(M, Hb, E, _ptr(x2), 0, E, _ptr(w1), 1, E, _ptr(h), Hb, bias=_ptr(b1), epi=1, device=dev)
         z = torch.empty(M, E, device=dev, dtype=torch.float32)
-        gemm(M, E, Hb, _ptr(h), 0, Hb, _ptr(w2), 1, Hb, _ptr(z), E, bias=_ptr(b2), device=dev)
+        _fwd_gemm(M, E, Hb, _ptr(h), Hb, w2, _ptr(z), E, bias=_ptr(b2), device=dev)
         _wt_note(w1, M, ctx.needs_input_grad[0])
         y, mean, rstd = _resln_fwd(z, x2, gamma, beta, eps)
         ctx.save_for_backward(x2, h, z, w1, b1, w2, b2, gamma, beta, mean, rstd)
@@ -776,8 +877,7 @@ class _LSTMFn(Function):
             x, w_ih, b_ih = xs[i], p[1], p[3]
             In_i = x.shape[2]
             gx = torch.empty(B, T, 4 * H, device=dev, dtype=torch.float32)
-            gemm(B * T, 4 * H, In_i, _ptr(x), 0, In_i, _ptr(w_ih), 1, In_i, _ptr(gx), 4 * H,
-                 bias=_ptr(b_ih), device=dev)
+            _fwd_gemm(B * T, 4 * H, In_i, _ptr(x), In_i, w_ih, _ptr(gx), 4 * H, bias=_ptr(b_ih), device=dev)
             _wt_note(w_ih, B * T, ctx.needs_input_grad[1 + K * i])
             gxs.append(gx)
             if concat:
@@ -1200,10 +1300,9 @@ class _MHAFn(Function):
         q2 = q_in.contiguous()
         kv2 = kv_in.contiguous()
         Q = torch.empty(B, Tq, E, device=dev, dtype=torch.float32)
-        gemm(B * Tq, E, E, _ptr(q2), 0, E, _ptr(in_w), 1, E, _ptr(Q), E, bias=_ptr(in_b), device=dev)
+        _fwd_gemm(B * Tq, E, E, _ptr(q2), E, in_w[:E], _ptr(Q), E, bias=_ptr(in_b), device=dev)
         KV = torch.empty(B, Tk, 2 * E, device=dev, dtype=torch.float32)
-        gemm(B * Tk, 2 * E, E, _ptr(kv2), 0, E, _ptr(in_w, E * E), 1, E, _ptr(KV), 2 * E,
-             bias=_ptr(in_b, E), device=dev)
+        _fwd_gemm(B * Tk, 2 * E, E, _ptr(kv2), E, in_w[E:], _ptr(KV), 2 * E, bias=_ptr(in_b, E), device=dev)
         O = torch.empty(B, Tq, E, device=dev, dtype=torch.float32)
         lse = torch.empty(B, heads, Tq, device=dev, dtype=torch.float32)
         scale = 1.0 / math.sqrt(D)
@@ -1215,7 +1314,7 @@ class _MHAFn(Function):
                                        _stream())
         _lib.check(rc, "attention fwd")
         out = torch.empty(B, Tq, E, device=dev, dtype=torch.float32)
-        gemm(B * Tq, E, E, _ptr(O), 0, E, _ptr(out_w), 1, E, _ptr(out), E, bias=_ptr(out_b), device=dev)
+        _fwd_gemm(B * Tq, E, E, _ptr(O), E, out_w, _ptr(out), E, bias=_ptr(out_b), device=dev)
         need_in = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
         _wt_note(out_w, B * Tq, need_in)
         _wt_note(in_w[:E], B * Tq, ctx.needs_input_grad[1])

@@ -225,6 +225,10 @@ class Metaformer(LightningSurface):
         mp = _cat_lead(leading_motion_partner[0].to(dev), motion_partner[0].to(dev))
         ms = _cat_lead(leading_motion_self[0].to(dev), motion_self[0].to(dev))
         T = mp.shape[1]
+        if torch.is_grad_enabled() and mp.shape[0] * T >= 2048:
+            # a training forward over whole sequences: the bf16 planes of every weight, once per step
+            # (functional.prepare_weight_planes; per-frame decode forwards keep the step's planes)
+            Fn.prepare_weight_planes(self.parameters())
         mm = gen_attention_mask(ms, mp, self.num_heads, PADDING_VALUE).view(-1, T, T)
         ma = gen_attention_mask(ms, a, self.num_heads, PADDING_VALUE).view(-1, T, a.shape[1])
         self_masks = [gen_attention_mask(x, x, self.num_heads, PADDING_VALUE) if t == "mha" else None

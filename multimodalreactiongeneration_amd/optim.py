@@ -117,6 +117,8 @@ class FusedAdamW(torch.optim.Optimizer):
             _ptr(self.flat), _ptr(self.flat_grad), _ptr(self.exp_avg), _ptr(self.exp_avg_sq),
             self.flat.numel(), _ptr(self.step_lr), float(g["weight_decay"]), float(b1), float(b2),
             float(g["eps"]), _ptr(_err_flag(self.flat.device)), _stream()), "adamw")
+        from . import functional as Fn
+        Fn.invalidate_weight_planes()  # the weights changed: their bf16 planes are stale
         return loss
 
     def zero_grad(self, set_to_none: bool = False):

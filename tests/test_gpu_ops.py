@@ -149,6 +149,48 @@ def test_glds_gemm_vs_fp64(M, N, K, epi, rowmap, depth, bn):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("M,N,K", [(19200, 256, 256), (4096, 1024, 256), (2100, 512, 96)])
+def test_weight_planes_linear_vs_fp64(M, N, K):
+    """Pre-split weights (prepare_weight_planes: three bf16 planes of W and of W^T in one launch) feed
+    the forward product x W^T and the input-gradient product dY W (mrg_gemm_x6_planes); the weight
+    gradient stays on the fp32-operand path.  All against fp64; planes dropped after the optimizer
+    would have run (invalidate) and when the weight is rewritten through torch (version check)."""
+    from multimodalreactiongeneration_amd import functional as Fn
+    g = torch.Generator().manual_seed(M + N + K)
+    x = torch.randn(M, K, generator=g)
+    w = torch.randn(N, K, generator=g) / math.sqrt(K)
+    b = torch.randn(N, generator=g)
+    dy = torch.randn(M, N, generator=g)
+    xd = x.to(DEV).requires_grad_(True)
+    wd, bd = _param(w), _param(b)
+    prev = Fn.set_weight_planes(True)
+    try:
+        Fn.prepare_weight_planes([wd])
+        assert Fn._plane_operand(wd, False) is not None and Fn._plane_operand(wd, True) is not None
+        y = Fn.linear(xd, wd, bd)
+        y.backward(dy.to(DEV))
+        torch.cuda.synchronize()
+    finally:
+        Fn.set_weight_planes(prev)
+    xr = x.double().requires_grad_(True)
+    wr = w.double().requires_grad_(True)
+    yr = torch.nn.functional.linear(xr, wr, b.double())
+    yr.backward(dy.double())
+    assert rel_err(y, yr) < 2e-6
+    assert rel_err(xd.grad, xr.grad) < 2e-6
+    assert rel_err(wd.grad, wr.grad) < 2e-6
+    Fn.set_weight_planes(True)
+    try:
+        Fn.prepare_weight_planes([wd])
+        with torch.no_grad():
+            wd.mul_(2.0)   # rewritten through torch: the planes are stale and must not be used
+        assert Fn._plane_operand(wd, False) is None
+        Fn.invalidate_weight_planes()
+        assert not Fn._PLANES
+    finally:
+        Fn.set_weight_planes(prev)
+
+
 @pytest.mark.parametrize("M,N,K,transB,a_off", [
     (64, 256, 1024, 0, 0), (64, 128, 512, 1, 0), (37, 96, 516, 0, 0), (64, 256, 1024, 1, 1), (50, 40, 64, 1, 3)])
 def test_few_row_gemm_operand_layouts(M, N, K, transB, a_off):

@@ -53,7 +53,14 @@ def run_shape(M, N, K, ta, tb, wgrad, iters=20):
     ldb = B.shape[1]
     splits = Fn.wgrad_splits(M, N, K) if wgrad else 1
 
+    planes = os.environ.get("MRG_BENCH_PLANES") == "1" and not ta and tb and not wgrad
+    if planes:   # B as a weight [N][K] with its bf16 planes (functional.prepare_weight_planes)
+        Fn.prepare_weight_planes([B])
+
     def go():
+        if planes:
+            Fn._fwd_gemm(M, N, K, Fn._ptr(A), lda, B, Fn._ptr(C), N, device=A.device)
+            return
         Fn.gemm(M, N, K, Fn._ptr(A), ta, lda, Fn._ptr(B), tb, ldb, Fn._ptr(C), N,
                 beta=1.0 if wgrad else 0.0, splits=splits, device=A.device)
     go()
