@@ -36,7 +36,8 @@ PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_pmc_summary.json")
 
 # probe name (functional._probe) -> kernels it brackets; FLOPs are algorithmic
 FAMILIES = {
-    "gemm": "gemm_x6_kernel (+ splitk_reduce4_kernel): every GEMM of the step, 2MNK FLOP per launch",
+    "gemm": "gemm_x6g_kernel (LDS-DMA, activation and input-gradient products) + gemm_x6_kernel (weight gradients, "
+            "+ splitk_reduce4_kernel): every GEMM of the step, 2MNK FLOP per launch",
     "lstm_fwd": "lstm_fwd_kernel<256,8,BS>: persistent recurrence, 8H^2 FLOP per (b, t) per layer",
     "lstm_bwd": "lstm_bwd_kernel<256,8,BS>: persistent reverse recurrence, 8H^2 FLOP per (b, t) per layer",
     "attn_fwd": "attn_fwd_kernel<64>: block-causal flash attention, 4D FLOP per visible (q, k) pair per head",
@@ -49,7 +50,7 @@ PEAK_NOTES = {
     "lstm_bwd": "latency-bound (one cross-CU hand-off per time step); VALU v_pk_fma_f32 peak = 157.3",
 }
 # rocprofv3 kernel-name prefix of each family in the PMC summary (tools/tools_pmc_summary.py)
-PMC_KEYS = {"gemm": "gemm_x6_kernel", "lstm_fwd": "lstm_fwd_kernel", "lstm_bwd": "lstm_bwd_kernel",
+PMC_KEYS = {"gemm": "gemm_all", "lstm_fwd": "lstm_fwd_kernel", "lstm_bwd": "lstm_bwd_kernel",
             "attn_fwd": "attn_fwd_kernel", "attn_bwd": "attn_bwd"}
 
 

@@ -1,6 +1,6 @@
 """Summarise rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools_pmc.sh) into per-kernel HBM bytes per launch.
 
-    python tools/tools_pmc_summary.py gpurun_out/pmc profiles/r01_pmc_summary.json
+    python tools/tools_pmc_summary.py gpurun_out/r02/pmc profiles/r02_pmc_summary.json
 
 Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE (KiB) is doubled on gfx950
 (it tallies 128-B requests at 64 B); WRITE_SIZE is taken as is.
@@ -46,7 +46,8 @@ for k in sorted(set(fetch) | set(write)):
 
 
 def fam_total(prefix):
-    ks = [k for k in summary if k.startswith(prefix)]
+    prefixes = (prefix,) if isinstance(prefix, str) else prefix
+    ks = [k for k in summary if k.startswith(prefixes)]
     n = sum(summary[k]["dispatches"] for k in ks)
     if not n:
         return None
@@ -56,8 +57,10 @@ def fam_total(prefix):
 
 doc = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) over "
                  "`bench.py --graph 0 --cpu-baseline 0 --steps 1 --warmup 1`; FETCH_SIZE x2 (gfx950 correction)",
-       "families": {p: fam_total(p) for p in ("lstm_fwd_kernel", "lstm_bwd_kernel", "gemm_x6_kernel", "gemm_f32_kernel", "splitk_reduce",
-                                              "attn_fwd_kernel", "attn_bwd", "resln", "adamw_kernel")},
+       "families": dict({p: fam_total(p) for p in ("lstm_fwd_kernel", "lstm_bwd_kernel", "gemm_x6_kernel", "gemm_f32_kernel",
+                                                   "splitk_reduce", "attn_fwd_kernel", "attn_bwd", "resln",
+                                                   "adamw_kernel")},
+                        gemm_all=fam_total(("gemm_x6_kernel", "gemm_x6g_kernel", "gemm_rows_kernel"))),
        "kernels": summary}
 txt = json.dumps(doc, indent=1)
 if dst:

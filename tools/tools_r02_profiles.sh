@@ -20,7 +20,7 @@ for c in FETCH_SIZE WRITE_SIZE; do
     > $O/pmc_$c.log 2>&1 || { echo "pmc $c failed"; tail -20 $O/pmc_$c.log; exit 1; }
   echo "pmc $c ok"
 done
-[ -x $R/tools/pmc_calib ] && for c in FETCH_SIZE WRITE_SIZE; do
+for c in $([ -x $R/tools/pmc_calib ] && echo FETCH_SIZE WRITE_SIZE); do
   timeout -k 10 120 rocprofv3 --pmc $c -d $O/calib/$c -o pmc --output-format csv -- $R/tools/pmc_calib \
     > $O/calib_$c.log 2>&1 || { echo "calib $c failed"; tail -20 $O/calib_$c.log; exit 1; }
   echo "calib $c ok"
