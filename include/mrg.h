@@ -55,6 +55,9 @@ int mrg_gemm_set_blocks_per_cu(int n);
  * >= 2048 rows, >= 256 columns): ring depth 2..4 (0 = off; default 2, MRG_GEMM_GLDS) and column
  * tile (64 forces 64-wide tiles, 128 = by shape).                                               */
 int mrg_gemm_set_glds(int depth, int bn);
+/* Weight-gradient products (transA 1, transB 0) on the LDS-DMA kernel (1, default) or the
+ * register-staged one (0); returns the previous setting.                                        */
+int mrg_gemm_set_glds_wg(int on);
 /* dst_i [cols_i][rows_i] = src_i [rows_i][cols_i]^T for n row-major fp32 matrices (host arrays of
  * device pointers and sizes), one launch per 32 matrices: the [in][out] weight copies that let the
  * input-gradient products dY W run k-contiguous (nn.Linear / LSTM backward, mixer_block.py:63-74).*/

@@ -867,6 +867,10 @@ static int g_glds = [] {
   const char* e = getenv("MRG_GEMM_GLDS");
   return e ? atoi(e) : 2;
 }();
+static int g_glds_wg = [] {  // weight-gradient products on gemm_x6g_wgrad_kernel (MRG_GEMM_GLDS_WG=0: off)
+  const char* e = getenv("MRG_GEMM_GLDS_WG");
+  return e ? atoi(e) : 1;
+}();
 static int g_glds_bn = [] {  // 64 forces 64-wide column tiles (tuning); 128 = by shape
   const char* e = getenv("MRG_GEMM_GLDS_BN");
   return e ? atoi(e) : 128;
@@ -920,6 +924,13 @@ MRG_API int mrg_gemm_set_mode(int mode) {
   return 0;
 }
 MRG_API int mrg_gemm_get_mode(void) { return g_gemm_mode; }
+
+// Weight-gradient products on the LDS-DMA kernel (1) or the register-staged one (0); returns the old value.
+MRG_API int mrg_gemm_set_glds_wg(int on) {
+  const int prev = g_glds_wg;
+  g_glds_wg = on ? 1 : 0;
+  return prev;
+}
 
 // LDS-DMA x6 kernel for k-contiguous products: ring depth 2..4 (0 = off) and column tile (64 forces
 // 64-wide tiles; 128 = the shape heuristic).
@@ -1097,7 +1108,15 @@ static int gemm_ex(int mode, int M, int N, int K, float alpha,
     const long tiles = (long)((M + 63) / 64) * ((N + 63) / 64);
     if (tiles <= MRG_GEMM_COUNTERS && (long)splits * 64 * 64 * 4 <= 65536) a.cnt = counters;
   }
-  if (launch_gemm(mode, a, tile, bk, transA, transB, va, vb, splits, stream)) return 2;
+  // weight gradients (dY^T X) on the LDS-DMA kernel: k-strided operands, split-K slabs, fused row sums
+  const bool wg = mode == 1 && g_glds_wg && g_tile_override < 0 && transA && !transB && va && vb && K > 0 &&
+                  (K % 32) == 0 && (M % 4) == 0 && (N % 4) == 0 && M >= 64 && N >= 64 && !a.cnt;
+  if (wg) {
+    tile = 0;
+    launch_x6g_wgrad(a, splits, 128, 128, stream);
+  } else if (launch_gemm(mode, a, tile, bk, transA, transB, va, vb, splits, stream)) {
+    return 2;
+  }
   if (check_launch("gemm_f32_kernel")) return 1;
   // unsplit 64x64-tile GEMM (x6): its n0 == 0 tiles wrote asum_out directly
   bool asum_done = splits == 1 && tile == 2 && mx;

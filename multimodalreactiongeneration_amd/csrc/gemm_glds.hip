@@ -36,6 +36,13 @@ __device__ __forceinline__ f32x4v_ lds_read16(unsigned addr) {
   return v;
 }
 
+// 4-B LDS read the compiler does not track (see gemm_x6g_kernel); the caller waits lgkmcnt
+__device__ __forceinline__ float lds_read4(unsigned addr) {
+  float v;
+  asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(addr) : "memory");
+  return v;
+}
+
 // 8 consecutive-k fp32 -> three bf16x8 planes (v = p0 + p1 + p2 + r, |r| <= 2^-24 |v|)
 __device__ __forceinline__ void split8(f32x4v_ v0, f32x4v_ v1, bf16x8 (&f)[3]) {
   unsigned a0, a1, a2, b0, b1, b2, c0, c1, c2, d0, d1, d2;
@@ -259,6 +266,197 @@ static void launch_shape(GemmArgs a, int ns, int bm, int bn, long bplane, hipStr
 }
 
 void launch_x6g(GemmArgs a, int ns, int bm, int bn, hipStream_t s) { launch_shape<0>(a, ns, bm, bn, 0, s); }
+
+
+// ----------------------------------------------------------------------------------------------
+// Weight-gradient form (transA = 1, transB = 0): C[m][n] = sum_k A[k][m] B[k][n] over the B*T rows
+// k (dW = dY^T X), split over K (fp32 slabs, ordered reduce) and with the bias gradient (row sums
+// of A over k) fused.  Both operands are k-strided: a ring slot holds A [32 k][BM] and B [32 k][BN]
+// fp32 rows as they lie in memory (one DMA wave-instruction = 1 KB = 1024 / (4 X) k-rows), and a
+// fragment (8 consecutive k of one m) is 8 ds_read_b32; the 16-B chunk of row k sits at chunk
+// c ^ 8 ((k >> 3) & 1) (source swizzle), so the two half-waves (rows k and k + 8) hit opposite
+// bank halves.  K % 32 == 0 and M, N multiples of 4 (clamped chunk reads past the tile edge).
+template <int X>
+__device__ __forceinline__ int wg_off(int k, int c) {  // byte offset of chunk c of k-row k, X floats per row
+  return k * X * 4 + ((c ^ (((k >> 3) & 1) << 3)) << 4);
+}
+
+template <int BM, int BN, int NS>
+__global__ __launch_bounds__(NT, 1) void gemm_x6g_wgrad_kernel(GemmArgs a) {
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int SA = 32 * BM * 4, SS = SA + 32 * BN * 4;
+  constexpr int GA = SA / 4096, GB = (32 * BN * 4) / 4096;  // 1-KB DMA instructions per wave per k-tile
+  constexpr int GT = GA + GB;
+  constexpr int RA = 1024 / (BM * 4), RB = 1024 / (BN * 4);  // k-rows per DMA instruction
+  static_assert(NS >= 2 && NS <= 4 && (BM == 64 || BM == 128) && (BN == 64 || BN == 128), "wgrad tile");
+  __shared__ __attribute__((aligned(16))) unsigned char lds[NS * SS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = (wave >> 1) * (BM / 2), wn = (wave & 1) * (BN / 2);
+  const int lr = lane & 31, lh = lane >> 5;
+  const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int z = t / a.tiles_mn, tr = t - z * a.tiles_mn;
+  const int m0 = (tr / a.tiles_n) * BM, n0 = (tr % a.tiles_n) * BN;
+  const int kbeg = z * a.kchunk, kend = min(a.K, kbeg + a.kchunk);
+  const int nk = (kend - kbeg) / 32;
+
+  const float* src[GT];
+  long rstep[GT];  // not used: rows advance through the RowMap per k-tile
+  int kk[GT], dsto[GT];
+#pragma unroll
+  for (int g = 0; g < GT; ++g) {
+    if (g < GA) {
+      const int grp = wave * GA + g, k = grp * RA + lane / (BM / 4), c = lane % (BM / 4);
+      const int chunk = c ^ (((k >> 3) & 1) << 3);
+      src[g] = a.A + min(m0 + 4 * chunk, a.M - 4);
+      kk[g] = k;
+      dsto[g] = grp << 10;
+    } else {
+      const int grp = wave * GB + (g - GA), k = grp * RB + lane / (BN / 4), c = lane % (BN / 4);
+      const int chunk = c ^ (((k >> 3) & 1) << 3);
+      src[g] = a.B + min(n0 + 4 * chunk, a.N - 4);
+      kk[g] = k;
+      dsto[g] = SA + (grp << 10);
+    }
+    rstep[g] = 0;
+  }
+  (void)rstep;
+  auto issue = [&](int kt, int slot) {
+#pragma unroll
+    for (int g = 0; g < GT; ++g) {
+      const int k = kbeg + kt * 32 + kk[g];
+      const float* p = src[g] + (g < GA ? a.amap.off(k) : a.bmap.off(k));
+      __builtin_amdgcn_global_load_lds((const void*)p, (__attribute__((address_space(3))) void*)(lds + slot * SS + dsto[g]),
+                                       16, 0, 0);
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+  const bool do_asum = a.asum && n0 == 0 && (wave & 1) == 0;
+  float cs[TM] = {};
+  const unsigned lds_base = (unsigned)(uintptr_t)((__attribute__((address_space(3))) unsigned char*)lds);
+
+#pragma unroll
+  for (int st = 0; st < NS - 1; ++st)
+    if (st < nk) issue(st, st);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int ahead = min(NS - 2, nk - 1 - kt);
+    if (ahead >= 2) vm_wait<2 * GT>();
+    else if (ahead == 1) vm_wait<GT>();
+    else vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    if (kt + NS - 1 < nk) issue(kt + NS - 1, (kt + NS - 1) % NS);
+    const unsigned sa = lds_base + (kt % NS) * SS;
+    const unsigned sb = sa + SA;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float va[TM][8], vb[TN][8];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = wm + 32 * i + lr;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) va[i][j] = lds_read4(sa + wg_off<BM>(16 * s + 8 * lh + j, m >> 2) + 4 * (m & 3));
+      }
+#pragma unroll
+      for (int jj = 0; jj < TN; ++jj) {
+        const int n = wn + 32 * jj + lr;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) vb[jj][j] = lds_read4(sb + wg_off<BN>(16 * s + 8 * lh + j, n >> 2) + 4 * (n & 3));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      bf16x8 fa[TM][3], fb[TN][3];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        if (do_asum)
+          cs[i] += ((va[i][0] + va[i][1]) + (va[i][2] + va[i][3])) + ((va[i][4] + va[i][5]) + (va[i][6] + va[i][7]));
+        split8(f32x4v_{va[i][0], va[i][1], va[i][2], va[i][3]}, f32x4v_{va[i][4], va[i][5], va[i][6], va[i][7]}, fa[i]);
+      }
+#pragma unroll
+      for (int jj = 0; jj < TN; ++jj)
+        split8(f32x4v_{vb[jj][0], vb[jj][1], vb[jj][2], vb[jj][3]}, f32x4v_{vb[jj][4], vb[jj][5], vb[jj][6], vb[jj][7]},
+               fb[jj]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][2], fa[i][0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][1], fa[i][1], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][0], fa[i][2], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][1], fa[i][0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][0], fa[i][1], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][0], fa[i][0], acc[i][j], 0, 0, 0);
+        }
+    }
+  }
+  if (do_asum) {  // lanes l and l + 32 hold the two k halves of row m = wm + 32 i + (l & 31)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const float v = cs[i] + __shfl_xor(cs[i], 32, 64);
+      const int m = m0 + wm + 32 * i + lr;
+      if (lh == 0 && m < a.M) a.asum[(long)z * a.M + m] = v;
+    }
+  }
+  __syncthreads();
+  if constexpr (BN >= 128) {
+    constexpr int WC = TN * 32, PITCH = WC + 4, C4 = WC / 4;
+    float* stg = reinterpret_cast<float*>(lds) + wave * 32 * PITCH;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4)
+          *reinterpret_cast<float4*>(stg + lr * PITCH + j * 32 + 8 * r4 + 4 * lh) =
+              make_float4(acc[i][j][4 * r4], acc[i][j][4 * r4 + 1], acc[i][j][4 * r4 + 2], acc[i][j][4 * r4 + 3]);
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int it = 0; it < 32 * C4 / 64; ++it) {
+        const int qq = lane + 64 * it, row = qq / C4, c4 = qq % C4;
+        const float4 v = *reinterpret_cast<const float4*>(stg + row * PITCH + 4 * c4);
+        const int m = m0 + wm + i * 32 + row;
+        if (m < a.M) store4(a, z, m, n0 + wn + 4 * c4, v);
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wm + i * 32 + lr;
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) {
+          const int n = n0 + wn + j * 32 + 8 * r4 + 4 * lh;
+          const float4 v = make_float4(acc[i][j][4 * r4], acc[i][j][4 * r4 + 1], acc[i][j][4 * r4 + 2],
+                                       acc[i][j][4 * r4 + 3]);
+          if (m < a.M) store4(a, z, m, n, v);
+        }
+    }
+  }
+}
+
+void launch_x6g_wgrad(GemmArgs a, int splits, int bm, int bn, hipStream_t s) {
+  auto go = [&](auto kern, int BM_, int BN_) {
+    a.tiles_n = (a.N + BN_ - 1) / BN_;
+    a.tiles_mn = a.tiles_n * ((a.M + BM_ - 1) / BM_);
+    a.ntiles = a.tiles_mn * splits;
+    a.nsplit = splits;
+    kern<<<(unsigned)a.ntiles, NT, 0, s>>>(a);
+  };
+  if (bm == 64 && bn == 64) go(gemm_x6g_wgrad_kernel<64, 64, 2>, 64, 64);
+  else if (bm == 64) go(gemm_x6g_wgrad_kernel<64, 128, 2>, 64, 128);
+  else if (bn == 64) go(gemm_x6g_wgrad_kernel<128, 64, 2>, 128, 64);
+  else go(gemm_x6g_wgrad_kernel<128, 128, 2>, 128, 128);
+}
 
 // ----------------------------------------------------------------------------------------------
 // Batched transpose: dst_i [cols_i][rows_i] = src_i [rows_i][cols_i]^T for up to MRG_TP_MAX

@@ -191,6 +191,50 @@ def test_weight_planes_linear_vs_fp64(M, N, K):
         Fn.set_weight_planes(prev)
 
 
+@pytest.mark.parametrize("wg", [1, 0], ids=["glds", "regstaged"])
+@pytest.mark.parametrize("rows,N,In,time_shift", [(19200, 1024, 256, False), (64 * 299, 1024, 256, True),
+                                                  (19200, 256, 256, False), (2048, 100, 36, False)])
+def test_weight_grad_kernels_vs_fp64(rows, N, In, time_shift, wg):
+    """Weight gradients dW += dY^T X with the fused bias sums, on the LDS-DMA weight-gradient kernel
+    (gemm_x6g_wgrad_kernel: k-strided operands through the DMA ring, split-K slabs) and on the
+    register-staged one, against fp64; the time-shifted form (dY rows t >= 1 against X rows t - 1 of
+    [B, T] tensors, dW_hh) reads both operands through RowMaps."""
+    from multimodalreactiongeneration_amd import functional as Fn
+    g = torch.Generator().manual_seed(rows + N + In + wg)
+    if time_shift:
+        B_, T_ = 64, 300
+        dy_full = torch.randn(B_, T_, N, generator=g)
+        x_full = torch.randn(B_, T_, In, generator=g)
+        dy = dy_full[:, 1:].reshape(-1, N)
+        x = x_full[:, :-1].reshape(-1, In)
+        dyd, xd = dy_full.to(DEV), x_full.to(DEV)
+        kw = dict(dy_hi=T_ * N, dy_div=T_ - 1, x_hi=T_ * In, x_div=T_ - 1)
+        dyp, xp = Fn._ptr(dyd, N), Fn._ptr(xd)
+    else:
+        dy = torch.randn(rows, N, generator=g)
+        x = torch.randn(rows, In, generator=g)
+        dyd, xd = dy.to(DEV), x.to(DEV)
+        kw = {}
+        dyp, xp = Fn._ptr(dyd), Fn._ptr(xd)
+    gw0 = torch.randn(N, In, generator=g)
+    gb0 = torch.randn(N, generator=g)
+    gw, gb = gw0.to(DEV), gb0.to(DEV)
+    from multimodalreactiongeneration_amd import _lib as L
+    lib = L.load()
+    prev = Fn.set_wgrad_stream(False)
+    try:
+        old = lib.mrg_gemm_set_glds_wg(wg)
+        Fn._wgrad(dyp, N, xp, In, dy.shape[0], N, In, gw, DEV, gb=gb, keep=(dyd, xd), **kw)
+        torch.cuda.synchronize()
+        lib.mrg_gemm_set_glds_wg(old)
+    finally:
+        Fn.set_wgrad_stream(prev)
+    ref_w = gw0.double() + dy.double().t() @ x.double()
+    ref_b = gb0.double() + dy.double().sum(0)
+    assert rel_err(gw, ref_w) < 2e-6
+    assert rel_err(gb, ref_b) < 2e-6
+
+
 @pytest.mark.parametrize("M,N,K,transB,a_off", [
     (64, 256, 1024, 0, 0), (64, 128, 512, 1, 0), (37, 96, 516, 0, 0), (64, 256, 1024, 1, 1), (50, 40, 64, 1, 3)])
 def test_few_row_gemm_operand_layouts(M, N, K, transB, a_off):
