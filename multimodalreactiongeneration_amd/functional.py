@@ -230,6 +230,9 @@ def act_splits(M, N, K):
     return int(max(1, min(4, K // 64, 128 // tiles)))
 
 
+_WG_TARGET = int(os.environ.get("MRG_WGRAD_TARGET_WG", "512"))  # workgroups a weight-gradient product aims at
+
+
 def wgrad_splits(M, N, K):
     """split-K factor for weight-gradient GEMMs (small M x N output, long B*T reduction).
 
@@ -238,7 +241,7 @@ def wgrad_splits(M, N, K):
     """
     if _lib.load().mrg_gemm_get_mode() == 1 or _ARITH[0] == "bf16":
         tiles = ((M + 127) // 128) * ((N + 127) // 128)
-        s = max(1, 512 // max(1, tiles))
+        s = max(1, _WG_TARGET // max(1, tiles))
         return int(max(1, min(s, K // 128, 128)))
     tiles = ((M + 63) // 64) * ((N + 63) // 64)
     s = max(1, 512 // max(1, tiles))
