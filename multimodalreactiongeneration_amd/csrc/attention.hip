@@ -176,7 +176,6 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   using C = AttnCfg<D>;
   __shared__ __attribute__((aligned(16))) float Ks[TT * C::SA];
   __shared__ __attribute__((aligned(16))) float Vs[TT * C::SV];
-  __shared__ unsigned char Kp[TT];
   // grid (heads, B, query blocks), the last (most keys under the causal mask) dispatched first
   const int h = blockIdx.x, b = blockIdx.y;
   const int q0 = (gridDim.z - 1 - blockIdx.z) * 64;
@@ -203,18 +202,22 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   const int klim = key_bound(a, q0 + 63);
   const float* kb_ = a.k + (long)b * a.k_bs + hoff;
   const float* vb_ = a.v + (long)b * a.v_bs + hoff;
+  const unsigned char* kpb = pad ? a.kpad + (long)b * a.Tk : nullptr;
   TileRegs<D> tk, tv;
   tk.load(kb_, a.k_ts, 0, a.Tk);
   tv.load(vb_, a.v_ts, 0, a.Tk);
+  unsigned char kpn = (pad && lane < a.Tk) ? kpb[lane] : 0;  // padding flag of key k0 + lane
   for (int k0 = 0; k0 < klim; k0 += TT) {
     __syncthreads();
     tk.template store<C::SA>(Ks);
     tv.template store<C::SV>(Vs);
-    if (pad && threadIdx.x < TT) Kp[threadIdx.x] = (k0 + threadIdx.x < a.Tk) ? a.kpad[(long)b * a.Tk + k0 + threadIdx.x] : 0;
+    const unsigned long long kbits = __ballot(kpn != 0);
+    const unsigned long long qmask = qp ? kbits : 0ull;  // keys of this tile padding hides from query qi
     __syncthreads();
     if (k0 + TT < klim) {
       tk.load(kb_, a.k_ts, k0 + TT, a.Tk);
       tv.load(vb_, a.v_ts, k0 + TT, a.Tk);
+      kpn = (pad && k0 + TT + lane < a.Tk) ? kpb[k0 + TT + lane] : 0;
     }
     // 32 keys per online-softmax update: two independent S^T sub-tiles (four MFMA chains), one
     // max / sum reduction and one rescale of O per pair
@@ -238,7 +241,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int kl = (sp + h) * 16 + lg * 4 + r;
-            const bool vis = (k0 + kl < kmax) && !(qp && Kp[kl]);
+            const bool vis = (k0 + kl < kmax) && !((qmask >> kl) & 1ull);
             sv[4 * h + r] = vis ? s4[h][r] : -INFINITY;
             mx = fmaxf(mx, sv[4 * h + r]);
           }
@@ -289,15 +292,18 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   }
 }
 
+// Backward.  The padding flags of a 64-row tile are one wave-uniform 64-bit mask (a ballot over
+// the lanes' prefetched flag bytes), the visibility test is a select (no divergent branches around
+// exp), and the log-sum-exp / delta rows of the dK/dV pass are float4 LDS reads.
+//
 // dQ for 64 queries of one (b, head): recompute P^T, dP^T = V dO^T, dS^T, dQ^T += K^T dS^T.
 // Also forms delta = rowsum(dO * O) for these rows (the dK/dV kernel reads it from a.dlt).
 template <int D>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
   using C = AttnCfg<D>;
+  constexpr int ST = 1;  // 16-row sub-tiles per step (2 measured no faster)
   __shared__ __attribute__((aligned(16))) float Ks[TT * C::SA];
   __shared__ __attribute__((aligned(16))) float Vs[TT * C::SA];
-  __shared__ unsigned char Kp[TT];
-  // grid (heads, B, query blocks), the last (most keys under the causal mask) dispatched first
   const int h = blockIdx.x, b = blockIdx.y;
   const int q0 = (gridDim.z - 1 - blockIdx.z) * 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -308,8 +314,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
   const bool pad = a.qpad && a.kpad;
   const bool qp = pad && qv && a.qpad[(long)b * a.Tq + qi];
   const int kmax = key_bound(a, qi);
-  const int wmin = key_bound(a, q0 + wave * 16);
-  const int wlim = key_bound(a, q0 + wave * 16 + 15);  // sub-tiles from here on: dS = 0 for the wave
+  const int wlim = key_bound(a, q0 + wave * 16 + 15);
   float qreg[C::KS], dreg[C::KS];
   float dsum = 0.0f;
 #pragma unroll
@@ -332,50 +337,70 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
   const int klim = key_bound(a, q0 + 63);
   const float* kb_ = a.k + (long)b * a.k_bs + hoff;
   const float* vb_ = a.v + (long)b * a.v_bs + hoff;
+  const unsigned char* kpb = pad ? a.kpad + (long)b * a.Tk : nullptr;
   TileRegs<D> tk, tv;
   tk.load(kb_, a.k_ts, 0, a.Tk);
   tv.load(vb_, a.v_ts, 0, a.Tk);
+  unsigned char kpn = (pad && lane < a.Tk) ? kpb[lane] : 0;  // padding flag of key k0 + lane
   for (int k0 = 0; k0 < klim; k0 += TT) {
     __syncthreads();
     tk.template store<C::SA>(Ks);
     tv.template store<C::SA>(Vs);
-    if (pad && threadIdx.x < TT) Kp[threadIdx.x] = (k0 + threadIdx.x < a.Tk) ? a.kpad[(long)b * a.Tk + k0 + threadIdx.x] : 0;
+    const unsigned long long kbits = __ballot(kpn != 0);
+    const unsigned long long qmask = qp ? kbits : 0ull;  // keys of this tile padding hides from query qi
     __syncthreads();
     if (k0 + TT < klim) {
       tk.load(kb_, a.k_ts, k0 + TT, a.Tk);
       tv.load(vb_, a.v_ts, k0 + TT, a.Tk);
+      kpn = (pad && k0 + TT + lane < a.Tk) ? kpb[k0 + TT + lane] : 0;
     }
 #pragma unroll
-    for (int sub = 0; sub < TT / 16; ++sub) {
+    for (int sub = 0; sub < TT / 16; sub += ST) {
       const int kb = k0 + sub * 16;
       if (kb >= wlim) break;
-      f32x4 s4 = f32x4{0.f, 0.f, 0.f, 0.f};
-      f32x4 dp4 = f32x4{0.f, 0.f, 0.f, 0.f};
+      const bool two = ST == 2 && kb + 16 < wlim;
+      f32x4 s4[ST], dp4[ST];
+#pragma unroll
+      for (int u = 0; u < ST; ++u) {
+        s4[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dp4[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
       {
-        float kk[C::KS], vv[C::KS];
-        row_operands<D, C::SA>(Ks, sub * 16 + lq, lg, kk);
-        row_operands<D, C::SA>(Vs, sub * 16 + lq, lg, vv);
+        float kk[ST][C::KS], vv[ST][C::KS];
 #pragma unroll
-        for (int s = 0; s < C::KS; ++s) {
-          s4 = __builtin_amdgcn_mfma_f32_16x16x4f32(kk[s], qreg[s], s4, 0, 0, 0);
-          dp4 = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[s], dreg[s], dp4, 0, 0, 0);
+        for (int u = 0; u < ST; ++u) {
+          row_operands<D, C::SA>(Ks, (sub + u) * 16 + lq, lg, kk[u]);
+          row_operands<D, C::SA>(Vs, (sub + u) * 16 + lq, lg, vv[u]);
         }
+#pragma unroll
+        for (int s = 0; s < C::KS; ++s)
+#pragma unroll
+          for (int u = 0; u < ST; ++u) {
+            s4[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(kk[u][s], qreg[s], s4[u], 0, 0, 0);
+            dp4[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[u][s], dreg[s], dp4[u], 0, 0, 0);
+          }
       }
-      const bool full = !pad && kb + 16 <= wmin;
-      float ds[4];
+      float ds[ST][4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int kl = sub * 16 + lg * 4 + r;
-        const bool vis = qv && (full || ((k0 + kl < kmax) && !(qp && Kp[kl])));
-        const float p = vis ? __expf(s4[r] - lse) : 0.0f;
-        ds[r] = p * (dp4[r] - dl);
-      }
+      for (int u = 0; u < ST; ++u)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        float kk[C::DT];
-        col_operands<D, C::SA>(Ks, sub * 16 + 4 * lg + s, lq, kk);
+        for (int r = 0; r < 4; ++r) {
+          const int kl = (sub + u) * 16 + lg * 4 + r;
+          const bool vis = qv && (k0 + kl < kmax) && !((qmask >> kl) & 1ull);
+          const float e = __expf(s4[u][r] - lse);
+          ds[u][r] = (vis ? e : 0.0f) * (dp4[u][r] - dl);
+        }
 #pragma unroll
-        for (int dt = 0; dt < C::DT; ++dt) dq[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(kk[dt], ds[s], dq[dt], 0, 0, 0);
+      for (int u = 0; u < ST; ++u) {
+        if (u == 1 && !two) break;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          float kk[C::DT];
+          col_operands<D, C::SA>(Ks, (sub + u) * 16 + 4 * lg + s, lq, kk);
+#pragma unroll
+          for (int dt = 0; dt < C::DT; ++dt)
+            dq[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(kk[dt], ds[u][s], dq[dt], 0, 0, 0);
+        }
       }
     }
   }
@@ -396,11 +421,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
 template <int D>
 __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
   using C = AttnCfg<D>;
+  constexpr int ST = 1;
   __shared__ __attribute__((aligned(16))) float Qs[TT * C::SA];
   __shared__ __attribute__((aligned(16))) float Ds[TT * C::SA];
-  __shared__ float Ls[TT], Dl[TT];
-  __shared__ unsigned char Qp[TT];
-  // grid (heads, B, key blocks), the first (seen by the most queries) dispatched first
+  __shared__ __attribute__((aligned(16))) float Ls[TT];
+  __shared__ __attribute__((aligned(16))) float Dl[TT];
   const int h = blockIdx.x, b = blockIdx.y;
   const int kb0 = blockIdx.z * 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -410,9 +435,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
   const bool kv = kj < a.Tk;
   const bool pad = a.qpad && a.kpad;
   const bool kp = pad && kv && a.kpad[(long)b * a.Tk + kj];
-  const int qmin = query_start(a, kj);                       // first query seeing this lane's key
-  const int wmax = query_start(a, min(kb0 + wave * 16 + 15, a.Tk - 1));  // largest in the wave
-  const int wq0 = query_start(a, min(kb0 + wave * 16, a.Tk - 1));        // smallest in the wave
+  const int qmin = query_start(a, kj);
+  const int wq0 = query_start(a, min(kb0 + wave * 16, a.Tk - 1));
   float kreg[C::KS], vreg[C::KS];
 #pragma unroll
   for (int s = 0; s < C::KS; ++s) {
@@ -428,10 +452,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
   const int qs = (query_start(a, kb0) / 16) * 16;
   const float* qb_ = a.q + (long)b * a.q_bs + hoff;
   const float* db_ = a.dout + (long)b * a.do_bs + hoff;
+  const unsigned char* qpb = pad ? a.qpad + (long)b * a.Tq : nullptr;
   TileRegs<D> tq, td;
+  unsigned char qpn = 0;  // padding flag of query qt0 + lane
   if (qs < a.Tq) {
     tq.load(qb_, a.q_ts, qs, a.Tq);
     td.load(db_, a.do_ts, qs, a.Tq);
+    qpn = (pad && qs + lane < a.Tq) ? qpb[qs + lane] : 0;
   }
   for (int qt0 = qs; qt0 < a.Tq; qt0 += TT) {
     __syncthreads();
@@ -442,50 +469,71 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
       const long ri = ((long)b * a.Hh + h) * a.Tq + qq;
       Ls[threadIdx.x] = qq < a.Tq ? a.lse[ri] : 0.0f;
       Dl[threadIdx.x] = qq < a.Tq ? a.dlt[ri] : 0.0f;
-      if (pad) Qp[threadIdx.x] = qq < a.Tq ? a.qpad[(long)b * a.Tq + qq] : 0;
     }
+    const unsigned long long qbits = __ballot(qpn != 0);
+    const unsigned long long kmask = kp ? qbits : 0ull;  // queries of this tile padding hides from key kj
     __syncthreads();
     if (qt0 + TT < a.Tq) {
       tq.load(qb_, a.q_ts, qt0 + TT, a.Tq);
       td.load(db_, a.do_ts, qt0 + TT, a.Tq);
+      qpn = (pad && qt0 + TT + lane < a.Tq) ? qpb[qt0 + TT + lane] : 0;
     }
 #pragma unroll
-    for (int sub = 0; sub < TT / 16; ++sub) {
+    for (int sub = 0; sub < TT / 16; sub += ST) {
       const int qb = qt0 + sub * 16;
       if (qb >= a.Tq) break;
-      if (qb + 16 <= wq0) continue;  // no query of this sub-tile sees a key of this wave (P = dS = 0)
-      f32x4 s4 = f32x4{0.f, 0.f, 0.f, 0.f};
-      f32x4 dp4 = f32x4{0.f, 0.f, 0.f, 0.f};
-      {
-        float qq[C::KS], dd[C::KS];
-        row_operands<D, C::SA>(Qs, sub * 16 + lk, lg, qq);
-        row_operands<D, C::SA>(Ds, sub * 16 + lk, lg, dd);
+      if (qb + 16 * ST <= wq0) continue;  // no query of these sub-tiles sees a key of this wave
+      const bool two = ST == 2 && qb + 16 < a.Tq;
+      f32x4 s4[ST], dp4[ST];
 #pragma unroll
-        for (int s = 0; s < C::KS; ++s) {
-          s4 = __builtin_amdgcn_mfma_f32_16x16x4f32(qq[s], kreg[s], s4, 0, 0, 0);
-          dp4 = __builtin_amdgcn_mfma_f32_16x16x4f32(dd[s], vreg[s], dp4, 0, 0, 0);
+      for (int u = 0; u < ST; ++u) {
+        s4[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dp4[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      {
+        float qq[ST][C::KS], dd[ST][C::KS];
+#pragma unroll
+        for (int u = 0; u < ST; ++u) {
+          row_operands<D, C::SA>(Qs, (sub + u) * 16 + lk, lg, qq[u]);
+          row_operands<D, C::SA>(Ds, (sub + u) * 16 + lk, lg, dd[u]);
+        }
+#pragma unroll
+        for (int s = 0; s < C::KS; ++s)
+#pragma unroll
+          for (int u = 0; u < ST; ++u) {
+            s4[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(qq[u][s], kreg[s], s4[u], 0, 0, 0);
+            dp4[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(dd[u][s], vreg[s], dp4[u], 0, 0, 0);
+          }
+      }
+      float p[ST][4], ds[ST][4];
+#pragma unroll
+      for (int u = 0; u < ST; ++u) {
+        const int qr = (sub + u) * 16 + lg * 4;  // query row of accumulator register 0
+        const float4 L4 = *reinterpret_cast<const float4*>(Ls + qr);
+        const float4 D4 = *reinterpret_cast<const float4*>(Dl + qr);
+        const float lv[4] = {L4.x, L4.y, L4.z, L4.w}, dv[4] = {D4.x, D4.y, D4.z, D4.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qq = qt0 + qr + r;
+          const bool vis = kv && qq >= qmin && qq < a.Tq && !((kmask >> (qr + r)) & 1ull);
+          const float e = __expf(s4[u][r] * a.scale - lv[r]);
+          p[u][r] = vis ? e : 0.0f;
+          ds[u][r] = p[u][r] * (dp4[u][r] - dv[r]);
         }
       }
-      // every key of the wave is seen by all 16 queries of the sub-tile (all < Tq)
-      const bool full = !pad && qb >= wmax && qb + 16 <= a.Tq;
-      float p[4], ds[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int ql = sub * 16 + lg * 4 + r;  // query row of this accumulator register
-        const int qq = qt0 + ql;
-        const bool vis = kv && (full || (qq >= qmin && qq < a.Tq && !(kp && Qp[ql])));
-        p[r] = vis ? __expf(s4[r] * a.scale - Ls[ql]) : 0.0f;
-        ds[r] = p[r] * (dp4[r] - Dl[ql]);
-      }
+      for (int u = 0; u < ST; ++u) {
+        if (u == 1 && !two) break;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        float dd[C::DT], qq[C::DT];
-        col_operands<D, C::SA>(Ds, sub * 16 + 4 * lg + s, lk, dd);
-        col_operands<D, C::SA>(Qs, sub * 16 + 4 * lg + s, lk, qq);
+        for (int s = 0; s < 4; ++s) {
+          float dd[C::DT], qq[C::DT];
+          col_operands<D, C::SA>(Ds, (sub + u) * 16 + 4 * lg + s, lk, dd);
+          col_operands<D, C::SA>(Qs, (sub + u) * 16 + 4 * lg + s, lk, qq);
 #pragma unroll
-        for (int dt = 0; dt < C::DT; ++dt) {
-          dvT[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(dd[dt], p[s], dvT[dt], 0, 0, 0);
-          dkT[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(qq[dt], ds[s], dkT[dt], 0, 0, 0);
+          for (int dt = 0; dt < C::DT; ++dt) {
+            dvT[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(dd[dt], p[u][s], dvT[dt], 0, 0, 0);
+            dkT[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(qq[dt], ds[u][s], dkT[dt], 0, 0, 0);
+          }
         }
       }
     }

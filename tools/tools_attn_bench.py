@@ -1,0 +1,110 @@
+"""Timing + fp64 check of the attention kernels at the lstmformer step shape
+(B=64, 4 heads, D=64, Tq=Tk=300, block-causal r=1, padded batch as in training).
+
+    python tools/tools_attn_bench.py [repeats]      (on a GPU box; MRG_LIB_PATH picks the library)
+
+Prints, per repeat, the forward and backward µs per call and TFLOP/s (4D / 10D FLOP per visible pair per head, the
+bench's accounting) and the max relative error of dQ/dK/dV against a float64 torch reference on
+the first 4 samples.
+"""
+import ctypes
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # repo root
+from multimodalreactiongeneration_amd import _lib  # noqa: E402
+from multimodalreactiongeneration_amd.functional import visible_pairs  # noqa: E402
+
+B, H, T, D = 64, 4, 300, 64
+E = H * D
+PEAK = 157.3
+
+
+def ptr(t, off=0):
+    return ctypes.c_void_p(t.data_ptr() + 4 * off) if t is not None else None
+
+
+def main():
+    lib = _lib.load()
+    dev = "cuda:0"
+    g = torch.Generator(device="cpu").manual_seed(0)
+    Q = torch.randn(B, T, E, generator=g).to(dev)
+    KV = torch.randn(B, T, 2 * E, generator=g).to(dev)
+    dO = torch.randn(B, T, E, generator=g).to(dev)
+    lens = torch.randint(T // 2, T + 1, (B,), generator=g)
+    lens[0] = T
+    pad = (torch.arange(T)[None, :] >= lens[:, None]).to(torch.uint8).to(dev)
+    O = torch.empty(B, T, E, device=dev)
+    lse = torch.empty(B, H, T, device=dev)
+    dQ = torch.empty(B, T, E, device=dev)
+    dKV = torch.empty(B, T, 2 * E, device=dev)
+    ws = torch.empty(B * H * T, device=dev)
+    scale = D ** -0.5
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def fwd():
+        rc = lib.mrg_attention_fwd(B, H, T, T, D, ptr(Q), T * E, E, ptr(KV), T * 2 * E, 2 * E, ptr(KV, E),
+                                   T * 2 * E, 2 * E, ptr(O), T * E, E, ptr(lse), ptr(pad), ptr(pad), 1,
+                                   ctypes.c_float(scale), stream)
+        assert rc == 0
+
+    def bwd():
+        rc = lib.mrg_attention_bwd(B, H, T, T, D, ptr(Q), T * E, E, ptr(KV), T * 2 * E, 2 * E, ptr(KV, E),
+                                   T * 2 * E, 2 * E, ptr(O), T * E, E, ptr(lse), ptr(pad), ptr(pad), 1,
+                                   ctypes.c_float(scale), ptr(dO), T * E, E, ptr(dQ), T * E, E, ptr(dKV),
+                                   T * 2 * E, 2 * E, ptr(dKV, E), T * 2 * E, 2 * E, ptr(ws), stream)
+        assert rc == 0
+
+    # float64 reference on the first 4 samples (the reference's mask: causal, AND-padding)
+    nb = 4
+    q = Q[:nb].double().view(nb, T, H, D).transpose(1, 2).requires_grad_()
+    k = KV[:nb, :, :E].double().reshape(nb, T, H, D).transpose(1, 2).requires_grad_()
+    v = KV[:nb, :, E:].double().reshape(nb, T, H, D).transpose(1, 2).requires_grad_()
+    causal = torch.arange(T, device=dev)[None, :] > torch.arange(T, device=dev)[:, None]
+    pm = pad[:nb].bool()
+    mask = causal[None] | (pm[:, :, None] & pm[:, None, :])
+    s = (q @ k.transpose(-1, -2)) * scale
+    s = s.masked_fill(mask[:, None], float("-inf"))
+    o = torch.softmax(s, -1) @ v
+    o.backward(dO[:nb].double().view(nb, T, H, D).transpose(1, 2))
+    ref = [q.grad.transpose(1, 2).reshape(nb, T, E), k.grad.transpose(1, 2).reshape(nb, T, E),
+           v.grad.transpose(1, 2).reshape(nb, T, E)]
+    ok_rows = ~torch.isnan(o.detach().transpose(1, 2).reshape(nb, T, E)).any(-1)
+
+    pairs = B * H * visible_pairs(T, T, True)
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+    for var in range(reps):
+        fwd()
+        bwd()
+        torch.cuda.synchronize()
+        got = [dQ[:nb].double(), dKV[:nb, :, :E].double(), dKV[:nb, :, E:].double()]
+        if var == 0:
+            first = (dQ.clone(), dKV.clone())
+        same = torch.equal(first[0], dQ) and torch.equal(first[1], dKV)
+        errs = []
+        for gt, rt in zip(got, ref):
+            m = ok_rows[..., None].expand_as(rt)
+            errs.append(((gt - rt).abs()[m].max() / rt.abs()[m].max()).item())
+        res = {}
+        for name, fn in (("fwd", fwd), ("bwd", bwd)):
+            for _ in range(3):
+                fn()
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            n = 30
+            ev[0].record()
+            for _ in range(n):
+                fn()
+            ev[1].record()
+            torch.cuda.synchronize()
+            res[name] = ev[0].elapsed_time(ev[1]) / n * 1e3
+        tf_f = 4 * D * pairs / res["fwd"] / 1e6
+        tf_b = 10 * D * pairs / res["bwd"] / 1e6
+        print(f"repeat {var}: fwd {res['fwd']:.1f} us ({tf_f:.1f} TF/s, {tf_f / PEAK:.3f})  "
+              f"bwd {res['bwd']:.1f} us ({tf_b:.1f} TF/s, {tf_b / PEAK:.3f})  "
+              f"max rel err dQ {errs[0]:.2e} dK {errs[1]:.2e} dV {errs[2]:.2e}  bitwise={same}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
