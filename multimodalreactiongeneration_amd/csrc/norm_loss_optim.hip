@@ -254,7 +254,7 @@ __global__ __launch_bounds__(1024) void resln_param_reduce_kernel(const float* p
   const int c = blockIdx.x * 64 + lane;
   float s = 0.0f;
   if (c < 2 * E) {
-#pragma unroll 4
+#pragma unroll 16  // 16 loads in flight per wave: the 8-block grid is latency-bound
     for (int i = wave; i < nblk; i += 16) s += part[(long)i * 2 * E + c];
   }
   red[wave][lane] = s;
