@@ -46,6 +46,7 @@ struct AttnArgs {
   int B, Hh, Tq, Tk;
   int causal;
   float scale;
+  int qvec, ovec, dkvvec;  // rows of q / o / dk and dv 16-B aligned: float4 loads and stores
 };
 
 // exclusive upper bound of the keys query i may see (causal rule only; Tk when not causal)
@@ -155,6 +156,46 @@ __device__ __forceinline__ void col_operands(const float* S, int row, int l16, f
   }
 }
 
+// this lane's KS contraction values of one row (row pointer p, 16-B aligned): v[s] = p[dmap(lg, s)]
+// (float4 loads when the map is lane-contiguous), zero when !valid
+template <int D>
+__device__ __forceinline__ void row_values(const float* p, int lg, bool valid, float (&v)[AttnCfg<D>::KS]) {
+  using C = AttnCfg<D>;
+  if constexpr (C::VEC) {
+#pragma unroll
+    for (int i = 0; i < C::KS; i += 4) {
+      const float4 t = valid ? *reinterpret_cast<const float4*>(p + C::KS * lg + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[i] = t.x; v[i + 1] = t.y; v[i + 2] = t.z; v[i + 3] = t.w;
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) v[s] = valid ? p[4 * s + lg] : 0.0f;
+  }
+}
+
+// store this lane's output values of one row: p[dout(lg, dt, r)] = v[dt][r] * mul (float4 per r
+// when the map is lane-contiguous with DT = 4 and vec is set)
+template <int D>
+__device__ __forceinline__ void store_row(float* p, int lg, bool vec, const f32x4 (&v)[AttnCfg<D>::DT], float mul) {
+  using C = AttnCfg<D>;
+  if constexpr (C::VEC && C::DT == 4) {
+    if (vec) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        *reinterpret_cast<float4*>(p + 4 * (4 * lg + r)) =
+            make_float4(v[0][r] * mul, v[1][r] * mul, v[2][r] * mul, v[3][r] * mul);
+      return;
+    }
+  }
+#pragma unroll
+  for (int dt = 0; dt < C::DT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int d = dout<D>(lg, dt, r);
+      if (d < D) p[d] = v[dt][r] * mul;
+    }
+}
+
 // S^T tile (16 keys x 16 queries) = K rows [kr..kr+15] . Q^T, two accumulation chains
 template <int D>
 __device__ __forceinline__ f32x4 qk16(const float* Ks, int rowbase, const float (&qreg)[AttnCfg<D>::KS], int lq,
@@ -190,9 +231,15 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   const int wlim = key_bound(a, q0 + wave * 16 + 15);   // largest: sub-tiles from here on are masked
 
   float qreg[C::KS];
+  if (a.qvec) {
+    row_values<D>(a.q + (long)b * a.q_bs + (long)min(qi, a.Tq - 1) * a.q_ts + hoff, lg, qi < a.Tq, qreg);
 #pragma unroll
-  for (int s = 0; s < C::KS; ++s)
-    qreg[s] = qi < a.Tq ? a.q[(long)b * a.q_bs + (long)qi * a.q_ts + hoff + dmap<D>(lg, s)] * a.scale : 0.0f;
+    for (int s = 0; s < C::KS; ++s) qreg[s] *= a.scale;
+  } else {
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s)
+      qreg[s] = qi < a.Tq ? a.q[(long)b * a.q_bs + (long)qi * a.q_ts + hoff + dmap<D>(lg, s)] * a.scale : 0.0f;
+  }
 
   f32x4 o[C::DT];
 #pragma unroll
@@ -279,15 +326,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
     }
   }
   if (qi < a.Tq) {
-    const float inv = 1.0f / l;  // l == 0 (fully masked row) -> NaN like softmax(-inf row)
-    float* op = a.o + (long)b * a.o_bs + (long)qi * a.o_ts + hoff;
-#pragma unroll
-    for (int dt = 0; dt < C::DT; ++dt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int d = dout<D>(lg, dt, r);
-        if (d < D) op[d] = (l == 0.0f) ? NAN : o[dt][r] * inv;
-      }
+    const float inv = (l == 0.0f) ? NAN : 1.0f / l;  // l == 0 (fully masked row) -> NaN like softmax(-inf row)
+    store_row<D>(a.o + (long)b * a.o_bs + (long)qi * a.o_ts + hoff, lg, a.ovec, o, inv);
     if (lg == 0) a.lse[((long)b * a.Hh + h) * a.Tq + qi] = (l == 0.0f) ? NAN : m + __logf(l);
   }
 }
@@ -317,13 +357,19 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
   const int wlim = key_bound(a, q0 + wave * 16 + 15);
   float qreg[C::KS], dreg[C::KS];
   float dsum = 0.0f;
+  row_values<D>(a.q + (long)b * a.q_bs + (long)min(qi, a.Tq - 1) * a.q_ts + hoff, lg, qv, qreg);
+  row_values<D>(a.dout + (long)b * a.do_bs + (long)min(qi, a.Tq - 1) * a.do_ts + hoff, lg, qv, dreg);
+  float oreg[C::KS];
+  if (a.ovec) {
+    row_values<D>(a.o + (long)b * a.o_bs + (long)min(qi, a.Tq - 1) * a.o_ts + hoff, lg, qv, oreg);
+  } else {
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) oreg[s] = qv ? a.o[(long)b * a.o_bs + (long)qi * a.o_ts + hoff + dmap<D>(lg, s)] : 0.0f;
+  }
 #pragma unroll
   for (int s = 0; s < C::KS; ++s) {
-    const int d = dmap<D>(lg, s);
-    qreg[s] = qv ? a.q[(long)b * a.q_bs + (long)qi * a.q_ts + hoff + d] * a.scale : 0.0f;
-    dreg[s] = qv ? a.dout[(long)b * a.do_bs + (long)qi * a.do_ts + hoff + d] : 0.0f;
-    const float ov = qv ? a.o[(long)b * a.o_bs + (long)qi * a.o_ts + hoff + d] : 0.0f;
-    dsum = fmaf(dreg[s], ov, dsum);
+    qreg[s] *= a.scale;
+    dsum = fmaf(dreg[s], oreg[s], dsum);
   }
   dsum += __shfl_xor(dsum, 16, 64);
   dsum += __shfl_xor(dsum, 32, 64);
@@ -438,11 +484,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
   const int qmin = query_start(a, kj);
   const int wq0 = query_start(a, min(kb0 + wave * 16, a.Tk - 1));
   float kreg[C::KS], vreg[C::KS];
-#pragma unroll
-  for (int s = 0; s < C::KS; ++s) {
-    kreg[s] = kv ? a.k[(long)b * a.k_bs + (long)kj * a.k_ts + hoff + dmap<D>(lg, s)] : 0.0f;
-    vreg[s] = kv ? a.v[(long)b * a.v_bs + (long)kj * a.v_ts + hoff + dmap<D>(lg, s)] : 0.0f;
-  }
+  row_values<D>(a.k + (long)b * a.k_bs + (long)min(kj, a.Tk - 1) * a.k_ts + hoff, lg, kv, kreg);
+  row_values<D>(a.v + (long)b * a.v_bs + (long)min(kj, a.Tk - 1) * a.v_ts + hoff, lg, kv, vreg);
   f32x4 dkT[C::DT], dvT[C::DT];
 #pragma unroll
   for (int dt = 0; dt < C::DT; ++dt) {
@@ -539,18 +582,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
     }
   }
   if (kv) {
-    float* pk = a.dk + (long)b * a.dk_bs + (long)kj * a.dk_ts + hoff;
-    float* pv = a.dv + (long)b * a.dv_bs + (long)kj * a.dv_ts + hoff;
-#pragma unroll
-    for (int dt = 0; dt < C::DT; ++dt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int d = dout<D>(lg, dt, r);
-        if (d < D) {
-          pk[d] = dkT[dt][r] * a.scale;
-          pv[d] = dvT[dt][r];
-        }
-      }
+    store_row<D>(a.dk + (long)b * a.dk_bs + (long)kj * a.dk_ts + hoff, lg, a.dkvvec, dkT, a.scale);
+    store_row<D>(a.dv + (long)b * a.dv_bs + (long)kj * a.dv_ts + hoff, lg, a.dkvvec, dvT, 1.0f);
   }
 }
 
@@ -601,6 +634,8 @@ MRG_API int mrg_attention_fwd(int B, int Hh, int Tq, int Tk, int D,
               "attention fwd: K/V rows must be 16-B aligned (strides multiple of 4 floats)");
   AttnArgs a = attn_base(B, Hh, Tq, Tk, q, q_bs, q_ts, k, k_bs, k_ts, v, v_bs, v_ts, o, o_bs, o_ts, lse,
                          qpad, kpad, causal, scale);
+  a.qvec = rows16(q, q_bs, q_ts) && (D % 4) == 0;
+  a.ovec = rows16(o, o_bs, o_ts) && (D % 4) == 0;
   dim3 grid(Hh, B, (Tq + 63) / 64);
   MRG_ATTN_DISPATCH(attn_fwd_kernel, grid, a);
   return check_launch("attn_fwd_kernel");
@@ -627,6 +662,9 @@ MRG_API int mrg_attention_bwd(int B, int Hh, int Tq, int Tk, int D,
   a.dout = dout; a.do_bs = do_bs; a.do_ts = do_ts; a.dlt = workspace;
   a.dq = dq; a.dq_bs = dq_bs; a.dq_ts = dq_ts; a.dk = dk; a.dk_bs = dk_bs; a.dk_ts = dk_ts;
   a.dv = dv; a.dv_bs = dv_bs; a.dv_ts = dv_ts;
+  a.qvec = 1;  // required above
+  a.ovec = rows16(o, o_bs, o_ts);
+  a.dkvvec = rows16(dk, dk_bs, dk_ts) && rows16(dv, dv_bs, dv_ts);
   dim3 gq(Hh, B, (Tq + 63) / 64);
   MRG_ATTN_DISPATCH(attn_bwd_dq_kernel, gq, a);  // also writes delta = rowsum(dO * O) to the workspace
   if (check_launch("attn_bwd_dq_kernel")) return 1;
