@@ -124,6 +124,7 @@ class GradReducer:
         es = self.flat_grad.element_size()
         spans = sorted(((p.grad.data_ptr() - base) // es, p.numel(), p) for p in params)
         self.buckets, self.bucket_of = [], {}
+        self._named = [(f"param[{i}] {tuple(p.shape)}", p) for i, p in enumerate(params)]
         cur, start, end = [], None, None
         for off, k, p in reversed(spans):          # reverse registration order = backward order
             if cur and (end - off) > cap:
@@ -181,6 +182,12 @@ class GradReducer:
         Fn._flush_touched()
         if self.expected is None:                    # census pass: remember the structure
             self.expected = dict(self.counts)
+            missing = [n for n, p in self._named if id(p) not in self.counts]
+            if missing:
+                # a gradient written outside libmrg (torch's AccumulateGrad) is invisible to the
+                # listener: its bucket could launch before the write lands
+                raise RuntimeError("GradReducer(overlap=True): parameters whose gradients do not come "
+                                   f"from libmrg ops: {missing[:5]}; use overlap=False")
         for b in range(len(self.buckets)):
             if not self.launched[b]:
                 self._launch(b)
@@ -222,8 +229,35 @@ class GradReducer:
             return
         if not self.overlap:
             return self.allreduce()
+        self._agree_error_flag()
         if self.stream is not None:
             torch.cuda.current_stream(self.flat_grad.device).wait_stream(self.stream)
+
+    def _agree_error_flag(self):
+        """Sum the device error flag (a persistent recurrence's hand-off timeout, functional._err_flag)
+        over the ranks on the comm stream, after the gradient buckets: the faulting rank's gradients
+        are already averaged into every rank's buffer, so every rank must skip that AdamW update (the
+        kernel skips on a non-zero flag) and raise, not only the rank that saw the timeout."""
+        from . import functional as Fn
+        dev = self.flat_grad.device
+        err = Fn._err_flag(dev)
+        if not hasattr(self, "_errf"):
+            self._errf = torch.zeros(1, dtype=torch.float32, device=dev)
+        cur = torch.cuda.current_stream(dev) if self.stream is not None else None
+        ctx = torch.cuda.stream(self.stream) if self.stream is not None else None
+        if cur is not None:
+            self.stream.wait_stream(cur)
+            ctx.__enter__()
+        try:
+            self._errf.copy_(err)
+            if self.comm is not None:
+                self.comm.allreduce(self._errf, None, "sum")
+            else:
+                dist.all_reduce(self._errf, op=dist.ReduceOp.SUM)
+            err.copy_(self._errf)
+        finally:
+            if ctx is not None:
+                ctx.__exit__(None, None, None)
 
     def close(self):
         if self.overlap:
@@ -242,6 +276,7 @@ class GradReducer:
             self.stream.wait_stream(cur)
             with torch.cuda.stream(self.stream):
                 self.comm.allreduce(self.flat_grad, self.buckets, "mean")
+            self._agree_error_flag()
             cur.wait_stream(self.stream)
             return
         if self.stream is not None:
@@ -250,9 +285,11 @@ class GradReducer:
             with torch.cuda.stream(self.stream):
                 for s, e in self.buckets:
                     dist.all_reduce(self.flat_grad[s:e], op=op)
+            self._agree_error_flag()
             cur.wait_stream(self.stream)
         else:
             for s, e in self.buckets:
                 dist.all_reduce(self.flat_grad[s:e], op=op)
+            self._agree_error_flag()
         if scale != 1.0:
             self.flat_grad.mul_(scale)

@@ -449,7 +449,9 @@ class LSTMwithSample(LightningSurface):
                 sampling_mask = torch.rand(T) < (self.current_epoch / self.max_epochs)
             else:
                 sampling_mask = (torch.ones if full_generation else torch.zeros)(T, dtype=torch.bool)
-        if self.use_fused_decode and self._fused_params() is not None:
+        # the fused decode computes in fp32 only: under precision='bf16' the per-frame path runs, so
+        # every product of the step follows the selected arithmetic (as _LSTMCellFn's fused step does)
+        if self.use_fused_decode and Fn._ARITH[0] is None and self._fused_params() is not None:
             return self._fused_prediction(batch, sampling_mask), target
         # time-major copies made once: every per-frame slice below is then contiguous, so the
         # ops of the T single-frame forwards run on it in place (no per-frame layout copies)
