@@ -127,7 +127,7 @@ int mrg_colsum_f32(int rows, int N, const float* X, long ld, long ld_hi, int rdi
  * input projection gx = x W_ih^T + b_ih.  Replaces the cuDNN RNN behind
  * LSTMMixer.forward (mixer_block.py:248-252), LSTMModule.forward
  * (lstm_block.py:38-46) and LSTMSampler.forward (lstm_sampler.py:26-34).
- * `nprob` (1..4) independent same-shape recurrences share one launch
+ * `nprob` (1..12) independent same-shape recurrences share one launch
  * (e.g. the audio and partner encoders of block 0).  Arrays are indexed by
  * problem.  xbuf[i] must be zeroed before every call
  * (mrg_lstm_fwd_xbuf_bytes / mrg_lstm_bwd_xbuf_bytes); *err is OR-ed with 1
@@ -142,15 +142,20 @@ int mrg_lstm_fwd(int nprob, int B, int T, int H,
                  const float* const* h0, const float* const* c0,
                  float* const* y, const long* y_bs, const long* y_ts,
                  float* const* gates, float* const* cs, float* const* hT, float* const* cT,
-                 const int* reverse, void* const* xbuf, int* err, int cus, int force_bs,
-                 hipStream_t stream);
-/* Backward: dG[B, T, 4H] = d(pre-activation gates); dh0 / dc0 optional. */
+                 const int* reverse, void* const* xbuf, const long* lay, int* err, int cus,
+                 int force_bs, hipStream_t stream);
+/* Backward: dG[B, T, 4H] = d(pre-activation gates); dh0 / dc0 optional.
+ * lay (nullable = dense [B, T, .] / [B, H]): 8 strides (elements) per problem, so a problem can be
+ * a time chunk of a longer (e.g. time-major) sequence, its state carried through h0/c0 = the
+ * previous chunk's last y / c:  fwd {gates bs, gates ts, cs bs, cs ts, h0 bs, c0 bs, -, -},
+ * bwd {gates bs, gates ts, cs bs, cs ts, c0 bs, dG bs, dG ts, -}.                              */
 int mrg_lstm_bwd(int nprob, int B, int T, int H,
                  const float* const* w_hh, const float* const* gates, const float* const* cs,
                  const float* const* c0, const float* const* dy, const long* dy_bs,
                  const long* dy_ts, const float* const* dhT, const float* const* dcT,
                  float* const* dG, float* const* dh0, float* const* dc0, const int* reverse,
-                 void* const* xbuf, int* err, int cus, int force_bs, hipStream_t stream);
+                 void* const* xbuf, const long* lay, int* err, int cus, int force_bs,
+                 hipStream_t stream);
 
 /* Fault injection (tests only): mode 1 makes the NEXT mrg_lstm_fwd launch drop member 0's first
  * hand-off, so the recurrence times out and reports through *err; 0 disarms.  Process-wide.  */
@@ -296,6 +301,17 @@ int mrg_residual_layernorm_bwd(int rows, int E, const float* dy, const float* a,
  * only the optimizer reads parameter gradients.                                              */
 int mrg_residual_layernorm_param_reduce(int rows, int E, const float* workspace, float* dgamma,
                                         float* dbeta, int accumulate, hipStream_t stream);
+/* Row-mapped forms (E % 4 == 0, 16-byte aligned rows) for the time-major encoder stack
+ * (mixer_block.py:479-507 per layer, run as time chunks): the forward's output rows y and the
+ * backward's incoming gradient rows dy sit at (r / div) * hi + (r % div) * lo (div = 0: r * lo), so
+ * time-major rows [T, B, E] write / read a batch-major [B, T, E] tensor in place.  The backward
+ * leaves dgamma / dbeta partials in workspace (one 32-row block each; a chunk passes its offset). */
+int mrg_residual_layernorm_fwd_map(int rows, int E, const float* a, const float* b, const float* gamma,
+                                   const float* beta, float eps, float* y, long y_lo, long y_hi, int y_div,
+                                   float* mean, float* rstd, hipStream_t stream);
+int mrg_residual_layernorm_bwd_map(int rows, int E, const float* dy, long dy_lo, long dy_hi, int dy_div,
+                                   const float* a, const float* b, const float* gamma, const float* mean,
+                                   const float* rstd, float* dx, float* workspace, hipStream_t stream);
 
 /* ---------------------------------------------------------------- loss
  * Masked regression loss of training_step (lstmformer.py:372-380,

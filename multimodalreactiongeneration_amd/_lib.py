@@ -65,10 +65,10 @@ SIGNATURES = {
     "mrg_lstm_fwd": (c_int, [c_int, c_int, c_int, c_int,
                              PP, PL, PL, PP, PP, PP, PP,
                              PP, PL, PL, PP, PP, PP, PP,
-                             PI, PP, P, c_int, c_int, P]),
+                             PI, PP, PL, P, c_int, c_int, P]),
     "mrg_lstm_bwd": (c_int, [c_int, c_int, c_int, c_int,
                              PP, PP, PP, PP, PP, PL, PL, PP, PP,
-                             PP, PP, PP, PI, PP, P, c_int, c_int, P]),
+                             PP, PP, PP, PI, PP, PL, P, c_int, c_int, P]),
     "mrg_lstm_config": (c_int, [c_int]),
     "mrg_lstm_cell_fwd": (c_int, [c_int, c_int, P, c_long, P, P, P, P, P, c_long, P, P]),
     "mrg_lstm_cell_bwd": (c_int, [c_int, c_int, P, P, P, P, c_long, P, P, P, P, P]),
@@ -92,6 +92,9 @@ SIGNATURES = {
     "mrg_residual_layernorm_bwd_workspace_bytes": (c_size, [c_int, c_int]),
     "mrg_residual_layernorm_bwd": (c_int, [c_int, c_int, P, P, P, P, P, P, P, P, P, c_int, P, P]),
     "mrg_residual_layernorm_param_reduce": (c_int, [c_int, c_int, P, P, P, c_int, P]),
+    "mrg_residual_layernorm_fwd_map": (c_int, [c_int, c_int, P, P, P, P, c_float, P, c_long, c_long, c_int,
+                                               P, P, P]),
+    "mrg_residual_layernorm_bwd_map": (c_int, [c_int, c_int, P, c_long, c_long, c_int, P, P, P, P, P, P, P, P]),
     "mrg_loss_workspace_bytes": (c_size, [c_int, c_int, c_int]),
     "mrg_masked_loss_fwd": (c_int, [c_int, c_int, c_int, P, c_long, P, c_int, c_float, c_float,
                                     c_int, c_int, c_float, P, P, P]),

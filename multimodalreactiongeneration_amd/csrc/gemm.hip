@@ -1074,13 +1074,14 @@ static int gemm_ex(int mode, int M, int N, int K, float alpha,
   // LDS-DMA pipelined x6 kernel: k-contiguous A and B, whole 32-deep k-tiles, unsplit
   // (tile by shape, measured with tools/tools_gemm_bench.py: 128 x 128 for N >= 1024, 64 x 64 for
   // N = K = 256, else 64 x 128; ring depth 2 = two workgroups per CU)
-  if (mode == 1 && g_glds > 0 && !transA && transB && splits == 1 && !asum_out && K > 0 && (K % 32) == 0 && va &&
+  // (mode 2, bf16 operands: the same kernel with one plane and one MFMA per block)
+  if (mx && g_glds > 0 && !transA && transB && splits == 1 && !asum_out && K > 0 && (K % 32) == 0 && va &&
       vb && M >= 2048 && N >= 256) {
     int bm = 64, bn = 128;
     if (N >= 1024) bm = 128;
     else if (N == 256 && K <= 256) bn = 64;
     if (g_glds_bn == 64) bn = 64;
-    launch_x6g(a, g_glds, bm, bn, stream);
+    launch_x6g(a, g_glds, bm, bn, stream, mode == 2 ? 1 : 3);
     return check_launch("gemm_x6g_kernel");
   }
   int tile;  // 0: 128x128, 1: 128x64, 2: 64x64
@@ -1109,11 +1110,11 @@ static int gemm_ex(int mode, int M, int N, int K, float alpha,
     if (tiles <= MRG_GEMM_COUNTERS && (long)splits * 64 * 64 * 4 <= 65536) a.cnt = counters;
   }
   // weight gradients (dY^T X) on the LDS-DMA kernel: k-strided operands, split-K slabs, fused row sums
-  const bool wg = mode == 1 && g_glds_wg && g_tile_override < 0 && transA && !transB && va && vb && K > 0 &&
+  const bool wg = mx && g_glds_wg && g_tile_override < 0 && transA && !transB && va && vb && K > 0 &&
                   (K % 32) == 0 && (M % 4) == 0 && (N % 4) == 0 && M >= 64 && N >= 64 && !a.cnt;
   if (wg) {
     tile = 0;
-    launch_x6g_wgrad(a, splits, 128, 128, stream);
+    launch_x6g_wgrad(a, splits, 128, 128, stream, mode == 2 ? 1 : 3);
   } else if (launch_gemm(mode, a, tile, bk, transA, transB, va, vb, splits, stream)) {
     return 2;
   }

@@ -56,6 +56,31 @@ __device__ __forceinline__ void split8(f32x4v_ v0, f32x4v_ v1, bf16x8 (&f)[3]) {
   f[2] = __builtin_bit_cast(bf16x8, p2);
 }
 
+// one plane: 8 consecutive-k fp32 -> bf16x8 (RNE), the bf16-operand arithmetic (precision "bf16")
+__device__ __forceinline__ bf16x8 cvt8(f32x4v_ v0, f32x4v_ v1) {
+  const u32x4 p = {pk_bf16(v0.x, v0.y), pk_bf16(v0.z, v0.w), pk_bf16(v1.x, v1.y), pk_bf16(v1.z, v1.w)};
+  return __builtin_bit_cast(bf16x8, p);
+}
+
+// NP = 3: the x6 split (fp32-class, six MFMAs per block); NP = 1: bf16 operands, one MFMA per block
+template <int NP>
+__device__ __forceinline__ void planes8(f32x4v_ v0, f32x4v_ v1, bf16x8 (&f)[NP]) {
+  if constexpr (NP == 3) split8(v0, v1, f);
+  else f[0] = cvt8(v0, v1);
+}
+
+template <int NP>
+__device__ __forceinline__ f32x16 mfma_planes(const bf16x8 (&b)[NP], const bf16x8 (&a)[NP], f32x16 acc) {
+  if constexpr (NP == 3) {  // small terms first; (B, A) operand order -> C^T per lane
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[2], a[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[1], a[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[0], a[2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[1], a[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[0], a[1], acc, 0, 0, 0);
+  }
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[0], a[0], acc, 0, 0, 0);
+}
+
 template <int N>
 __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -66,8 +91,9 @@ __device__ __forceinline__ void vm_wait() {
 // A is split in the loop (half the VALU of the split; the B fragments are three ds_read_b128).
 // B plane rows are 64 B per k-tile: one DMA wave-instruction fills 16 rows (lane L -> row 16g + L/4,
 // 16-B slot L%4 holding 8-k chunk (L%4) ^ ((row >> 2) & 3)).
-template <int BM, int BN, int NS, int PB>
+template <int BM, int BN, int NS, int PB, int NP = 3>
 __global__ __launch_bounds__(NT, 1) void gemm_x6g_kernel(GemmArgs a, long bplane) {
+  static_assert(NP == 3 || (NP == 1 && PB == 0), "gemm_x6g: one-plane form has no pre-split B");
   constexpr int TM = BM / 64, TN = BN / 64;
   constexpr int SA = BM * 128;                                   // A: [BM][32] fp32
   constexpr int SBP = BN * 64;                                   // one B plane: [BN][32] bf16
@@ -172,29 +198,22 @@ __global__ __launch_bounds__(NT, 1) void gemm_x6g_kernel(GemmArgs a, long bplane
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-      bf16x8 fa[TM][3], fb[TN][3];
+      bf16x8 fa[TM][NP], fb[TN][NP];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) split8(ra[i][0], ra[i][1], fa[i]);
+      for (int i = 0; i < TM; ++i) planes8<NP>(ra[i][0], ra[i][1], fa[i]);
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        if (PB) {
+        if constexpr (PB) {
 #pragma unroll
           for (int p = 0; p < 3; ++p) fb[j][p] = __builtin_bit_cast(bf16x8, rp[j][p]);
         } else {
-          split8(rb[j][0], rb[j][1], fb[j]);
+          planes8<NP>(rb[j][0], rb[j][1], fb[j]);
         }
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {  // small terms first; (B, A) operand order -> C^T per lane
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][2], fa[i][0], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][1], fa[i][1], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][0], fa[i][2], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][1], fa[i][0], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][0], fa[i][1], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][0], fa[i][0], acc[i][j], 0, 0, 0);
-        }
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma_planes<NP>(fb[j], fa[i], acc[i][j]);
     }
   }
   __syncthreads();  // every wave's last fragment reads are done: the ring becomes the epilogue stage
@@ -238,7 +257,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_x6g_kernel(GemmArgs a, long bplane
   }
 }
 
-template <int BM, int BN, int PB>
+template <int BM, int BN, int PB, int NP>
 static void launch_tiles(GemmArgs a, int ns, long bplane, hipStream_t s) {
   a.tiles_n = (a.N + BN - 1) / BN;
   a.tiles_mn = a.tiles_n * ((a.M + BM - 1) / BM);
@@ -246,6 +265,10 @@ static void launch_tiles(GemmArgs a, int ns, long bplane, hipStream_t s) {
   a.nsplit = 1;
   a.ws = nullptr;
   const unsigned grid = (unsigned)a.tiles_mn;
+  if constexpr (NP == 1) {  // one-plane form: ring depth 2 only
+    gemm_x6g_kernel<BM, BN, 2, 0, 1><<<grid, NT, 0, s>>>(a, bplane);
+    return;
+  }
   switch (ns) {
     case 2: gemm_x6g_kernel<BM, BN, 2, PB><<<grid, NT, 0, s>>>(a, bplane); break;
     case 4: gemm_x6g_kernel<BM, BN, 4, PB><<<grid, NT, 0, s>>>(a, bplane); break;
@@ -253,19 +276,22 @@ static void launch_tiles(GemmArgs a, int ns, long bplane, hipStream_t s) {
   }
 }
 
-template <int PB>
+template <int PB, int NP = 3>
 static void launch_shape(GemmArgs a, int ns, int bm, int bn, long bplane, hipStream_t s) {
   if (bm == 64) {
-    if (bn == 64) launch_tiles<64, 64, PB>(a, ns, bplane, s);
-    else launch_tiles<64, 128, PB>(a, ns, bplane, s);
+    if (bn == 64) launch_tiles<64, 64, PB, NP>(a, ns, bplane, s);
+    else launch_tiles<64, 128, PB, NP>(a, ns, bplane, s);
   } else if (bn == 64) {
-    launch_tiles<128, 64, PB>(a, ns, bplane, s);
+    launch_tiles<128, 64, PB, NP>(a, ns, bplane, s);
   } else {
-    launch_tiles<128, 128, PB>(a, ns, bplane, s);
+    launch_tiles<128, 128, PB, NP>(a, ns, bplane, s);
   }
 }
 
-void launch_x6g(GemmArgs a, int ns, int bm, int bn, hipStream_t s) { launch_shape<0>(a, ns, bm, bn, 0, s); }
+void launch_x6g(GemmArgs a, int ns, int bm, int bn, hipStream_t s, int planes) {
+  if (planes == 1) launch_shape<0, 1>(a, 2, bm, bn, 0, s);
+  else launch_shape<0>(a, ns, bm, bn, 0, s);
+}
 
 
 // ----------------------------------------------------------------------------------------------
@@ -281,7 +307,7 @@ __device__ __forceinline__ int wg_off(int k, int c) {  // byte offset of chunk c
   return k * X * 4 + ((c ^ (((k >> 3) & 1) << 3)) << 4);
 }
 
-template <int BM, int BN, int NS>
+template <int BM, int BN, int NS, int NP = 3>
 __global__ __launch_bounds__(NT, 1) void gemm_x6g_wgrad_kernel(GemmArgs a) {
   constexpr int TM = BM / 64, TN = BN / 64;
   constexpr int SA = 32 * BM * 4, SS = SA + 32 * BN * 4;
@@ -371,28 +397,22 @@ __global__ __launch_bounds__(NT, 1) void gemm_x6g_wgrad_kernel(GemmArgs a) {
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-      bf16x8 fa[TM][3], fb[TN][3];
+      bf16x8 fa[TM][NP], fb[TN][NP];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         if (do_asum)
           cs[i] += ((va[i][0] + va[i][1]) + (va[i][2] + va[i][3])) + ((va[i][4] + va[i][5]) + (va[i][6] + va[i][7]));
-        split8(f32x4v_{va[i][0], va[i][1], va[i][2], va[i][3]}, f32x4v_{va[i][4], va[i][5], va[i][6], va[i][7]}, fa[i]);
+        planes8<NP>(f32x4v_{va[i][0], va[i][1], va[i][2], va[i][3]}, f32x4v_{va[i][4], va[i][5], va[i][6], va[i][7]},
+                    fa[i]);
       }
 #pragma unroll
       for (int jj = 0; jj < TN; ++jj)
-        split8(f32x4v_{vb[jj][0], vb[jj][1], vb[jj][2], vb[jj][3]}, f32x4v_{vb[jj][4], vb[jj][5], vb[jj][6], vb[jj][7]},
-               fb[jj]);
+        planes8<NP>(f32x4v_{vb[jj][0], vb[jj][1], vb[jj][2], vb[jj][3]},
+                    f32x4v_{vb[jj][4], vb[jj][5], vb[jj][6], vb[jj][7]}, fb[jj]);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][2], fa[i][0], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][1], fa[i][1], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][0], fa[i][2], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][1], fa[i][0], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][0], fa[i][1], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j][0], fa[i][0], acc[i][j], 0, 0, 0);
-        }
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma_planes<NP>(fb[j], fa[i], acc[i][j]);
     }
   }
   if (do_asum) {  // lanes l and l + 32 hold the two k halves of row m = wm + 32 i + (l & 31)
@@ -444,7 +464,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_x6g_wgrad_kernel(GemmArgs a) {
   }
 }
 
-void launch_x6g_wgrad(GemmArgs a, int splits, int bm, int bn, hipStream_t s) {
+void launch_x6g_wgrad(GemmArgs a, int splits, int bm, int bn, hipStream_t s, int planes) {
   auto go = [&](auto kern, int BM_, int BN_) {
     a.tiles_n = (a.N + BN_ - 1) / BN_;
     a.tiles_mn = a.tiles_n * ((a.M + BM_ - 1) / BM_);
@@ -452,7 +472,8 @@ void launch_x6g_wgrad(GemmArgs a, int splits, int bm, int bn, hipStream_t s) {
     a.nsplit = splits;
     kern<<<(unsigned)a.ntiles, NT, 0, s>>>(a);
   };
-  if (bm == 64 && bn == 64) go(gemm_x6g_wgrad_kernel<64, 64, 2>, 64, 64);
+  if (planes == 1) go(gemm_x6g_wgrad_kernel<128, 128, 2, 1>, 128, 128);
+  else if (bm == 64 && bn == 64) go(gemm_x6g_wgrad_kernel<64, 64, 2>, 64, 64);
   else if (bm == 64) go(gemm_x6g_wgrad_kernel<64, 128, 2>, 64, 128);
   else if (bn == 64) go(gemm_x6g_wgrad_kernel<128, 64, 2>, 128, 64);
   else go(gemm_x6g_wgrad_kernel<128, 128, 2>, 128, 128);

@@ -38,7 +38,7 @@
 
 namespace mrg {
 
-static constexpr int MAXP = 4;
+static constexpr int MAXP = 12;  // problems per launch (kernarg: 12 x 176 B)
 
 struct LstmFwdProblem {
   const float* gx;  // pre-activations from the input GEMM (+ b_ih)
@@ -54,6 +54,8 @@ struct LstmFwdProblem {
   float* hT;     // [B, H] or null
   float* cT;     // [B, H] or null
   unsigned long long* xbuf;  // [2][B][H] granules
+  long g_bs, g_ts, cs_bs, cs_ts, h0_bs, c0_bs;  // strides (elements) of gates / cs / h0 / c0: time chunks of a
+                                                // longer sequence, time-major layouts
   int reverse;
 };
 
@@ -70,6 +72,7 @@ struct LstmBwdProblem {
   float* dh0;        // nullable
   float* dc0;        // nullable
   unsigned long long* xbuf;  // [2][B][G][H] granules
+  long g_bs, g_ts, cs_bs, cs_ts, c0_bs, dG_bs, dG_ts;  // strides (elements) of gates / cs / c0 / dG
   int reverse;
 };
 
@@ -252,8 +255,10 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
   // register blocking of the recurrent GEMV: a thread owns RT gate rows x KL hidden inputs, the
   // KC lanes of a row group split the hidden dimension (DPP-reduced), so every h value read from
   // LDS feeds RT FMAs (the GEMV is LDS-issue bound otherwise)
-  // (KC = 8 lanes x 2 rows measured fastest at H = 256: 3 DPP levels, 128-B LDS reads per lane)
-  constexpr int KC = (H >= 128) ? (2 * NT / R) : ((H / 4 < 16) ? H / 4 : 16);
+  // (KC = 8 lanes x 2 rows measured fastest at H = 256 and batch tiles 1-2: 3 DPP levels, 128-B LDS
+  // reads per lane; from batch tile 4 the step is bound by those LDS reads of h (each h value feeds
+  // RT FMAs), so there KC = 16 lanes x 4 rows halves them for one more DPP level)
+  constexpr int KC = (H >= 128) ? ((BS >= 4 ? 4 : 2) * NT / R) : ((H / 4 < 16) ? H / 4 : 16);
   constexpr int RT = R * KC / NT;
   constexpr int KL = H / KC;
   constexpr int KLP = ((KL / 4) % 2 == 0) ? KL + 4 : KL;  // odd 16-B chunk pitch: conflict-free b128
@@ -300,14 +305,14 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
   if (cvalid) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) bh[q] = P.b_hh[q * H + hcol];
-    if (P.c0) c = P.c0[(long)bg * H + hcol];
+    if (P.c0) c = P.c0[(long)bg * P.c0_bs + hcol];
   }
 
   // initial h_{-1}
   for (int e = tid; e < BS * H; e += NT) {
     int b = e / H, k = e % H;
     float v = 0.0f;
-    if (P.h0 && b0 + b < B) v = P.h0[(long)(b0 + b) * H + k];
+    if (P.h0 && b0 + b < B) v = P.h0[(long)(b0 + b) * P.h0_bs + k];
     hs[b][k / KL][k % KL] = v;
   }
   float gxv[4] = {0.f, 0.f, 0.f, 0.f};
@@ -369,9 +374,9 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
       h = og * tanhf_(c);
       if (!(args.inject == 1 && j == 0 && tt == 0)) put_granule(xb + ((long)par * B + bg) * H + hcol, (unsigned)(tt + 1), h, local);
       P.y[(long)bg * P.y_bs + (long)t * P.y_ts + hcol] = h;
-      float* gs = P.gates + ((long)bg * T + t) * 4 * H + hcol;
+      float* gs = P.gates + (long)bg * P.g_bs + (long)t * P.g_ts + hcol;
       gs[0] = ig; gs[H] = fg; gs[2 * H] = gg; gs[3 * H] = og;
-      P.cs[((long)bg * T + t) * H + hcol] = c;
+      P.cs[(long)bg * P.cs_bs + (long)t * P.cs_ts + hcol] = c;
       if (tt + 1 < T) load_gx(P.reverse ? t - 1 : t + 1);
     }
     MRG_STAMP(4);
@@ -422,8 +427,10 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
   __shared__ __attribute__((aligned(16))) float dgl[BS][RC][RLP];
   __shared__ float sv[2][7][BS * U];  // saved i, f, g, o, c_t, c_{t-1}, dy of the cells, by step parity
   constexpr int CW = (BS * U + 63) / 64;
-  constexpr int IOFF = CW * 64;  // first io thread
-  static_assert(IOFF + BS * U <= NT, "LSTM bwd: no room for the io waves");
+  // no spare waves for the io role at the largest batch tiles: the cell threads then move their own
+  // saved activations (same schedule: stage step tt+1, prefetch tt+2, after the step's GEMV)
+  constexpr bool SELF_IO = CW * 64 + BS * U > NT;
+  constexpr int IOFF = SELF_IO ? 0 : CW * 64;  // first io thread
 
   int prob, grp, j;
   const int ngroups = (args.B + BS - 1) / BS;
@@ -471,10 +478,11 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
     if (!iovalid || tt2 >= T) return;
     const int t = P.reverse ? tt2 : T - 1 - tt2;
     const int tp = P.reverse ? t + 1 : t - 1;
-    const float* gs = P.gates + ((long)ibg * T + t) * 4 * H + iocol;
+    const float* gs = P.gates + (long)ibg * P.g_bs + (long)t * P.g_ts + iocol;
     pf[0] = gs[0]; pf[1] = gs[H]; pf[2] = gs[2 * H]; pf[3] = gs[3 * H];
-    pf[4] = P.cs[((long)ibg * T + t) * H + iocol];
-    pf[5] = (tp >= 0 && tp < T) ? P.cs[((long)ibg * T + tp) * H + iocol] : (P.c0 ? P.c0[(long)ibg * H + iocol] : 0.0f);
+    pf[4] = P.cs[(long)ibg * P.cs_bs + (long)t * P.cs_ts + iocol];
+    pf[5] = (tp >= 0 && tp < T) ? P.cs[(long)ibg * P.cs_bs + (long)tp * P.cs_ts + iocol]
+                                : (P.c0 ? P.c0[(long)ibg * P.c0_bs + iocol] : 0.0f);
     pf[6] = P.dy ? P.dy[(long)ibg * P.dy_bs + (long)t * P.dy_ts + iocol] : 0.0f;
   };
   auto io_stage = [&](int tt2) {  // pf -> sv slot of step tt2
@@ -574,7 +582,7 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
     }
     if (iovalid) {
       // dG of this step (still in dgl until the barrier), then stage step tt+1, prefetch tt+2
-      float* dgp = P.dG + ((long)ibg * T + t) * 4 * H + iocol;
+      float* dgp = P.dG + (long)ibg * P.dG_bs + (long)t * P.dG_ts + iocol;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int rr = q * U + iu;
@@ -617,7 +625,7 @@ template <int H, int G>
 static int launch_fwd(const LstmFwdArgs& a, int force_bs, int cus, hipStream_t s) {
   constexpr int NT = LstmNT<H, G>::value;
   const long groups1 = a.B;
-  for (int bs = 1; bs <= 8; bs *= 2) {
+  for (int bs = 1; bs <= 16; bs *= 2) {
     if (force_bs > 0 && bs != force_bs) continue;
     long nblk = (long)a.nprob * ((groups1 + bs - 1) / bs) * G;
     bool ok;
@@ -625,7 +633,8 @@ static int launch_fwd(const LstmFwdArgs& a, int force_bs, int cus, hipStream_t s
       case 1: ok = fits(lstm_fwd_kernel<H, G, 1>, NT, nblk, cus); if (ok) lstm_fwd_kernel<H, G, 1><<<nblk, NT, 0, s>>>(a); break;
       case 2: ok = fits(lstm_fwd_kernel<H, G, 2>, NT, nblk, cus); if (ok) lstm_fwd_kernel<H, G, 2><<<nblk, NT, 0, s>>>(a); break;
       case 4: ok = fits(lstm_fwd_kernel<H, G, 4>, NT, nblk, cus); if (ok) lstm_fwd_kernel<H, G, 4><<<nblk, NT, 0, s>>>(a); break;
-      default: ok = fits(lstm_fwd_kernel<H, G, 8>, NT, nblk, cus); if (ok) lstm_fwd_kernel<H, G, 8><<<nblk, NT, 0, s>>>(a); break;
+      case 8: ok = fits(lstm_fwd_kernel<H, G, 8>, NT, nblk, cus); if (ok) lstm_fwd_kernel<H, G, 8><<<nblk, NT, 0, s>>>(a); break;
+      default: ok = fits(lstm_fwd_kernel<H, G, 16>, NT, nblk, cus); if (ok) lstm_fwd_kernel<H, G, 16><<<nblk, NT, 0, s>>>(a); break;
     }
     if (ok) return check_launch("lstm_fwd_kernel");
   }
@@ -639,16 +648,17 @@ static int g_bwd_blocks_per_cu = 0;  // cap on resident workgroups per CU (mrg_l
 template <int H, int G>
 static int launch_bwd(const LstmBwdArgs& a, int force_bs, int cus, hipStream_t s) {
   constexpr int NT = LstmNT<H, G>::value;
-  for (int bs = 1; bs <= 8; bs *= 2) {
+  for (int bs = 1; bs <= 16; bs *= 2) {
     if (force_bs > 0 && bs != force_bs) continue;
     long nblk = (long)a.nprob * ((a.B + bs - 1) / bs) * G;
-    if (force_bs <= 0 && g_bwd_blocks_per_cu > 0 && bs < 8 && nblk > (long)g_bwd_blocks_per_cu * cus) continue;
+    if (force_bs <= 0 && g_bwd_blocks_per_cu > 0 && bs < 16 && nblk > (long)g_bwd_blocks_per_cu * cus) continue;
     bool ok;
     switch (bs) {
       case 1: ok = fits(lstm_bwd_kernel<H, G, 1>, NT, nblk, cus); if (ok) lstm_bwd_kernel<H, G, 1><<<nblk, NT, 0, s>>>(a); break;
       case 2: ok = fits(lstm_bwd_kernel<H, G, 2>, NT, nblk, cus); if (ok) lstm_bwd_kernel<H, G, 2><<<nblk, NT, 0, s>>>(a); break;
       case 4: ok = fits(lstm_bwd_kernel<H, G, 4>, NT, nblk, cus); if (ok) lstm_bwd_kernel<H, G, 4><<<nblk, NT, 0, s>>>(a); break;
-      default: ok = fits(lstm_bwd_kernel<H, G, 8>, NT, nblk, cus); if (ok) lstm_bwd_kernel<H, G, 8><<<nblk, NT, 0, s>>>(a); break;
+      case 8: ok = fits(lstm_bwd_kernel<H, G, 8>, NT, nblk, cus); if (ok) lstm_bwd_kernel<H, G, 8><<<nblk, NT, 0, s>>>(a); break;
+      default: ok = fits(lstm_bwd_kernel<H, G, 16>, NT, nblk, cus); if (ok) lstm_bwd_kernel<H, G, 16><<<nblk, NT, 0, s>>>(a); break;
     }
     if (ok) return check_launch("lstm_bwd_kernel");
   }
@@ -744,8 +754,8 @@ MRG_API int mrg_lstm_fwd(int nprob, int B, int T, int H,
                          const float* const* h0, const float* const* c0,
                          float* const* y, const long* y_bs, const long* y_ts,
                          float* const* gates, float* const* cs, float* const* hT, float* const* cT,
-                         const int* reverse, void* const* xbuf, int* err, int cus, int force_bs,
-                         hipStream_t stream) {
+                         const int* reverse, void* const* xbuf, const long* lay, int* err, int cus,
+                         int force_bs, hipStream_t stream) {
   MRG_REQUIRE(nprob >= 1 && nprob <= MAXP, "mrg_lstm_fwd: nprob %d out of range", nprob);
   int G = group_size(H);
   MRG_REQUIRE(G > 0, "mrg_lstm_fwd: unsupported hidden size %d", H);
@@ -763,6 +773,10 @@ MRG_API int mrg_lstm_fwd(int nprob, int B, int T, int H,
     p.y = y[i]; p.y_bs = y_bs[i]; p.y_ts = y_ts[i]; p.gates = gates[i]; p.cs = cs[i];
     p.hT = hT ? hT[i] : nullptr; p.cT = cT ? cT[i] : nullptr;
     p.xbuf = (unsigned long long*)xbuf[i]; p.reverse = reverse ? reverse[i] : 0;
+    const long* L = lay ? lay + 8 * i : nullptr;  // {gates bs, ts, cs bs, ts, h0 bs, c0 bs}
+    p.g_bs = L ? L[0] : (long)T * 4 * H; p.g_ts = L ? L[1] : 4 * H;
+    p.cs_bs = L ? L[2] : (long)T * H; p.cs_ts = L ? L[3] : H;
+    p.h0_bs = L ? L[4] : H; p.c0_bs = L ? L[5] : H;
     MRG_REQUIRE(((uintptr_t)p.w_hh & 15) == 0, "mrg_lstm_fwd: w_hh must be 16-byte aligned");
   }
   if (cus <= 0) cus = device_cus();
@@ -781,7 +795,8 @@ MRG_API int mrg_lstm_bwd(int nprob, int B, int T, int H,
                          const float* const* c0, const float* const* dy, const long* dy_bs,
                          const long* dy_ts, const float* const* dhT, const float* const* dcT,
                          float* const* dG, float* const* dh0, float* const* dc0, const int* reverse,
-                         void* const* xbuf, int* err, int cus, int force_bs, hipStream_t stream) {
+                         void* const* xbuf, const long* lay, int* err, int cus, int force_bs,
+                         hipStream_t stream) {
   MRG_REQUIRE(nprob >= 1 && nprob <= MAXP, "mrg_lstm_bwd: nprob %d out of range", nprob);
   int G = group_size(H);
   MRG_REQUIRE(G > 0, "mrg_lstm_bwd: unsupported hidden size %d", H);
@@ -797,6 +812,11 @@ MRG_API int mrg_lstm_bwd(int nprob, int B, int T, int H,
     p.dhT = dhT ? dhT[i] : nullptr; p.dcT = dcT ? dcT[i] : nullptr; p.dG = dG[i];
     p.dh0 = dh0 ? dh0[i] : nullptr; p.dc0 = dc0 ? dc0[i] : nullptr;
     p.xbuf = (unsigned long long*)xbuf[i]; p.reverse = reverse ? reverse[i] : 0;
+    const long* L = lay ? lay + 8 * i : nullptr;  // {gates bs, ts, cs bs, ts, c0 bs, dG bs, ts}
+    p.g_bs = L ? L[0] : (long)T * 4 * H; p.g_ts = L ? L[1] : 4 * H;
+    p.cs_bs = L ? L[2] : (long)T * H; p.cs_ts = L ? L[3] : H;
+    p.c0_bs = L ? L[4] : H;
+    p.dG_bs = L ? L[5] : (long)T * 4 * H; p.dG_ts = L ? L[6] : 4 * H;
   }
   if (cus <= 0) cus = device_cus();
   switch (H) {

@@ -116,7 +116,7 @@ __global__ __launch_bounds__(256) void resln_fwd_v4_kernel(const float* __restri
                                                            const float* __restrict__ gamma,
                                                            const float* __restrict__ beta, float* __restrict__ y,
                                                            float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                           int rows, float eps, int E) {
+                                                           int rows, float eps, int E, RowMap ymap) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
@@ -145,7 +145,7 @@ __global__ __launch_bounds__(256) void resln_fwd_v4_kernel(const float* __restri
     }
   }
   const float rstd = rsqrtf(wave_sum(var) * invE + eps);
-  float* py = y + (long)row * E;
+  float* py = y + ymap.off(row);  // the output rows may be laid out differently (time-major -> [B, T, E])
 #pragma unroll
   for (int i = 0; i < EPV; ++i) {
     const int c = i * 256 + lane * 4;
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(256) void resln_bwd_v4_kernel(const float* __restri
                                                            const float* __restrict__ mean_in,
                                                            const float* __restrict__ rstd_in, float* __restrict__ dx,
                                                            float* __restrict__ part, int rows, int rows_per_block,
-                                                           int E) {
+                                                           int E, RowMap dmap) {
   constexpr int EMAX = 256 * EPV;
   __shared__ __attribute__((aligned(16))) float red[4][2][EMAX];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -197,7 +197,7 @@ __global__ __launch_bounds__(256) void resln_bwd_v4_kernel(const float* __restri
         const int c = i * 256 + lane * 4;
         d[q][i] = x[q][i] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (c < E) {
-          d[q][i] = ld4(dy + (long)rr * E + c);
+          d[q][i] = ld4(dy + dmap.off(rr) + c);
           float4 u = ld4(a + (long)rr * E + c), v = ld4(b + (long)rr * E + c);
           x[q][i] = make_float4(u.x + v.x, u.y + v.y, u.z + v.z, u.w + v.w);
         }
@@ -477,9 +477,10 @@ MRG_API int mrg_residual_layernorm_fwd(int rows, int E, const float* a, const fl
                                        (uintptr_t)beta) & 15) == 0;
   if (v4) {
     const int epv = (E + 255) / 256;
-    if (epv == 1) resln_fwd_v4_kernel<1><<<grid, 256, 0, stream>>>(a, b, gamma, beta, y, mean, rstd, rows, eps, E);
-    else if (epv == 2) resln_fwd_v4_kernel<2><<<grid, 256, 0, stream>>>(a, b, gamma, beta, y, mean, rstd, rows, eps, E);
-    else resln_fwd_v4_kernel<4><<<grid, 256, 0, stream>>>(a, b, gamma, beta, y, mean, rstd, rows, eps, E);
+    const RowMap plain{E, 0, 0};
+    if (epv == 1) resln_fwd_v4_kernel<1><<<grid, 256, 0, stream>>>(a, b, gamma, beta, y, mean, rstd, rows, eps, E, plain);
+    else if (epv == 2) resln_fwd_v4_kernel<2><<<grid, 256, 0, stream>>>(a, b, gamma, beta, y, mean, rstd, rows, eps, E, plain);
+    else resln_fwd_v4_kernel<4><<<grid, 256, 0, stream>>>(a, b, gamma, beta, y, mean, rstd, rows, eps, E, plain);
     return check_launch("resln_fwd_v4_kernel");
   }
   const int epl = (E + 63) / 64;
@@ -514,9 +515,10 @@ MRG_API int mrg_residual_layernorm_bwd(int rows, int E, const float* dy, const f
   const int epl = (E + 63) / 64;
   if (v4) {
     const int epv = (E + 255) / 256;
-    if (epv == 1) resln_bwd_v4_kernel<1><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, rpb, E);
-    else if (epv == 2) resln_bwd_v4_kernel<2><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, rpb, E);
-    else resln_bwd_v4_kernel<4><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, rpb, E);
+    const RowMap plain{E, 0, 0};
+    if (epv == 1) resln_bwd_v4_kernel<1><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, rpb, E, plain);
+    else if (epv == 2) resln_bwd_v4_kernel<2><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, rpb, E, plain);
+    else resln_bwd_v4_kernel<4><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, rpb, E, plain);
   } else if (epl <= 1) resln_bwd_kernel<1><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, rpb, E);
   else if (epl <= 2) resln_bwd_kernel<2><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, rpb, E);
   else if (epl <= 4) resln_bwd_kernel<4><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, rpb, E);
@@ -526,6 +528,43 @@ MRG_API int mrg_residual_layernorm_bwd(int rows, int E, const float* dy, const f
   if (!dgamma && !dbeta) return 0;  // partials stay in the workspace (mrg_residual_layernorm_param_reduce)
   MRG_REQUIRE(dgamma && dbeta, "mrg_residual_layernorm_bwd: dgamma and dbeta must both be given or both null");
   return mrg_residual_layernorm_param_reduce(rows, E, workspace, dgamma, dbeta, accumulate, stream);
+}
+
+// Row-mapped forms (E % 4 == 0, 16-B aligned rows): the output rows of the forward and the incoming
+// gradient rows of the backward follow a RowMap, offset(r) = (r / div) * ld_hi + (r % div) * ld_lo
+// (div = 0: r * ld_lo), so a time-major [T, B, E] chunk writes / reads a batch-major [B, T, E] tensor
+// in place (the encoder stack's last LayerNorm, encoder_stack.py).  The backward writes the per-block
+// dgamma / dbeta partials into the workspace for mrg_residual_layernorm_param_reduce.
+MRG_API int mrg_residual_layernorm_fwd_map(int rows, int E, const float* a, const float* b, const float* gamma,
+                                           const float* beta, float eps, float* y, long y_lo, long y_hi, int y_div,
+                                           float* mean, float* rstd, hipStream_t stream) {
+  if (rows == 0) return 0;
+  MRG_REQUIRE(E % 4 == 0 && E <= 1024 && y_lo % 4 == 0 && y_hi % 4 == 0 &&
+                  (((uintptr_t)a | (uintptr_t)b | (uintptr_t)y | (uintptr_t)gamma | (uintptr_t)beta) & 15) == 0,
+              "mrg_residual_layernorm_fwd_map: E %% 4 == 0 and 16-byte aligned rows required (E=%d)", E);
+  const RowMap m{y_lo, y_hi, y_div};
+  dim3 grid((rows + 3) / 4);
+  const int epv = (E + 255) / 256;
+  if (epv == 1) resln_fwd_v4_kernel<1><<<grid, 256, 0, stream>>>(a, b, gamma, beta, y, mean, rstd, rows, eps, E, m);
+  else if (epv == 2) resln_fwd_v4_kernel<2><<<grid, 256, 0, stream>>>(a, b, gamma, beta, y, mean, rstd, rows, eps, E, m);
+  else resln_fwd_v4_kernel<4><<<grid, 256, 0, stream>>>(a, b, gamma, beta, y, mean, rstd, rows, eps, E, m);
+  return check_launch("resln_fwd_v4_kernel");
+}
+
+MRG_API int mrg_residual_layernorm_bwd_map(int rows, int E, const float* dy, long dy_lo, long dy_hi, int dy_div,
+                                           const float* a, const float* b, const float* gamma, const float* mean,
+                                           const float* rstd, float* dx, float* workspace, hipStream_t stream) {
+  if (rows == 0) return 0;
+  MRG_REQUIRE(E % 4 == 0 && E <= 1024 && dy_lo % 4 == 0 && dy_hi % 4 == 0 &&
+                  (((uintptr_t)dy | (uintptr_t)a | (uintptr_t)b | (uintptr_t)dx | (uintptr_t)gamma) & 15) == 0,
+              "mrg_residual_layernorm_bwd_map: E %% 4 == 0 and 16-byte aligned rows required (E=%d)", E);
+  const RowMap m{dy_lo, dy_hi, dy_div};
+  const int nblk = (rows + RESLN_RPB - 1) / RESLN_RPB;
+  const int epv = (E + 255) / 256;
+  if (epv == 1) resln_bwd_v4_kernel<1><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, RESLN_RPB, E, m);
+  else if (epv == 2) resln_bwd_v4_kernel<2><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, RESLN_RPB, E, m);
+  else resln_bwd_v4_kernel<4><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, RESLN_RPB, E, m);
+  return check_launch("resln_bwd_v4_kernel");
 }
 
 MRG_API int mrg_residual_layernorm_param_reduce(int rows, int E, const float* workspace, float* dgamma,

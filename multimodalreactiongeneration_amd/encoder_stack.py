@@ -1,0 +1,380 @@
+"""Layer-wavefront schedule of the first metaformer block's LSTM encoder stacks.
+
+Reference: ``MultiModalMetaformerBlock`` block 0 embeds every modality
+(multi_modal_metaformer.py:102-125) with an ``LSTMMixerLayerd`` per modality: the main
+modality through 1 ``LSTMMixerBlock``, audio and partner through ``encoder_num_layer`` = 5
+(lstmformer.py:165-170, mixer_block.py:833-843).  Each block is
+
+    y = LSTM(x)                       (mixer_block.py:479-507, zero initial state)
+    u = LN1(y + x)                    (ResidualConnection, residual_connection.py:20-37)
+    v = LN2(u W_ff^T + b_ff + u)      (FeedForward, nonlinearity none: one Linear, :37-87)
+
+and the modality's features enter through ``feature_embedding`` (Linear F -> H,
+multi_modal_metaformer.py:433-435,486-490).
+
+Every op above is causal in time, so layer l's time chunk c needs only layer l-1's chunk c
+and its own chunk c-1 (carried h, c).  The stacks therefore run as a wavefront over
+(layer, time chunk): diagonal d holds every (modality, layer l, chunk d - l), and all of
+them are ONE persistent recurrence launch (lstm.hip, up to 12 problems, the (h, c) state
+of chunk c-1 read in place as chunk c's h0 / c0).  Fifteen layers x 300 steps of latency-
+bound recurrence become (chunks + layers - 1) launches of one chunk each: the hand-off
+latencies of the layers in flight overlap instead of adding up.  The backward runs the
+same diagonals in reverse with (dh, dc) carried from chunk c+1 to c.
+
+Layout: everything inside the stack is time-major ([T, B, .] rows t*B + b), so a time
+chunk is a contiguous block of rows for the chunked GEMMs and LayerNorms; the embedding
+GEMM reads the batch-major features through a row map, and the last LayerNorm writes the
+batch-major output the integrators consume (mrg_residual_layernorm_fwd_map).  The
+arithmetic per element is the per-layer path's (same kernels, same fp32 math); only the
+launch granularity changes.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Sequence
+
+import torch
+from torch.autograd import Function
+
+from . import _lib
+from . import functional as Fn
+from .functional import _ptr, _stream, gemm, _fwd_gemm, _dx_gemm, _wgrad, _wt_note, _gbuf, _on_side
+
+# time steps per chunk (the diagonal width); MRG_STACK_CHUNK overrides
+CHUNK = int(os.environ.get("MRG_STACK_CHUNK", "60"))
+MAXP = int(os.environ.get("MRG_STACK_MAXP", "12"))   # problems per recurrence launch (lstm.hip: <= 12)
+VP, CL, CI = ctypes.c_void_p, ctypes.c_long, ctypes.c_int
+_PER_LAYER = 10   # w_ih, w_hh, b_ih, b_hh, ln1 gamma, ln1 beta, w_ff, b_ff, ln2 gamma, ln2 beta
+
+
+def _chunks(T, tc):
+    return [(t0, min(T, t0 + tc)) for t0 in range(0, T, tc)]
+
+
+def _p(t, off=0):
+    return VP(t.data_ptr() + 4 * off)
+
+
+class _Chain:
+    """One modality: features [B, T, F] -> embedding -> L layers (tensors are time-major)."""
+
+    def __init__(self, feat, emb_w, emb_b, layers):
+        self.feat, self.emb_w, self.emb_b, self.layers = feat, emb_w, emb_b, layers
+        self.B, self.T, self.F = feat.shape
+        self.H = emb_w.shape[0]
+        self.L = len(layers)
+
+
+def _launch_fwd(lib, items, B, Tc, H, dev):
+    """One persistent forward launch over `items` = [(chain, layer state dict, t0)]."""
+    n = len(items)
+    xb = torch.zeros(n, lib.mrg_lstm_fwd_xbuf_bytes(B, H) // 8, dtype=torch.int64, device=dev)
+    gx, gbs, gts, whh, bhh, h0, c0, y, ybs, yts, gates, cs, lay, rev = ([] for _ in range(14))
+    for ch, st, t0 in items:
+        r0 = t0 * B
+        gx.append(_p(st["gx"], r0 * 4 * H)); gbs.append(4 * H); gts.append(B * 4 * H)
+        whh.append(_p(st["w_hh"])); bhh.append(_p(st["b_hh"]))
+        h0.append(None if t0 == 0 else _p(st["y"], (r0 - B) * H))
+        c0.append(None if t0 == 0 else _p(st["cs"], (r0 - B) * H))
+        y.append(_p(st["y"], r0 * H)); ybs.append(H); yts.append(B * H)
+        gates.append(_p(st["gates"], r0 * 4 * H)); cs.append(_p(st["cs"], r0 * H))
+        lay += [4 * H, B * 4 * H, H, B * H, H, H, 0, 0]
+        rev.append(0)
+    A = lambda ct, v: (ct * n)(*v)  # noqa: E731
+    with Fn._probe("lstm_fwd", 8.0 * H * H * B * Tc * n):
+        rc = lib.mrg_lstm_fwd(n, B, Tc, H, A(VP, gx), A(CL, gbs), A(CL, gts), A(VP, whh), A(VP, bhh),
+                              A(VP, h0), A(VP, c0), A(VP, y), A(CL, ybs), A(CL, yts), A(VP, gates), A(VP, cs),
+                              None, None, A(CI, rev), A(VP, [_p(xb[i]) for i in range(n)]),
+                              (CL * (8 * n))(*lay), _ptr(Fn._err_flag(dev)), _lib.cu_count(dev.index or 0), 0,
+                              _stream())
+    _lib.check(rc, "lstm fwd (encoder stack)")
+
+
+def _launch_bwd(lib, items, B, Tc, H, dev):
+    """One persistent backward launch over `items` = [(chain, state, grads, t0, dhT, dcT, dh0, dc0)]."""
+    n = len(items)
+    xb = torch.zeros(n, lib.mrg_lstm_bwd_xbuf_bytes(B, H) // 8, dtype=torch.int64, device=dev)
+    whh, gates, cs, c0, dy, dybs, dyts, dhT, dcT, dG, dh0, dc0, lay, rev = ([] for _ in range(14))
+    for ch, st, gr, t0, dh_in, dc_in, dh_out, dc_out in items:
+        r0 = t0 * B
+        whh.append(_p(st["w_hh"])); gates.append(_p(st["gates"], r0 * 4 * H)); cs.append(_p(st["cs"], r0 * H))
+        c0.append(None if t0 == 0 else _p(st["cs"], (r0 - B) * H))
+        dy.append(_p(gr["g1"], r0 * H)); dybs.append(H); dyts.append(B * H)
+        dhT.append(None if dh_in is None else _p(dh_in)); dcT.append(None if dc_in is None else _p(dc_in))
+        dG.append(_p(gr["dG"], r0 * 4 * H))
+        dh0.append(None if dh_out is None else _p(dh_out)); dc0.append(None if dc_out is None else _p(dc_out))
+        lay += [4 * H, B * 4 * H, H, B * H, H, 4 * H, B * 4 * H, 0]
+        rev.append(0)
+    A = lambda ct, v: (ct * n)(*v)  # noqa: E731
+    with Fn._probe("lstm_bwd", 8.0 * H * H * B * Tc * n):
+        rc = lib.mrg_lstm_bwd(n, B, Tc, H, A(VP, whh), A(VP, gates), A(VP, cs), A(VP, c0), A(VP, dy),
+                              A(CL, dybs), A(CL, dyts), A(VP, dhT), A(VP, dcT), A(VP, dG), A(VP, dh0), A(VP, dc0),
+                              A(CI, rev), A(VP, [_p(xb[i]) for i in range(n)]), (CL * (8 * n))(*lay),
+                              _ptr(Fn._err_flag(dev)), _lib.cu_count(dev.index or 0), 0, _stream())
+    _lib.check(rc, "lstm bwd (encoder stack)")
+
+
+def _diagonals(chains, tc):
+    """[(d, [(m, l, c, t0, t1)])]: every (chain, layer, chunk) with l + c = d."""
+    out = []
+    D = max(ch.L + len(_chunks(ch.T, tc)) - 1 for ch in chains)
+    for d in range(D):
+        probs = []
+        for m, ch in enumerate(chains):
+            ck = _chunks(ch.T, tc)
+            for l in range(ch.L):
+                c = d - l
+                if 0 <= c < len(ck):
+                    probs.append((m, l, c, ck[c][0], ck[c][1]))
+        out.append(probs)
+    return out
+
+
+def _groups(items, key):
+    """Split into launches: same key (chunk length), at most MAXP problems each."""
+    by = {}
+    for it in items:
+        by.setdefault(key(it), []).append(it)
+    out = []
+    for k, v in by.items():
+        for s in range(0, len(v), MAXP):
+            out.append((k, v[s:s + MAXP]))
+    return out
+
+
+class _EncoderStackFn(Function):
+    """spec = (layers per chain, chunk length, eps); tensors = per chain [feat, emb_w, emb_b,
+    10 per layer]; returns the last layer's output of every chain, batch-major [B, T, H]."""
+
+    @staticmethod
+    @Fn._keeps_precision
+    def forward(ctx, spec, *tensors):
+        nls, tc, eps = spec
+        lib = _lib.load()
+        chains, k = [], 0
+        for L in nls:
+            feat, ew, eb = tensors[k:k + 3]
+            k += 3
+            layers = [tensors[k + _PER_LAYER * i:k + _PER_LAYER * (i + 1)] for i in range(L)]
+            k += _PER_LAYER * L
+            chains.append(_Chain(feat.contiguous(), ew, eb, layers))
+        _lib.require_device(chains[0].feat)
+        dev = chains[0].feat.device
+        B, H = chains[0].B, chains[0].H
+        f32 = dict(device=dev, dtype=torch.float32)
+        states, outs = [], []
+        for ch in chains:
+            T, F = ch.T, ch.F
+            rows = T * B
+            # embedding, time-major output: A rows read in (t, b) order from the [B, T, F] features
+            x0 = torch.empty(T, B, H, **f32)
+            gemm(rows, H, F, _ptr(ch.feat), 0, T * F, _ptr(ch.emb_w), 1, F, _ptr(x0), H, bias=_ptr(ch.emb_b),
+                 a_hi=F, a_div=B, device=dev)
+            sts = []
+            for l, (w_ih, w_hh, b_ih, b_hh, g1, be1, w_ff, b_ff, g2, be2) in enumerate(ch.layers):
+                st = dict(w_ih=w_ih, w_hh=w_hh, b_ih=b_ih, b_hh=b_hh, g1=g1, be1=be1, w_ff=w_ff, b_ff=b_ff, g2=g2,
+                          be2=be2, x=x0 if l == 0 else sts[-1]["v"],
+                          gx=torch.empty(T, B, 4 * H, **f32), y=torch.empty(T, B, H, **f32),
+                          gates=torch.empty(T, B, 4 * H, **f32), cs=torch.empty(T, B, H, **f32),
+                          u=torch.empty(T, B, H, **f32), z=torch.empty(T, B, H, **f32),
+                          v=torch.empty(T, B, H, **f32) if l + 1 < ch.L else None,
+                          m1=torch.empty(rows, **f32), r1=torch.empty(rows, **f32),
+                          m2=torch.empty(rows, **f32), r2=torch.empty(rows, **f32))
+                _wt_note(w_ih, rows)
+                _wt_note(w_ff, rows)
+                sts.append(st)
+            states.append(sts)
+            outs.append(torch.empty(B, T, H, **f32))
+
+        for probs in _diagonals(chains, tc):
+            for m, l, c, t0, t1 in probs:   # input projections of this diagonal's chunks
+                st = states[m][l]
+                r0, n = t0 * B, (t1 - t0) * B
+                _fwd_gemm(n, 4 * H, H, _p(st["x"], r0 * H), H, st["w_ih"], _p(st["gx"], r0 * 4 * H), 4 * H,
+                          bias=_ptr(st["b_ih"]), device=dev)
+            for tlen, grp in _groups(probs, key=lambda p: p[4] - p[3]):
+                _launch_fwd(lib, [(chains[m], states[m][l], t0) for m, l, c, t0, t1 in grp], B, tlen, H, dev)
+            for m, l, c, t0, t1 in probs:   # residual LN, FeedForward, residual LN of the chunk
+                ch, st = chains[m], states[m][l]
+                r0, n = t0 * B, (t1 - t0) * B
+                _lib.check(lib.mrg_residual_layernorm_fwd(
+                    n, H, _p(st["y"], r0 * H), _p(st["x"], r0 * H), _ptr(st["g1"]), _ptr(st["be1"]), eps,
+                    _p(st["u"], r0 * H), _p(st["m1"], r0), _p(st["r1"], r0), _stream()), "layernorm fwd")
+                _fwd_gemm(n, H, H, _p(st["u"], r0 * H), H, st["w_ff"], _p(st["z"], r0 * H), H, bias=_ptr(st["b_ff"]),
+                          device=dev)
+                if st["v"] is not None:
+                    rc = lib.mrg_residual_layernorm_fwd(
+                        n, H, _p(st["z"], r0 * H), _p(st["u"], r0 * H), _ptr(st["g2"]), _ptr(st["be2"]), eps,
+                        _p(st["v"], r0 * H), _p(st["m2"], r0), _p(st["r2"], r0), _stream())
+                else:   # last layer: rows (t, b) land in the batch-major output [B, T, H]
+                    rc = lib.mrg_residual_layernorm_fwd_map(
+                        n, H, _p(st["z"], r0 * H), _p(st["u"], r0 * H), _ptr(st["g2"]), _ptr(st["be2"]), eps,
+                        _p(outs[m], t0 * H), ch.T * H, H, B, _p(st["m2"], r0), _p(st["r2"], r0), _stream())
+                _lib.check(rc, "layernorm fwd (encoder stack)")
+
+        ctx.chains, ctx.tc, ctx.B, ctx.H = chains, tc, B, H
+        save = []
+        for sts in states:
+            for st in sts:
+                st.pop("gx")   # not needed by the backward
+                for key in ("x", "y", "gates", "cs", "u", "z", "m1", "r1", "m2", "r2"):
+                    save.append(st[key])
+        ctx.save_for_backward(*save)
+        ctx.keys = ("x", "y", "gates", "cs", "u", "z", "m1", "r1", "m2", "r2")
+        ctx.params = [[{k2: st[k2] for k2 in ("w_ih", "w_hh", "b_ih", "b_hh", "g1", "be1", "w_ff", "b_ff", "g2",
+                                               "be2")} for st in sts] for sts in states]
+        return tuple(outs)
+
+    @staticmethod
+    @Fn._keeps_precision
+    def backward(ctx, *douts):
+        chains, tc, B, H = ctx.chains, ctx.tc, ctx.B, ctx.H
+        lib = _lib.load()
+        saved = list(ctx.saved_tensors)
+        dev = saved[0].device
+        f32 = dict(device=dev, dtype=torch.float32)
+        states, k = [], 0
+        for m, ch in enumerate(chains):
+            sts = []
+            for l in range(ch.L):
+                st = dict(zip(ctx.keys, saved[k:k + len(ctx.keys)]))
+                k += len(ctx.keys)
+                st.update(ctx.params[m][l])
+                sts.append(st)
+            states.append(sts)
+        grads, carry = [], {}
+        wsb = lib.mrg_residual_layernorm_bwd_workspace_bytes
+        for m, ch in enumerate(chains):
+            T, rows = ch.T, ch.T * B
+            nblk = sum((c1 - c0) * B // 32 + ((c1 - c0) * B % 32 > 0) for c0, c1 in _chunks(T, tc))
+            gl = []
+            for l in range(ch.L):
+                gl.append(dict(dG=torch.empty(T, B, 4 * H, **f32), g1=torch.empty(T, B, H, **f32),
+                               g2=torch.empty(T, B, H, **f32),
+                               dv=torch.empty(T, B, H, **f32),   # gradient of this layer's input x
+                               ws1=torch.empty(nblk * 2 * H, **f32), ws2=torch.empty(nblk * 2 * H, **f32),
+                               nblk=nblk))
+                carry[(m, l)] = [torch.empty(B, H, **f32) for _ in range(4)]   # dh, dc of two chunks
+            grads.append(gl)
+            if douts[m] is None:
+                douts = list(douts)
+                douts[m] = torch.zeros(B, T, H, **f32)
+        douts = [d.contiguous() for d in douts]
+
+        def block_off(T, c):
+            return sum((c1 - c0) * B // 32 + ((c1 - c0) * B % 32 > 0) for c0, c1 in _chunks(T, tc)[:c])
+
+        diags = _diagonals(chains, tc)
+        # backward: diagonals in reverse, within one the chunk index of every chain's top layer first
+        rdiag = []
+        D = max(ch.L + len(_chunks(ch.T, tc)) - 1 for ch in chains)
+        for rd in range(D):
+            probs = []
+            for m, ch in enumerate(chains):
+                ck = _chunks(ch.T, tc)
+                for l in range(ch.L - 1, -1, -1):
+                    c = len(ck) - 1 - (rd - (ch.L - 1 - l))
+                    if 0 <= c < len(ck):
+                        probs.append((m, l, c, ck[c][0], ck[c][1]))
+            rdiag.append(probs)
+        del diags
+
+        for probs in rdiag:
+            for m, l, c, t0, t1 in probs:   # LN2, FeedForward, LN1 backward of the chunk
+                ch, st, gr = chains[m], states[m][l], grads[m][l]
+                r0, n = t0 * B, (t1 - t0) * B
+                bo = block_off(ch.T, c) * 2 * H
+                if l == ch.L - 1:   # the stack's output gradient, batch-major
+                    rc = lib.mrg_residual_layernorm_bwd_map(
+                        n, H, _p(douts[m], t0 * H), ch.T * H, H, B, _p(st["z"], r0 * H), _p(st["u"], r0 * H),
+                        _ptr(st["g2"]), _p(st["m2"], r0), _p(st["r2"], r0), _p(gr["g2"], r0 * H),
+                        _p(gr["ws2"], bo), _stream())
+                else:
+                    rc = lib.mrg_residual_layernorm_bwd_map(
+                        n, H, _p(grads[m][l + 1]["dv"], r0 * H), H, 0, 0, _p(st["z"], r0 * H), _p(st["u"], r0 * H),
+                        _ptr(st["g2"]), _p(st["m2"], r0), _p(st["r2"], r0), _p(gr["g2"], r0 * H),
+                        _p(gr["ws2"], bo), _stream())
+                _lib.check(rc, "layernorm bwd (encoder stack)")
+                du = torch.empty(n, H, **f32)   # d(u) = g2 W_ff + g2 (residual branch in the epilogue)
+                _dx_gemm(n, H, H, _p(gr["g2"], r0 * H), H, st["w_ff"], _ptr(du), H, epi=3, aux=_p(gr["g2"], r0 * H),
+                         ldaux=H, device=dev)
+                _lib.check(lib.mrg_residual_layernorm_bwd_map(
+                    n, H, _ptr(du), H, 0, 0, _p(st["y"], r0 * H), _p(st["x"], r0 * H), _ptr(st["g1"]),
+                    _p(st["m1"], r0), _p(st["r1"], r0), _p(gr["g1"], r0 * H), _p(gr["ws1"], bo), _stream()),
+                    "layernorm bwd (encoder stack)")
+            items = {}
+            for m, l, c, t0, t1 in probs:
+                ch = chains[m]
+                nc = len(_chunks(ch.T, tc))
+                cb = carry[(m, l)]
+                cur, nxt = (cb[0], cb[1]) if c % 2 == 0 else (cb[2], cb[3])   # this chunk's dh0 / dc0 out
+                prv = (cb[2], cb[3]) if c % 2 == 0 else (cb[0], cb[1])        # chunk c+1's dh0 / dc0
+                dh_in, dc_in = (None, None) if c == nc - 1 else prv
+                dh_out, dc_out = (None, None) if c == 0 else (cur, nxt)
+                items.setdefault(t1 - t0, []).append(
+                    (ch, states[m][l], grads[m][l], t0, dh_in, dc_in, dh_out, dc_out))
+            for tlen, grp in items.items():
+                for s in range(0, len(grp), MAXP):
+                    _launch_bwd(lib, grp[s:s + MAXP], B, tlen, H, dev)
+            for m, l, c, t0, t1 in probs:   # input gradient of the chunk: dG W_ih + g1 (residual)
+                ch, st, gr = chains[m], states[m][l], grads[m][l]
+                r0, n = t0 * B, (t1 - t0) * B
+                _dx_gemm(n, H, 4 * H, _p(gr["dG"], r0 * 4 * H), 4 * H, st["w_ih"], _p(gr["dv"], r0 * H), H, epi=3,
+                         aux=_p(gr["g1"], r0 * H), ldaux=H, device=dev)
+                if c == 0:
+                    _EncoderStackFn._weight_grads(lib, ch, st, gr, l, B, H, dev)
+        return (None,) + tuple(_EncoderStackFn._input_grads(chains, ctx.needs_input_grad))
+
+    @staticmethod
+    def _weight_grads(lib, ch, st, gr, l, B, H, dev):
+        """Every parameter gradient of layer l over the whole sequence (its last chunk is done)."""
+        T = ch.T
+        rows = T * B
+        dG, g2, g1 = gr["dG"], gr["g2"], gr["g1"]
+        gbi, gbh = _gbuf(st["b_ih"]), _gbuf(st["b_hh"])
+        first = gbi if gbi is not None else gbh
+        _wgrad(_ptr(dG), 4 * H, _ptr(st["x"]), H, rows, 4 * H, H, _gbuf(st["w_ih"]), dev, gb=first,
+               gb2=gbh if gbi is not None else None, keep=(dG, st["x"]))
+        gw = _gbuf(st["w_hh"])
+        if gw is not None and T > 1:   # sum_t dG_t^T y_{t-1}: time-major rows shifted by one step (B rows)
+            _wgrad(_p(dG, B * 4 * H), 4 * H, _ptr(st["y"]), H, (T - 1) * B, 4 * H, H, gw, dev, keep=(dG, st["y"]))
+        _wgrad(_ptr(g2), H, _ptr(st["u"]), H, rows, H, H, _gbuf(st["w_ff"]), dev, gb=_gbuf(st["b_ff"]),
+               keep=(g2, st["u"]))
+        for ws, gam, bet in ((gr["ws1"], st["g1"], st["be1"]), (gr["ws2"], st["g2"], st["be2"])):
+            gg, gb = _gbuf(gam), _gbuf(bet)
+            if gg is None and gb is None:
+                continue
+
+            def reduce(ws=ws, gg=gg, gb=gb, nblk=gr["nblk"]):
+                scratch = torch.empty(2, H, device=dev, dtype=torch.float32) if (gg is None or gb is None) else None
+                _lib.check(lib.mrg_residual_layernorm_param_reduce(
+                    nblk * 32, H, _ptr(ws), _ptr(gg if gg is not None else scratch[0]),
+                    _ptr(gb if gb is not None else scratch[1]), 1, _stream()), "layernorm param reduce")
+            _on_side(dev, rows, (ws,), reduce)
+        if l == 0:   # the embedding: dW_emb = sum dx0^T feat (features read time-major through a row map)
+            dx0 = gr["dv"]
+            _wgrad(_ptr(dx0), H, _ptr(ch.feat), T * ch.F, rows, H, ch.F, _gbuf(ch.emb_w), dev, x_hi=ch.F, x_div=B,
+                   gb=_gbuf(ch.emb_b), keep=(dx0, ch.feat))
+
+    @staticmethod
+    def _input_grads(chains, need):
+        # the features are data (no gradient), parameters get theirs in place through _gbuf
+        return [None] * (len(need) - 1)
+
+
+def stack_eligible(H, B) -> bool:
+    lib = _lib.load()
+    return bool(lib.mrg_lstm_supported_hidden(H)) and H % 4 == 0 and Fn._ARITH[0] is None
+
+
+def encoder_stack(chains: Sequence[Sequence], eps: float, chunk: int = 0) -> List[torch.Tensor]:
+    """chains: [(feat [B, T, F], emb_w, emb_b, [(w_ih, w_hh, b_ih, b_hh, ln1_w, ln1_b, ff_w, ff_b, ln2_w,
+    ln2_b)] per layer)]; returns the last layer's output of every chain ([B, T, H], batch-major)."""
+    flat, nls = [], []
+    for feat, ew, eb, layers in chains:
+        flat += [feat, ew, eb]
+        for lay in layers:
+            flat += list(lay)
+        nls.append(len(layers))
+    return list(_EncoderStackFn.apply((tuple(nls), int(chunk or CHUNK), float(eps)), *flat))

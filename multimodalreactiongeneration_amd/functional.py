@@ -518,8 +518,11 @@ def set_weight_planes(on: bool) -> bool:
 
 
 def invalidate_weight_planes():
-    """The weights changed (optimizer step): forget their planes until the next prepare."""
+    """The weights changed (optimizer step): forget their planes and their [in][out] copies (_WT_CACHE)
+    until the next forward notes them again, so no backward can use a transpose of old weights."""
     _PLANES.clear()
+    _WT_CACHE.clear()
+    _WT_PENDING.clear()
 
 
 def prepare_weight_planes(weights):
@@ -916,7 +919,7 @@ class _LSTMFn(Function):
             arr(VP, [_ptr(g) for g in gates]), arr(VP, [_ptr(c) for c in cs]),
             arr(VP, [_ptr(h) for h in hT]), arr(VP, [_ptr(c) for c in cT]),
             arr(ctypes.c_int, [int(r) for r in reverse]),
-            arr(VP, [_ptr(xbuf[i]) for i in range(nprob)]), _ptr(_err_flag(dev)),
+            arr(VP, [_ptr(xbuf[i]) for i in range(nprob)]), None, _ptr(_err_flag(dev)),
             _lib.cu_count(dev.index or 0), force_bs, _stream())
         pr.__exit__()
         _lib.check(rc, "lstm fwd")
@@ -1006,7 +1009,7 @@ class _LSTMFn(Function):
             arr(VP, [_ptr(t) for t in dhT]), arr(VP, [_ptr(t) for t in dcT]),
             arr(VP, [_ptr(t) for t in dG]), arr(VP, [_ptr(t) for t in dh0]),
             arr(VP, [_ptr(t) for t in dc0]), arr(ctypes.c_int, [int(r) for r in reverse]),
-            arr(VP, [_ptr(xbuf[i]) for i in range(nprob)]), _ptr(_err_flag(dev)),
+            arr(VP, [_ptr(xbuf[i]) for i in range(nprob)]), None, _ptr(_err_flag(dev)),
             _lib.cu_count(dev.index or 0), force_bs, _stream())
         pr.__exit__()
         _lib.check(rc, "lstm bwd")
@@ -1318,8 +1321,9 @@ class _MHAFn(Function):
         _lib.check(rc, "attention fwd")
         out = torch.empty(B, Tq, E, device=dev, dtype=torch.float32)
         _fwd_gemm(B * Tq, E, E, _ptr(O), E, out_w, _ptr(out), E, bias=_ptr(out_b), device=dev)
-        need_in = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
-        _wt_note(out_w, B * Tq, need_in)
+        # dO = dout W_out runs in every backward (the in_proj weight gradient needs dO even when
+        # neither input does), so out_w is noted unconditionally (a stale copy is never reused)
+        _wt_note(out_w, B * Tq)
         _wt_note(in_w[:E], B * Tq, ctx.needs_input_grad[1])
         _wt_note(in_w[E:], B * Tk, ctx.needs_input_grad[2])
         extra = []

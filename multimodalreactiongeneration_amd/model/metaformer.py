@@ -11,6 +11,7 @@ which is legal because the reference's recurrent state is never carried
 """
 from __future__ import annotations
 
+import os
 from typing import Any, List, Tuple
 
 import torch
@@ -229,6 +230,57 @@ class MultiModalMetaformer(nn.Module):
                         xs[i] = chains[i][layer].feed_forward(u)
         return xs
 
+    # ---- MI355X schedule: block 0's embedding stacks as one layer-wavefront (encoder_stack.py);
+    # MRG_ENCODER_STACK=1 turns it on (off by default until the recurrence's large-batch-tile form
+    # makes the wavefront's wider launches pay: DESIGN.md §8)
+    use_encoder_stack = os.environ.get("MRG_ENCODER_STACK", "0") == "1"
+
+    def _stack_layers(self, block: MultiModalMetaformerBlock):
+        """Per modality the (w_ih, w_hh, b_ih, b_hh, ln1, ff, ln2) tensors of block 0's LSTM blocks, or
+        None when a block is outside the stack's form (LSTM 1-layer unidirectional H -> H, residual LN,
+        FeedForward = one Linear + residual LN, one LayerNorm eps)."""
+        from torch import nn as _nn
+        out, eps = [], set()
+        for lay in block.embedding.modal_embeddings:
+            layers = []
+            for mb in lay.mixer:
+                lstm = mb.mixer.module.mixer if isinstance(mb.mixer, ResidualConnection) else None
+                ff = getattr(mb.feed_forward, "feed_forward", None)
+                if lstm is None or lstm.num_layers != 1 or lstm.bidirectional or mb.mixer.layer_norm is None:
+                    return None
+                if lstm.input_size != lstm.hidden_size or not isinstance(ff, ResidualConnection) or ff.layer_norm is None:
+                    return None
+                mods = list(ff.module.children())
+                if len(mods) != 1 or not isinstance(mods[0], _nn.Linear) or mods[0].bias is None:
+                    return None
+                ln1, ln2 = mb.mixer.layer_norm, ff.layer_norm
+                eps.update((ln1.eps, ln2.eps))
+                layers.append((*lstm.direction_params(0), ln1.weight, ln1.bias, mods[0].weight, mods[0].bias,
+                               ln2.weight, ln2.bias))
+            out.append(layers)
+        if len(eps) != 1:
+            return None
+        return out, eps.pop()
+
+    def _stack_first_block(self, block, feats):
+        """Block 0's embeddings (feature Linear + every LSTM block of every modality) as one wavefront, or
+        None when outside it (the per-layer schedule below then runs)."""
+        from ..encoder_stack import encoder_stack, stack_eligible
+        if not (self.use_encoder_stack and block.encode_other_modal and len(feats) == self.modal_num):
+            return None
+        got = self._stack_layers(block)
+        if got is None:
+            return None
+        layers, eps = got
+        H = self.hidden_dim
+        if not (stack_eligible(H, feats[0].shape[0]) and all(f.dim() == 3 and f.is_cuda and f.shape[1] >= 8
+                                                             and f.shape[0] == feats[0].shape[0] for f in feats)):
+            return None
+        embs = list(self.feature_embedding)
+        if any(e.bias is None for e in embs):
+            return None
+        return encoder_stack([(f, e.weight, e.bias, l) for f, e, l in zip(feats, embs, layers)], eps)
+
     def _fast_eligible(self) -> bool:
         if self.interlayer_residual:
             return False
@@ -250,14 +302,18 @@ class MultiModalMetaformer(nn.Module):
         The record the reference returns holds only None leaves (states are never
         produced), and feeding it back is stateless; both are mirrored.
         """
-        main_modal = self.feature_embedding[0](main_modal)
-        other_modals = [self.feature_embedding[i + 1](o) for i, o in enumerate(other_modals)]
-        if _none_leaves(hx) and _none_leaves(main_modal_others) and _none_leaves(other_modals_others) \
-                and self._fast_eligible():
+        fast = _none_leaves(hx) and _none_leaves(main_modal_others) and _none_leaves(other_modals_others) \
+            and self._fast_eligible()
+        stacked = self._stack_first_block(self.metaformer_blocks[0], [main_modal] + list(other_modals)) \
+            if fast else None
+        if stacked is None:
+            main_modal = self.feature_embedding[0](main_modal)
+            other_modals = [self.feature_embedding[i + 1](o) for i, o in enumerate(other_modals)]
+        if fast:
             record = []
-            for block in self.metaformer_blocks:
+            for bi, block in enumerate(self.metaformer_blocks):
                 mods = [main_modal] + (list(other_modals) if block.encode_other_modal else [])
-                enc = self._fast_first_embedding(block, mods)
+                enc = stacked if (bi == 0 and stacked is not None) else self._fast_first_embedding(block, mods)
                 main_modal = enc[0]
                 if block.encode_other_modal:
                     other_modals = enc[1:]

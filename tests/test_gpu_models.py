@@ -423,3 +423,43 @@ def test_simple_lstm_bf16_gate_vs_fp32_oracle():
         g, r = p.grad.detach().double().cpu().flatten(), grads[k].double().flatten()
         if r.norm() > 1e-12:
             assert torch.nn.functional.cosine_similarity(g, r, dim=0) >= 0.99, k
+
+
+@pytest.mark.parametrize("chunk,ratio,B,T", [(60, 1, 64, 300), (7, 2, 6, 40), (300, 1, 8, 50)])
+def test_encoder_stack_matches_per_layer_schedule(chunk, ratio, B, T):
+    """Block 0's embedding stacks as a (layer, time chunk) wavefront (encoder_stack.py) vs the
+    per-layer schedule: same loss, output and every parameter gradient (fp32 reorderings only:
+    weight-gradient sums run over time-major rows).  Ragged chunks (T % chunk != 0), audio at
+    twice the frame rate (more chunks than the pose chains) and padded frames included."""
+    from multimodalreactiongeneration_amd import configs as C
+    from multimodalreactiongeneration_amd import encoder_stack as ES
+    from multimodalreactiongeneration_amd.model import Metaformer
+    from multimodalreactiongeneration_amd.synthetic import make_batch, clone_batch
+    mc, oc, me = C.lstmformer_config(ratio=ratio)
+    torch.manual_seed(0)
+    m = Metaformer(mc, oc, me).to(DEV)
+    lengths = [T] * B
+    lengths[-1] = T - 5
+    batch = make_batch(B=B, T=T, lead=3, ratio=ratio, seed=11, lengths=lengths, device=DEV)
+    prev = ES.CHUNK
+    out = []
+    try:
+        ES.CHUNK = chunk
+        for use in (False, True):
+            m.metaformer.use_encoder_stack = use
+            for p in m.parameters():
+                p.grad = None
+            y = m(*clone_batch(batch, DEV)[:-1])[0]
+            loss = m.training_step(clone_batch(batch, DEV))["loss"]
+            loss.backward()
+            torch.cuda.synchronize()
+            out.append((y.detach().clone(), loss.detach().clone(),
+                        {k: p.grad.detach().clone() for k, p in m.named_parameters()}))
+    finally:
+        ES.CHUNK = prev
+        m.metaformer.use_encoder_stack = type(m.metaformer).use_encoder_stack
+    (y0, l0, g0), (y1, l1, g1) = out
+    assert rel_err(y1, y0) < 1e-5
+    assert abs(l1.item() - l0.item()) <= 1e-6 * abs(l0.item())
+    for k in g0:
+        assert rel_err(g1[k], g0[k]) < 1e-5, k

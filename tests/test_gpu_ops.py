@@ -235,6 +235,49 @@ def test_weight_grad_kernels_vs_fp64(rows, N, In, time_shift, wg):
     assert rel_err(gb, ref_b) < 2e-6
 
 
+def _bf16(t):
+    return t.to(torch.bfloat16).double()
+
+
+@pytest.mark.parametrize("M,N,K,kind", [(19200, 1024, 256, "nt"), (19200, 256, 256, "nt"), (4800, 512, 512, "nt"),
+                                        (19200, 1024, 256, "wgrad"), (19200, 256, 256, "wgrad")])
+def test_bf16_gemm_kernels_are_bf16_operands(M, N, K, kind):
+    """precision 'bf16' (BASELINE configs[1]): the LDS-DMA kernels' one-plane form (gemm_x6g_kernel /
+    gemm_x6g_wgrad_kernel with NP = 1) rounds each operand to bf16 (RNE) and accumulates in fp32:
+    equal to fp64 on the bf16-rounded operands up to fp32 accumulation, and visibly NOT the fp32
+    product (the arithmetic really is bf16)."""
+    from multimodalreactiongeneration_amd import functional as Fn
+    g = torch.Generator().manual_seed(M + N + K)
+    prev = Fn.set_wgrad_stream(False)
+    try:
+        with Fn.precision("bf16"):
+            if kind == "nt":
+                a = torch.randn(M, K, generator=g)
+                w = torch.randn(N, K, generator=g) / math.sqrt(K)
+                ad, wd = a.to(DEV), w.to(DEV)
+                c = torch.empty(M, N, device=DEV)
+                Fn.gemm(M, N, K, Fn._ptr(ad), 0, K, Fn._ptr(wd), 1, K, Fn._ptr(c), N, device=DEV)
+                exact = a.double() @ w.double().t()
+                ref = _bf16(a) @ _bf16(w).t()
+                out = c
+            else:
+                dy = torch.randn(M, N, generator=g)
+                x = torch.randn(M, K, generator=g)
+                dyd, xd = dy.to(DEV), x.to(DEV)
+                gw = torch.zeros(N, K, device=DEV)
+                gb = torch.zeros(N, device=DEV)
+                Fn._wgrad(Fn._ptr(dyd), N, Fn._ptr(xd), K, M, N, K, gw, DEV, gb=gb, keep=(dyd, xd))
+                exact = dy.double().t() @ x.double()
+                ref = _bf16(dy).t() @ _bf16(x)
+                out = gw
+                assert rel_err(gb, dy.double().sum(0)) < 2e-6   # bias sums stay fp32
+            torch.cuda.synchronize()
+    finally:
+        Fn.set_wgrad_stream(prev)
+    assert rel_err(out, ref) < 2e-6
+    assert rel_err(out, exact) > 1e-4
+
+
 @pytest.mark.parametrize("M,N,K,transB,a_off", [
     (64, 256, 1024, 0, 0), (64, 128, 512, 1, 0), (37, 96, 516, 0, 0), (64, 256, 1024, 1, 1), (50, 40, 64, 1, 3)])
 def test_few_row_gemm_operand_layouts(M, N, K, transB, a_off):
@@ -464,25 +507,40 @@ def test_lstm_single_step_chain_vs_oracle(H, In, B):
         assert rel_err(p.grad, r.grad) < TOL
 
 
-@pytest.mark.parametrize("bs", [1, 2, 4, 8])
-def test_lstm_batched_problems_and_forced_tiling(bs):
-    """3 independent recurrences in one launch, every batch-tile size, vs the oracle."""
+@pytest.mark.parametrize("bs,group", [(1, 8), (2, 8), (4, 8), (8, 8), (16, 8), (8, 16), (16, 16)])
+def test_lstm_batched_problems_and_forced_tiling(bs, group):
+    """3 independent recurrences in one launch, every batch-tile size and group size, vs the oracle
+    (outputs and input / weight gradients; batch tile 16 runs the backward's self-io form)."""
+    from multimodalreactiongeneration_amd import _lib
     from multimodalreactiongeneration_amd import functional as Fn
     from oracle import mrg_oracle as O
-    H, B, T = 256, 16, 40
+    lib = _lib.load()
+    H, B, T = 256, 20, 40   # 3 x 20 rows at batch tile 1 = 480 workgroups (fits 512); ragged last tiles
     g = torch.Generator().manual_seed(bs)
     probs, refs = [], []
     for _ in range(3):
         w = [torch.randn(4 * H, H, generator=g) * 0.06 for _ in range(2)]
         bb = [torch.randn(4 * H, generator=g) * 0.06 for _ in range(2)]
         x = torch.randn(B, T, H, generator=g)
-        probs.append((x.to(DEV), _param(w[0]), _param(w[1]), _param(bb[0]), _param(bb[1])))
-        refs.append(O.lstm_layer(x, w[0], w[1], bb[0], bb[1])[0])
-    ys = Fn.lstm_layers_batched(probs, force_bs=bs)
-    sum(y.sum() for y in ys).backward()
-    torch.cuda.synchronize()
-    for y, r in zip(ys, refs):
-        assert rel_err(y, r) < TOL
+        probs.append((x.to(DEV).requires_grad_(True), _param(w[0]), _param(w[1]), _param(bb[0]), _param(bb[1])))
+        xr = x.clone().requires_grad_(True)
+        rw = [t.clone().requires_grad_(True) for t in (w[0], w[1], bb[0], bb[1])]
+        yr = O.lstm_layer(xr, *rw)[0]
+        yr.square().sum().backward()
+        refs.append((yr, xr, rw))
+    try:
+        _lib.check(lib.mrg_lstm_config(group), "group")
+        ys = Fn.lstm_layers_batched(probs, force_bs=bs)
+        sum(y.square().sum() for y in ys).backward()
+        torch.cuda.synchronize()
+        Fn.check_errors()
+    finally:
+        lib.mrg_lstm_config(8)
+    for y, p, (yr, xr, rw) in zip(ys, probs, refs):
+        assert rel_err(y, yr) < TOL
+        assert rel_err(p[0].grad, xr.grad) < TOL
+        for a, r in zip(p[1:], rw):
+            assert rel_err(a.grad, r.grad) < TOL
 
 
 @pytest.mark.parametrize("H,B", [(256, 64), (256, 24), (128, 16), (32, 5)])

@@ -20,9 +20,11 @@ def main():
     lib = _lib.load()
     H, B, T = 256, 64, 300
     g = torch.Generator().manual_seed(0)
-    for G in (8, 16):
-        _lib.check(lib.mrg_lstm_config(G), "cfg")
-        for nprob in (1, 2, 3):
+    nps = [int(v) for v in os.environ.get("NPROB", "1,2,3").split(",")]
+    bss = [int(v) for v in os.environ.get("FORCE_BS", "0").split(",")]
+    gs = [int(v) for v in os.environ.get("GROUPS", "8,16").split(",")]
+    for G, nprob, fbs in [(G, n, b) for G in gs for n in nps for b in bss]:
+            _lib.check(lib.mrg_lstm_config(G), "cfg")
             probs = []
             for _ in range(nprob):
                 w = [(torch.randn(4 * H, H, generator=g) * 0.06).to(DEV).requires_grad_(True) for _ in range(2)]
@@ -31,21 +33,21 @@ def main():
                 probs.append((x, w[0], w[1], bb[0], bb[1]))
             try:
                 for _ in range(2):
-                    ys = Fn.lstm_layers_batched(probs)
+                    ys = Fn.lstm_layers_batched(probs, force_bs=fbs)
                     sum(y.sum() for y in ys).backward()
             except RuntimeError as e:
-                print(f"G={G:2d} nprob={nprob}  {e}", flush=True)
+                print(f"G={G:2d} nprob={nprob} bs={fbs}  {e}", flush=True)
                 continue
             torch.cuda.synchronize()
             Fn.probe_start("lstm_fwd", "lstm_bwd")
             for _ in range(5):
-                ys = Fn.lstm_layers_batched(probs)
+                ys = Fn.lstm_layers_batched(probs, force_bs=fbs)
                 sum(y.sum() for y in ys).backward()
             t = Fn.probe_stop()
             Fn.check_errors()
             f = sorted(t.get("lstm_fwd", [0]))[len(t.get("lstm_fwd", [0])) // 2]
             b = sorted(t.get("lstm_bwd", [0]))[len(t.get("lstm_bwd", [0])) // 2]
-            print(f"G={G:2d} nprob={nprob}  fwd {f * 1e3:7.1f} us ({f * 1e3 / T:5.2f} us/step)  "
+            print(f"G={G:2d} nprob={nprob:2d} bs={fbs:2d}  fwd {f * 1e3:7.1f} us ({f * 1e3 / T:5.2f} us/step)  "
                   f"bwd {b * 1e3:7.1f} us ({b * 1e3 / T:5.2f} us/step)", flush=True)
 
 

@@ -45,14 +45,18 @@ for k in sorted(set(fetch) | set(write)):
                   "hbm_bytes_per_launch": sum(rd) / len(rd) + sum(wr) / len(wr)}
 
 
-def fam_total(prefix):
+def fam_total(prefix, extra=()):
+    """Bytes per launch of the kernels matching `prefix`; kernels matching `extra` (helpers issued
+    inside the same library call, e.g. the split-K slab reduce of a weight-gradient GEMM) add their
+    bytes but not their dispatches, so the figure is per library launch, like the bench's probe."""
     prefixes = (prefix,) if isinstance(prefix, str) else prefix
     ks = [k for k in summary if k.startswith(prefixes)]
+    xs = [k for k in summary if extra and k.startswith(tuple(extra))]
     n = sum(summary[k]["dispatches"] for k in ks)
     if not n:
         return None
-    tot = sum(summary[k]["hbm_bytes_per_launch"] * summary[k]["dispatches"] for k in ks)
-    return {"dispatches": n, "hbm_bytes_per_launch": tot / n, "variants": ks}
+    tot = sum(summary[k]["hbm_bytes_per_launch"] * summary[k]["dispatches"] for k in ks + xs)
+    return {"dispatches": n, "hbm_bytes_per_launch": tot / n, "variants": ks, "helpers": xs}
 
 
 doc = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) over "
@@ -60,7 +64,9 @@ doc = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes
        "families": dict({p: fam_total(p) for p in ("lstm_fwd_kernel", "lstm_bwd_kernel", "gemm_x6_kernel", "gemm_f32_kernel",
                                                    "splitk_reduce", "attn_fwd_kernel", "attn_bwd", "resln",
                                                    "adamw_kernel")},
-                        gemm_all=fam_total(("gemm_x6_kernel", "gemm_x6g_kernel", "gemm_rows_kernel"))),
+                        gemm_all=fam_total(("gemm_x6_kernel", "gemm_x6g_kernel", "gemm_x6g_wgrad_kernel",
+                                            "gemm_rows_kernel", "gemm_f32_kernel", "gemm_bf16"),
+                                           extra=("splitk_reduce",))),
        "kernels": summary}
 txt = json.dumps(doc, indent=1)
 if dst:
