@@ -161,6 +161,11 @@ int mrg_lstm_bwd(int nprob, int B, int T, int H,
  * hand-off, so the recurrence times out and reports through *err; 0 disarms.  Process-wide.  */
 int mrg_lstm_debug_inject(int mode);
 
+/* MFMA form of the H = 256 recurrences (batch tiles of 16 rows, x6 bf16 split on
+ * v_mfma_f32_16x16x32_bf16, fp32-class): mode 0 never, 1 (default) when the VALU form would need
+ * batch tiles >= min_bs (several problems per launch), 2 whenever its grid fits; min_bs <= 0 keeps
+ * the current threshold.  Returns the previous mode.  Process-wide.  */
+int mrg_lstm_set_mx(int mode, int min_bs);
 /* Tuning knob: number of workgroups that share one batch row group at H = 256
  * (8 or 16; default 8).  Process-wide; set before capture, not during. */
 int mrg_lstm_config(int group256);

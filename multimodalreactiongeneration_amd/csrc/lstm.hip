@@ -33,208 +33,10 @@
 // P_j[b][:] = dG_j[b] W_hh[rows_j, :] over ALL H outputs; the exchange is a
 // reduce-scatter (each member sums the G partials of its own units), so the
 // bytes moved per step equal the forward's (BS x H granules per member).
-#include "mrg_common.h"
+#include "lstm_common.h"
 #include <cstdlib>
 
 namespace mrg {
-
-static constexpr int MAXP = 12;  // problems per launch (kernarg: 12 x 176 B)
-
-struct LstmFwdProblem {
-  const float* gx;  // pre-activations from the input GEMM (+ b_ih)
-  long gx_bs, gx_ts;
-  const float* w_hh;  // [4H, H]
-  const float* b_hh;  // [4H]
-  const float* h0;    // [B, H] or null
-  const float* c0;    // [B, H] or null
-  float* y;           // h_t
-  long y_bs, y_ts;
-  float* gates;  // [B, T, 4H] post-activation i, f, g, o (saved for backward)
-  float* cs;     // [B, T, H] cell states (saved for backward)
-  float* hT;     // [B, H] or null
-  float* cT;     // [B, H] or null
-  unsigned long long* xbuf;  // [2][B][H] granules
-  long g_bs, g_ts, cs_bs, cs_ts, h0_bs, c0_bs;  // strides (elements) of gates / cs / h0 / c0: time chunks of a
-                                                // longer sequence, time-major layouts
-  int reverse;
-};
-
-struct LstmBwdProblem {
-  const float* w_hh;
-  const float* gates;
-  const float* cs;
-  const float* c0;  // nullable
-  const float* dy;  // nullable
-  long dy_bs, dy_ts;
-  const float* dhT;  // nullable
-  const float* dcT;  // nullable
-  float* dG;         // [B, T, 4H]
-  float* dh0;        // nullable
-  float* dc0;        // nullable
-  unsigned long long* xbuf;  // [2][B][G][H] granules
-  long g_bs, g_ts, cs_bs, cs_ts, c0_bs, dG_bs, dG_ts;  // strides (elements) of gates / cs / c0 / dG
-  int reverse;
-};
-
-struct LstmFwdArgs {
-  LstmFwdProblem p[MAXP];
-  int nprob, B, T;
-  int inject;  // fault injection (mrg_lstm_debug_inject): 1 = member 0 drops its first hand-off
-  int local;   // granule stores keep the line in L2 (put_granule)
-  int* err;
-  unsigned long long* stamps;  // diagnostics only (mrg_lstm_debug_stamps); null in normal use
-};
-struct LstmBwdArgs {
-  LstmBwdProblem p[MAXP];
-  int nprob, B, T;
-  int local;
-  int* err;
-  unsigned long long* stamps;
-};
-
-// Phase stamps of block 0 / thread 0 (shader-clock s_memtime), [T][8] per launch.
-#define MRG_STAMP(ph)                                                                  \
-  do {                                                                                 \
-    if (args.stamps && blockIdx.x == 0 && threadIdx.x == 0) {                          \
-      unsigned long long _t;                                                           \
-      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");     \
-      args.stamps[(long)tt * 8 + (ph)] = _t;                                           \
-    }                                                                                  \
-  } while (0)
-
-static constexpr unsigned SPIN_LIMIT = 1u << 22;
-
-__device__ __forceinline__ unsigned long long make_granule(unsigned tag, float v) {
-  return ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(v);
-}
-
-// local != 0: the granule is published with a workgroup-scope store, which (unlike the agent-scope
-// one) keeps the line in the XCD's L2, so the group's pollers, which read with agent-scope loads
-// (L1 bypassed, L2 served), find it there instead of reading it back from the memory side
-// (MI355X_MICROARCH.md, "stores of each flavour"; measured: lstm fwd -14 %, bwd -12 %).  Only
-// for groups whose members all run on one XCD (group_on_one_xcd, checked at launch start).
-__device__ __forceinline__ void put_granule(unsigned long long* g, unsigned tag, float v, int local) {
-  if (local) __hip_atomic_store(g, make_granule(tag, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  else __hip_atomic_store(g, make_granule(tag, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Sum over aligned groups of N consecutive lanes with DPP (VALU, no LDS traffic):
-// quad_perm xor1, xor2, then row_half_mirror and row_mirror pair the quads / octets.
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-template <int N>
-__device__ __forceinline__ float group_sum(float v) {
-  static_assert(N == 1 || N == 2 || N == 4 || N == 8 || N == 16, "group_sum");
-  if (N >= 2) v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
-  if (N >= 4) v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
-  if (N >= 8) v += dpp_f<0x141>(v);  // row_half_mirror
-  if (N >= 16) v += dpp_f<0x140>(v); // row_mirror
-  return v;
-}
-
-// Poll N granules at once: all loads issued back-to-back (one round trip), then
-// only the stale ones are re-polled.  Bounded like get_granule.
-template <int N>
-__device__ __forceinline__ void get_granules(unsigned long long* base, long stride, unsigned tag, float (&out)[N],
-                                             int* err, bool& dead) {
-  unsigned long long v[N];
-#pragma unroll
-  for (int i = 0; i < N; ++i) v[i] = __hip_atomic_load(base + i * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  unsigned spins = 0;
-  while (!dead) {
-    bool ok = true;
-#pragma unroll
-    for (int i = 0; i < N; ++i) ok &= (unsigned)(v[i] >> 32) == tag;
-    if (ok) break;
-    if (++spins > SPIN_LIMIT) {
-      atomicOr(err, 1);
-      dead = true;
-      break;
-    }
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-      if ((unsigned)(v[i] >> 32) != tag)
-        v[i] = __hip_atomic_load(base + i * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-#pragma unroll
-  for (int i = 0; i < N; ++i) out[i] = __uint_as_float((unsigned)v[i]);
-}
-
-// As get_granules, for N granules at arbitrary offsets from base.
-template <int N>
-__device__ __forceinline__ void get_granules_idx(unsigned long long* base, const int (&idx)[N], unsigned tag,
-                                                 float (&out)[N], int* err, bool& dead) {
-  unsigned long long v[N];
-#pragma unroll
-  for (int i = 0; i < N; ++i) v[i] = __hip_atomic_load(base + idx[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  unsigned spins = 0;
-  while (!dead) {
-    bool ok = true;
-#pragma unroll
-    for (int i = 0; i < N; ++i) ok &= (unsigned)(v[i] >> 32) == tag;
-    if (ok) break;
-    if (++spins > SPIN_LIMIT) {
-      atomicOr(err, 1);
-      dead = true;
-      break;
-    }
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-      if ((unsigned)(v[i] >> 32) != tag)
-        v[i] = __hip_atomic_load(base + idx[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-#pragma unroll
-  for (int i = 0; i < N; ++i) out[i] = __uint_as_float((unsigned)v[i]);
-}
-
-// Local hand-offs are used only where every member of a group verified, at launch start, that it
-// runs on the same XCD as the others: each member publishes its HW_REG_XCC_ID with an agent-scope
-// store into the ring slot `slots[member]` (parity-1 slots, first written with step data at step
-// 1, after every member has finished this check) and reads the group's G ids back.  Every member
-// sees the same G ids, so the group decides alike; a group split over XCDs keeps agent-scope
-// stores.  Correctness never depends on placement; only the store flavour does.
-static constexpr unsigned XCC_TAG = 0xFFFFFFFEu;
-
-template <int G>
-__device__ __forceinline__ int group_on_one_xcd(unsigned long long* slots, int member, int* err, bool& dead,
-                                                int* flag) {
-  unsigned xcc;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-  if (threadIdx.x == 0) {
-    __hip_atomic_store(slots + member, make_granule(XCC_TAG, __uint_as_float(xcc)), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    float ids[G];
-    get_granules<G>(slots, 1, XCC_TAG, ids, err, dead);
-    int same = 1;
-#pragma unroll
-    for (int m = 0; m < G; ++m) same &= __float_as_uint(ids[m]) == xcc;
-    *flag = same;
-  }
-  __syncthreads();
-  const int same = *flag;
-  __syncthreads();
-  return same;
-}
-
-// block -> (problem, group, member); members of a group share blockIdx % 8 (one XCD)
-__device__ __forceinline__ void decompose(int G, int ngroups_per_prob, int nprob, int& prob, int& grp,
-                                          int& member) {
-  int b = blockIdx.x;
-  int total_groups = ngroups_per_prob * nprob;
-  int gid;
-  if ((total_groups & 7) == 0) {
-    int x = b & 7, idx = b >> 3;
-    member = idx % G;
-    gid = (idx / G) * 8 + x;
-  } else {
-    member = b % G;
-    gid = b / G;
-  }
-  prob = gid / ngroups_per_prob;
-  grp = gid % ngroups_per_prob;
-}
 
 // Threads per workgroup and resident workgroups per CU for a (hidden size, group size):
 //   H = 256, G = 8  : 512 threads (64 W_hh values per lane), 2 workgroups per CU
@@ -255,10 +57,9 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
   // register blocking of the recurrent GEMV: a thread owns RT gate rows x KL hidden inputs, the
   // KC lanes of a row group split the hidden dimension (DPP-reduced), so every h value read from
   // LDS feeds RT FMAs (the GEMV is LDS-issue bound otherwise)
-  // (KC = 8 lanes x 2 rows measured fastest at H = 256 and batch tiles 1-2: 3 DPP levels, 128-B LDS
-  // reads per lane; from batch tile 4 the step is bound by those LDS reads of h (each h value feeds
-  // RT FMAs), so there KC = 16 lanes x 4 rows halves them for one more DPP level)
-  constexpr int KC = (H >= 128) ? ((BS >= 4 ? 4 : 2) * NT / R) : ((H / 4 < 16) ? H / 4 : 16);
+  // (KC = 8 lanes x 2 rows measured fastest at H = 256: 3 DPP levels, 128-B LDS reads per lane; 16 x 4
+  // at batch tiles >= 4 (half the LDS reads of h, one more DPP level) measured 5-23 % slower, r03)
+  constexpr int KC = (H >= 128) ? (2 * NT / R) : ((H / 4 < 16) ? H / 4 : 16);
   constexpr int RT = R * KC / NT;
   constexpr int KL = H / KC;
   constexpr int KLP = ((KL / 4) % 2 == 0) ? KL + 4 : KL;  // odd 16-B chunk pitch: conflict-free b128
@@ -610,21 +411,44 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
   }
 }
 
-// Persistent launches need every workgroup of a group resident: pick the smallest
-// batch tile BS whose grid fits the occupancy the HW reports for that kernel, or fail.
-template <typename K>
-static bool fits(K kernel, int nt, long nblk, int cus) {
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kernel), nt, 0) !=
-      hipSuccess)
-    return false;
-  return nblk <= (long)per_cu * cus;
+int launch_fwd_mx(const LstmFwdArgs& a, int cus, hipStream_t s);   // lstm_mx.hip
+int launch_bwd_mx(const LstmBwdArgs& a, int cus, hipStream_t s);
+
+// MFMA form of the recurrence (lstm_mx.hip, H = 256, 8 members per group, batch tiles of 16):
+// 0 = never, 1 = when the VALU form would need batch tiles >= MX_MIN_BS (default), 2 = whenever it fits
+static int g_mx = [] {
+  const char* e = getenv("MRG_LSTM_MX");
+  return e ? atoi(e) : 1;
+}();
+static int g_mx_min_bs = [] {
+  const char* e = getenv("MRG_LSTM_MX_MIN_BS");
+  return e ? atoi(e) : 4;
+}();
+
+// batch tile the VALU launchers would pick (smallest fitting; 0 = none fits)
+template <typename K1, typename K2, typename K4, typename K8, typename K16>
+static int valu_bs(K1 k1, K2 k2, K4 k4, K8 k8, K16 k16, int nt, int nprob, int B, int G, int cus) {
+  for (int bs = 1; bs <= 16; bs *= 2) {
+    const long nblk = (long)nprob * ((B + bs - 1) / bs) * G;
+    const bool ok = bs == 1 ? fits(k1, nt, nblk, cus) : bs == 2 ? fits(k2, nt, nblk, cus)
+                  : bs == 4 ? fits(k4, nt, nblk, cus) : bs == 8 ? fits(k8, nt, nblk, cus) : fits(k16, nt, nblk, cus);
+    if (ok) return bs;
+  }
+  return 0;
 }
 
 template <int H, int G>
 static int launch_fwd(const LstmFwdArgs& a, int force_bs, int cus, hipStream_t s) {
   constexpr int NT = LstmNT<H, G>::value;
   const long groups1 = a.B;
+  if (H == 256 && G == 8 && g_mx && force_bs <= 0 && !a.inject && !a.stamps) {
+    const int bs = valu_bs(lstm_fwd_kernel<H, G, 1>, lstm_fwd_kernel<H, G, 2>, lstm_fwd_kernel<H, G, 4>,
+                           lstm_fwd_kernel<H, G, 8>, lstm_fwd_kernel<H, G, 16>, NT, a.nprob, a.B, G, cus);
+    if (g_mx == 2 || bs == 0 || bs >= g_mx_min_bs) {
+      const int r = launch_fwd_mx(a, cus, s);
+      if (r != 0) return r < 0 ? 1 : 0;
+    }
+  }
   for (int bs = 1; bs <= 16; bs *= 2) {
     if (force_bs > 0 && bs != force_bs) continue;
     long nblk = (long)a.nprob * ((groups1 + bs - 1) / bs) * G;
@@ -648,6 +472,14 @@ static int g_bwd_blocks_per_cu = 0;  // cap on resident workgroups per CU (mrg_l
 template <int H, int G>
 static int launch_bwd(const LstmBwdArgs& a, int force_bs, int cus, hipStream_t s) {
   constexpr int NT = LstmNT<H, G>::value;
+  if (H == 256 && G == 8 && g_mx && force_bs <= 0 && !a.stamps && g_bwd_blocks_per_cu == 0) {
+    const int bs = valu_bs(lstm_bwd_kernel<H, G, 1>, lstm_bwd_kernel<H, G, 2>, lstm_bwd_kernel<H, G, 4>,
+                           lstm_bwd_kernel<H, G, 8>, lstm_bwd_kernel<H, G, 16>, NT, a.nprob, a.B, G, cus);
+    if (g_mx == 2 || bs == 0 || bs >= g_mx_min_bs) {
+      const int r = launch_bwd_mx(a, cus, s);
+      if (r != 0) return r < 0 ? 1 : 0;
+    }
+  }
   for (int bs = 1; bs <= 16; bs *= 2) {
     if (force_bs > 0 && bs != force_bs) continue;
     long nblk = (long)a.nprob * ((a.B + bs - 1) / bs) * G;
@@ -665,15 +497,6 @@ static int launch_bwd(const LstmBwdArgs& a, int force_bs, int cus, hipStream_t s
   set_error("lstm bwd: persistent grid does not fit the GPU (nprob=%d B=%d H=%d force_bs=%d)", a.nprob, a.B, H,
             force_bs);
   return 4;
-}
-
-// members per group for a hidden size (U = 32 at H=256, U = 16 below)
-// CU count of the current device (occupancy check of the persistent grids)
-static int device_cus() {
-  int dev = 0, n = 0;
-  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    return 0;
-  return n;
 }
 
 static int g_group256 = 8;  // members per group at H = 256 (8 or 16), mrg_lstm_config
@@ -736,6 +559,16 @@ MRG_API int mrg_lstm_supported_hidden(int H) { return group_size(H) > 0; }
 MRG_API int mrg_lstm_set_blocks_per_cu(int n) {
   const int prev = g_bwd_blocks_per_cu;
   g_bwd_blocks_per_cu = n > 0 ? n : 0;
+  return prev;
+}
+
+// MFMA form of the H = 256 recurrences (lstm_mx.hip): 0 never, 1 when the VALU form needs batch tiles
+// >= min_bs (default 4), 2 whenever its grid fits.  Returns the previous mode.
+MRG_API int mrg_lstm_set_mx(int mode, int min_bs) {
+  MRG_REQUIRE(mode >= 0 && mode <= 2, "mrg_lstm_set_mx: mode must be 0..2");
+  const int prev = g_mx;
+  g_mx = mode;
+  if (min_bs > 0) g_mx_min_bs = min_bs;
   return prev;
 }
 

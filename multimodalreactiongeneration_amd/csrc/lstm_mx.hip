@@ -1,0 +1,343 @@
+// Persistent LSTM recurrence, MFMA form, for batch tiles of 16 rows (H = 256, 8 workgroups per
+// row group).  Same problem / argument blocks, hand-off protocol and results layout as lstm.hip
+// (lstm_common.h); what changes is the per-step product of each member:
+//
+//   forward   pre[16 b][128 own gate rows] = h_{t-1}[16][256] W_slice^T      (K = 256)
+//   backward  P  [16 b][256 h outputs]     = dG[16][128 own rows] W_slice    (K = 128)
+//
+// on v_mfma_f32_16x16x32_bf16 with the x6 split (each fp32 operand cut into three bf16 planes,
+// the six products with i + j <= 2 accumulated in fp32: fp32-class error, gemm_glds.hip), W_slice's
+// planes resident in VGPRs for the whole sequence (96 registers per lane) and h (or dG) split ONCE
+// per step into three bf16 planes in LDS as it arrives (a split per wave cost 8x the VALU).  The
+// VALU GEMV of lstm.hip reads every h value from LDS once per 2 FMAs, so at batch tiles >= 4 the
+// step is bound by those LDS reads; here a wave reads the planes once per 16-column output tile and
+// the product runs at the x6 MFMA rate (2.7x the fp32 VALU peak).  Used when a launch would need batch tiles >= 4 (several problems per launch: the
+// encoder stacks' wavefront, encoder_stack.py), selected in lstm.hip's launchers.
+#include "gemm_common.h"
+#include "lstm_common.h"
+
+namespace mrg {
+
+typedef float f32x4mx __attribute__((ext_vector_type(4)));
+
+static constexpr int MX_H = 256, MX_G = 8, MX_BS = 16, MX_NT = 512, MX_U = 32, MX_R = 128;
+static constexpr int MX_HPB = MX_H + 8;  // LDS row pitch of an h plane (bf16): conflict-free b128 fragment reads
+static constexpr int MX_RPB = MX_R + 8;  // LDS row pitch of a dG plane (bf16)
+static constexpr int MX_RP = MX_R + 4;   // LDS row pitch of the gate rows (floats)
+
+// 8 consecutive-k fp32 -> three bf16x8 planes (x6 split; gemm_glds.hip split8)
+__device__ __forceinline__ void mx_split8(float4 v0, float4 v1, bf16x8 (&f)[3]) {
+  unsigned a0, a1, a2, b0, b1, b2, c0, c1, c2, d0, d1, d2;
+  split2(v0.x, v0.y, a0, a1, a2);
+  split2(v0.z, v0.w, b0, b1, b2);
+  split2(v1.x, v1.y, c0, c1, c2);
+  split2(v1.z, v1.w, d0, d1, d2);
+  typedef unsigned u32x4mx __attribute__((ext_vector_type(4)));
+  const u32x4mx p0 = {a0, b0, c0, d0}, p1 = {a1, b1, c1, d1}, p2 = {a2, b2, c2, d2};
+  f[0] = __builtin_bit_cast(bf16x8, p0);
+  f[1] = __builtin_bit_cast(bf16x8, p1);
+  f[2] = __builtin_bit_cast(bf16x8, p2);
+}
+
+// acc += A B over the x6 terms, small terms first (A: lane l holds A[l & 15][8 (l >> 4) + j],
+// B: lane l holds B[8 (l >> 4) + j][l & 15]; D: lane l holds D[4 (l >> 4) + i][l & 15])
+__device__ __forceinline__ f32x4mx mx_mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x4mx acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc, 0, 0, 0);
+}
+
+// global W_hh row of a member's local gate row r (gate-major: r = q * U + u)
+__device__ __forceinline__ int mx_grow(int j, int r) { return (r / MX_U) * MX_H + j * MX_U + (r % MX_U); }
+
+__global__ __launch_bounds__(MX_NT, 1) void lstm_fwd_mx_kernel(LstmFwdArgs args) {
+  constexpr int H = MX_H, G = MX_G, BS = MX_BS, U = MX_U;
+  constexpr int WP = MX_HPB / 2;  // 32-bit words per plane row
+  __shared__ __attribute__((aligned(16))) unsigned hp[3][BS][WP];
+  __shared__ __attribute__((aligned(16))) float pre[BS][MX_RP];
+  __shared__ int xcc_flag;
+  int prob, grp, j;
+  const int ngroups = (args.B + BS - 1) / BS;
+  decompose(G, ngroups, args.nprob, prob, grp, j);
+  const LstmFwdProblem& P = args.p[prob];
+  const int B = args.B, T = args.T;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b0 = grp * BS;
+  bool dead = false;
+
+  // W planes: wave w owns local gate rows 16 w .. 16 w + 15 (the MFMA B operand, B[k][r] = W[r][k])
+  bf16x8 wf[8][3];
+  {
+    const float* wr = P.w_hh + (long)mx_grow(j, 16 * wave + (lane & 15)) * H + 8 * (lane >> 4);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const float4 v0 = *reinterpret_cast<const float4*>(wr + 32 * s);
+      const float4 v1 = *reinterpret_cast<const float4*>(wr + 32 * s + 4);
+      mx_split8(v0, v1, wf[s]);
+    }
+  }
+  // cell role: every thread owns one (row, unit) cell
+  const int cb = tid / U, cu = tid % U;
+  const int bg = b0 + cb;
+  const bool cvalid = bg < B;
+  const int hcol = j * U + cu;
+  float c = 0.0f, h = 0.0f, bh[4] = {0.f, 0.f, 0.f, 0.f}, gxv[4] = {0.f, 0.f, 0.f, 0.f};
+  if (cvalid) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bh[q] = P.b_hh[q * H + hcol];
+    if (P.c0) c = P.c0[(long)bg * P.c0_bs + hcol];
+  }
+  // h lands in LDS as three bf16 planes (x6 split), one 32-bit word = the pair (k, k + 1) of a row
+  auto put_pair = [&](int b, int k, float v0, float v1) {
+    unsigned p0, p1, p2;
+    split2(v0, v1, p0, p1, p2);
+    hp[0][b][k >> 1] = p0; hp[1][b][k >> 1] = p1; hp[2][b][k >> 1] = p2;
+  };
+  for (int e = 2 * tid; e < BS * H; e += 2 * MX_NT) {
+    const int b = e / H, k = e % H;
+    const bool ok = P.h0 && b0 + b < B;
+    put_pair(b, k, ok ? P.h0[(long)(b0 + b) * P.h0_bs + k] : 0.0f, ok ? P.h0[(long)(b0 + b) * P.h0_bs + k + 1] : 0.0f);
+  }
+  auto load_gx = [&](int t) {
+    if (cvalid) {
+      const float* g = P.gx + (long)bg * P.gx_bs + (long)t * P.gx_ts + hcol;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) gxv[q] = g[q * H];
+    }
+  };
+  load_gx(P.reverse ? T - 1 : 0);
+  __syncthreads();
+  unsigned long long* xb = P.xbuf;
+  const int local = args.local ? group_on_one_xcd<G>(xb + ((long)B + b0) * H, j, args.err, dead, &xcc_flag) : 0;
+  const int ar = lane & 15, ak = 8 * (lane >> 4);
+  const int nvalid = min(BS, B - b0) * H;
+
+  for (int tt = 0; tt < T; ++tt) {
+    const int t = P.reverse ? T - 1 - tt : tt;
+    // 1. pre[b][r] = sum_k h[b][k] W[r][k] for this wave's 16 rows
+    f32x4mx acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      bf16x8 fa[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) fa[p] = *reinterpret_cast<const bf16x8*>(&hp[p][ar][(32 * s + ak) >> 1]);
+      acc = mx_mfma6(fa, wf[s], acc);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pre[4 * (lane >> 4) + i][16 * wave + ar] = acc[i];
+    __syncthreads();
+    // 2. gates + cell, 3. publish, store, prefetch
+    const int par = tt & 1;
+    if (cvalid) {
+      const float zi = pre[cb][0 * U + cu] + gxv[0] + bh[0];
+      const float zf = pre[cb][1 * U + cu] + gxv[1] + bh[1];
+      const float zg = pre[cb][2 * U + cu] + gxv[2] + bh[2];
+      const float zo = pre[cb][3 * U + cu] + gxv[3] + bh[3];
+      const float ig = sigmoidf_(zi), fg = sigmoidf_(zf), gg = tanhf_(zg), og = sigmoidf_(zo);
+      c = fg * c + ig * gg;
+      h = og * tanhf_(c);
+      put_granule(xb + ((long)par * B + bg) * H + hcol, (unsigned)(tt + 1), h, local);
+      P.y[(long)bg * P.y_bs + (long)t * P.y_ts + hcol] = h;
+      float* gs = P.gates + (long)bg * P.g_bs + (long)t * P.g_ts + hcol;
+      gs[0] = ig; gs[H] = fg; gs[2 * H] = gg; gs[3 * H] = og;
+      P.cs[(long)bg * P.cs_bs + (long)t * P.cs_ts + hcol] = c;
+      if (tt + 1 < T) load_gx(P.reverse ? t - 1 : t + 1);
+    }
+    // 4. gather h_t of the group (BS x H granules, 8 per thread)
+    if (tt + 1 < T) {
+      constexpr int NG = BS * H / MX_NT;  // 8 granules: pairs (k, k + 1) at 4 rows
+      unsigned long long* rb = xb + ((long)par * B + b0) * H;
+      float gv[NG];
+      int idx[NG];
+#pragma unroll
+      for (int i = 0; i < NG; ++i) idx[i] = min(2 * tid + (i & 1) + 2 * MX_NT * (i >> 1), nvalid - 1);
+      get_granules_idx<NG>(rb, idx, (unsigned)(tt + 1), gv, args.err, dead);
+#pragma unroll
+      for (int m = 0; m < NG / 2; ++m) {
+        const int e = 2 * tid + 2 * MX_NT * m, b = e / H, k = e % H;
+        const bool ok = b0 + b < B;
+        put_pair(b, k, ok ? gv[2 * m] : 0.0f, ok ? gv[2 * m + 1] : 0.0f);
+      }
+    }
+    __syncthreads();
+  }
+  if (cvalid) {
+    if (P.hT) P.hT[(long)bg * H + hcol] = h;
+    if (P.cT) P.cT[(long)bg * H + hcol] = c;
+  }
+}
+
+__global__ __launch_bounds__(MX_NT, 1) void lstm_bwd_mx_kernel(LstmBwdArgs args) {
+  constexpr int H = MX_H, G = MX_G, BS = MX_BS, U = MX_U;
+  constexpr int RPB = MX_RPB;
+  __shared__ __attribute__((aligned(16))) __bf16 dgp[3][BS][RPB];   // dG as three bf16 planes
+  __shared__ float sv[2][7][BS * U];  // saved i, f, g, o, c_t, c_{t-1}, dy of the cells, by step parity
+  __shared__ int xcc_flag;
+  int prob, grp, j;
+  const int ngroups = (args.B + BS - 1) / BS;
+  decompose(G, ngroups, args.nprob, prob, grp, j);
+  const LstmBwdProblem& P = args.p[prob];
+  const int B = args.B, T = args.T;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b0 = grp * BS;
+  bool dead = false;
+
+  // W planes: wave w owns output column tiles 2 w, 2 w + 1 (B[k][n] = W[grow(k)][n], k = own gate row)
+  bf16x8 wf[2][4][3];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    const int n = 16 * (2 * wave + ct) + (lane & 15);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      float v[8];
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) v[jj] = P.w_hh[(long)mx_grow(j, 32 * s + 8 * (lane >> 4) + jj) * H + n];
+      mx_split8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), wf[ct][s]);
+    }
+  }
+  const int cb = tid / U, cu = tid % U;
+  const int bg = b0 + cb;
+  const bool cvalid = bg < B;
+  const int hcol = j * U + cu;
+  float dcn = 0.0f, dhrec = 0.0f, dgv[4];
+  if (cvalid) {
+    if (P.dcT) dcn = P.dcT[(long)bg * H + hcol];
+    if (P.dhT) dhrec = P.dhT[(long)bg * H + hcol];
+  }
+  // saved activations of processing step tt2 -> pf (the cell thread moves its own: no spare waves)
+  float pf[7];
+  auto io_load = [&](int tt2) {
+    if (!cvalid || tt2 >= T) return;
+    const int t = P.reverse ? tt2 : T - 1 - tt2;
+    const int tp = P.reverse ? t + 1 : t - 1;
+    const float* gs = P.gates + (long)bg * P.g_bs + (long)t * P.g_ts + hcol;
+    pf[0] = gs[0]; pf[1] = gs[H]; pf[2] = gs[2 * H]; pf[3] = gs[3 * H];
+    pf[4] = P.cs[(long)bg * P.cs_bs + (long)t * P.cs_ts + hcol];
+    pf[5] = (tp >= 0 && tp < T) ? P.cs[(long)bg * P.cs_bs + (long)tp * P.cs_ts + hcol]
+                                : (P.c0 ? P.c0[(long)bg * P.c0_bs + hcol] : 0.0f);
+    pf[6] = P.dy ? P.dy[(long)bg * P.dy_bs + (long)t * P.dy_ts + hcol] : 0.0f;
+  };
+  auto io_stage = [&](int tt2) {
+    if (!cvalid || tt2 >= T) return;
+#pragma unroll
+    for (int q = 0; q < 7; ++q) sv[tt2 & 1][q][tid] = pf[q];
+  };
+  io_load(0);
+  io_stage(0);
+  io_load(1);
+  __syncthreads();
+  unsigned long long* xb = P.xbuf;
+  const long xstride_b = (long)G * H;  // per batch row: [dest G][src G][U]
+  const int local = args.local ? group_on_one_xcd<G>(xb + ((long)B + b0) * xstride_b, j, args.err, dead, &xcc_flag)
+                               : 0;
+  const int ar = lane & 15, ak = 8 * (lane >> 4);
+
+  for (int tt = 0; tt < T; ++tt) {
+    const int t = P.reverse ? tt : T - 1 - tt;
+    if (cvalid) {
+      if (tt > 0) {
+        const int par = (tt - 1) & 1;
+        unsigned long long* g = xb + ((long)par * B + bg) * xstride_b + (long)j * H + cu;
+        float gv[G];
+        get_granules<G>(g, U, (unsigned)tt, gv, args.err, dead);
+        float s = 0.0f;
+#pragma unroll
+        for (int src = 0; src < G; ++src) s += gv[src];
+        dhrec = s;
+      }
+      const int sl = tt & 1;
+      const float ig = sv[sl][0][tid], fg = sv[sl][1][tid], gg = sv[sl][2][tid], og = sv[sl][3][tid];
+      const float cc = sv[sl][4][tid], cp = sv[sl][5][tid], dyv = sv[sl][6][tid];
+      const float dh = dhrec + dyv;
+      const float tc = tanhf_(cc);
+      const float dc = dh * og * (1.0f - tc * tc) + dcn;
+      dgv[0] = dc * gg * ig * (1.0f - ig);
+      dgv[1] = dc * cp * fg * (1.0f - fg);
+      dgv[2] = dc * ig * (1.0f - gg * gg);
+      dgv[3] = dh * tc * og * (1.0f - og);
+      dcn = dc * fg;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dgv[q] = 0.0f;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q += 2) {  // planes of (dG_q, dG_{q+1}): one split of the pair
+      unsigned p0, p1, p2;
+      split2(dgv[q], dgv[q + 1], p0, p1, p2);
+      const unsigned pw[3] = {p0, p1, p2};
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        dgp[p][cb][q * U + cu] = __builtin_bit_cast(__bf16, (unsigned short)(pw[p] & 0xffffu));
+        dgp[p][cb][(q + 1) * U + cu] = __builtin_bit_cast(__bf16, (unsigned short)(pw[p] >> 16));
+      }
+    }
+    __syncthreads();
+    // partial dh_{t-1}[b][n] = sum over this member's rows of dG[b][row] W[row][n], n in this wave's
+    // two column tiles; lane holds rows 4 (lane >> 4) + i, column 16 ct' + (lane & 15)
+    {
+      const int par = tt & 1;
+      f32x4mx acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        bf16x8 fa[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) fa[p] = *reinterpret_cast<const bf16x8*>(&dgp[p][ar][32 * s + ak]);
+        acc[0] = mx_mfma6(fa, wf[0][s], acc[0]);
+        acc[1] = mx_mfma6(fa, wf[1][s], acc[1]);
+      }
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        const int n = 16 * (2 * wave + ct) + ar;
+        const int dest = n / U, du = n % U;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int b = 4 * (lane >> 4) + i;
+          if (b0 + b < B)
+            put_granule(xb + ((long)par * B + b0 + b) * xstride_b + (long)dest * H + (long)j * U + du,
+                        (unsigned)(tt + 1), acc[ct][i], local);
+        }
+      }
+    }
+    if (cvalid) {  // dG of this step (fp32, from registers), stage step tt+1, prefetch tt+2
+      float* dgo = P.dG + (long)bg * P.dG_bs + (long)t * P.dG_ts + hcol;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dgo[q * H] = dgv[q];
+      io_stage(tt + 1);
+      io_load(tt + 2);
+    }
+    __syncthreads();
+  }
+  if (cvalid) {
+    if (P.dh0) {
+      const int par = (T - 1) & 1;
+      unsigned long long* g = xb + ((long)par * B + bg) * xstride_b + (long)j * H + cu;
+      float gv[G];
+      get_granules<G>(g, U, (unsigned)T, gv, args.err, dead);
+      float s = 0.0f;
+#pragma unroll
+      for (int src = 0; src < G; ++src) s += gv[src];
+      P.dh0[(long)bg * H + hcol] = s;
+    }
+    if (P.dc0) P.dc0[(long)bg * H + hcol] = dcn;
+  }
+}
+
+// 0 when the MFMA form does not apply or its grid does not fit (the caller takes lstm.hip's kernels)
+int launch_fwd_mx(const LstmFwdArgs& a, int cus, hipStream_t s) {
+  const long nblk = (long)a.nprob * ((a.B + MX_BS - 1) / MX_BS) * MX_G;
+  if (!fits(lstm_fwd_mx_kernel, MX_NT, nblk, cus)) return 0;
+  lstm_fwd_mx_kernel<<<(unsigned)nblk, MX_NT, 0, s>>>(a);
+  return check_launch("lstm_fwd_mx_kernel") ? -1 : 1;
+}
+
+int launch_bwd_mx(const LstmBwdArgs& a, int cus, hipStream_t s) {
+  const long nblk = (long)a.nprob * ((a.B + MX_BS - 1) / MX_BS) * MX_G;
+  if (!fits(lstm_bwd_mx_kernel, MX_NT, nblk, cus)) return 0;
+  lstm_bwd_mx_kernel<<<(unsigned)nblk, MX_NT, 0, s>>>(a);
+  return check_launch("lstm_bwd_mx_kernel") ? -1 : 1;
+}
+
+}  // namespace mrg

@@ -441,8 +441,11 @@ def test_encoder_stack_matches_per_layer_schedule(chunk, ratio, B, T):
     lengths = [T] * B
     lengths[-1] = T - 5
     batch = make_batch(B=B, T=T, lead=3, ratio=ratio, seed=11, lengths=lengths, device=DEV)
+    from multimodalreactiongeneration_amd import _lib
+    lib = _lib.load()
     prev = ES.CHUNK
     out = []
+    prev_mx = lib.mrg_lstm_set_mx(0, 0)   # one recurrence form on both sides: only the schedule differs
     try:
         ES.CHUNK = chunk
         for use in (False, True):
@@ -457,9 +460,40 @@ def test_encoder_stack_matches_per_layer_schedule(chunk, ratio, B, T):
                         {k: p.grad.detach().clone() for k, p in m.named_parameters()}))
     finally:
         ES.CHUNK = prev
+        lib.mrg_lstm_set_mx(prev_mx, 0)
         m.metaformer.use_encoder_stack = type(m.metaformer).use_encoder_stack
     (y0, l0, g0), (y1, l1, g1) = out
     assert rel_err(y1, y0) < 1e-5
     assert abs(l1.item() - l0.item()) <= 1e-6 * abs(l0.item())
     for k in g0:
         assert rel_err(g1[k], g0[k]) < 1e-5, k
+
+
+@pytest.mark.parametrize("stack", [True, False])
+def test_metaformer_benchmark_width_mfma_recurrence_vs_oracle(stack):
+    """Benchmark architecture at T = 300 vs the CPU oracle with every H = 256 recurrence on the MFMA
+    form (lstm_mx.hip, forced), through the encoder wavefront (encoder_stack.py) or per layer."""
+    from multimodalreactiongeneration_amd import _lib
+    from multimodalreactiongeneration_amd import configs as C
+    from multimodalreactiongeneration_amd.model import Metaformer
+    from multimodalreactiongeneration_amd.synthetic import make_batch, clone_batch
+    from oracle import mrg_oracle as O
+    lib = _lib.load()
+    mc, oc, me = C.lstmformer_config(ratio=1)
+    torch.manual_seed(0)
+    m = Metaformer(mc, oc, me)
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.to(DEV)
+    m.metaformer.use_encoder_stack = stack
+    batch = make_batch(B=4, T=300, seed=11)
+    prev = lib.mrg_lstm_set_mx(2, 0)
+    try:
+        loss = m.training_step(clone_batch(batch, DEV))["loss"]
+        loss.backward()
+        torch.cuda.synchronize()
+    finally:
+        lib.mrg_lstm_set_mx(prev, 0)
+    ref_loss, ref_y, grads, _ = O.run_train_step(O.metaformer_training_loss, sd, oc, mc, clone_batch(batch))
+    assert abs(loss.item() - ref_loss.item()) / abs(ref_loss.item()) < TOL
+    worst = max(rel_err(p.grad, grads[k]) for k, p in m.named_parameters())
+    assert worst < TOL, worst

@@ -543,6 +543,68 @@ def test_lstm_batched_problems_and_forced_tiling(bs, group):
             assert rel_err(a.grad, r.grad) < TOL
 
 
+@pytest.mark.parametrize("nprob,B,T,state", [(1, 37, 29, True), (5, 64, 40, False), (8, 64, 12, False),
+                                             (2, 16, 300, True)])
+def test_lstm_mfma_form_vs_oracle(nprob, B, T, state):
+    """The MFMA form of the H = 256 recurrence (lstm_mx.hip: batch tiles of 16 rows, x6 bf16 split on
+    v_mfma_f32_16x16x32_bf16), forced on: outputs, final states and every gradient (input, weights,
+    biases, initial state) vs the oracle, ragged last batch tiles (B = 37) and up to 8 problems."""
+    from multimodalreactiongeneration_amd import _lib
+    from multimodalreactiongeneration_amd import functional as Fn
+    from oracle import mrg_oracle as O
+    lib = _lib.load()
+    H = 256
+    g = torch.Generator().manual_seed(nprob * 1000 + B + T)
+    cases = []
+    for _ in range(nprob):
+        k = 1 / math.sqrt(H)
+        w = [(torch.rand(4 * H, H, generator=g) * 2 - 1) * k for _ in range(2)]
+        bb = [(torch.rand(4 * H, generator=g) * 2 - 1) * k for _ in range(2)]
+        x = torch.randn(B, T, H, generator=g)
+        h0 = torch.randn(B, H, generator=g) * 0.5 if state else None
+        c0 = torch.randn(B, H, generator=g) * 0.5 if state else None
+        dy = torch.randn(B, T, H, generator=g)
+        cases.append((w, bb, x, h0, c0, dy))
+    prev = lib.mrg_lstm_set_mx(2, 0)
+    try:
+        outs = []
+        if nprob == 1 or state:
+            for w, bb, x, h0, c0, dy in cases:
+                ps = [_param(t) for t in (*w, *bb)]
+                xd = x.to(DEV).requires_grad_(True)
+                hd = None if h0 is None else h0.to(DEV).requires_grad_(True)
+                cd = None if c0 is None else c0.to(DEV).requires_grad_(True)
+                y, hT, cT = Fn.lstm_layer(xd, *ps, hd, cd)
+                (y * dy.to(DEV)).sum().add(hT.sum()).add(cT.square().sum()).backward()
+                outs.append((y, hT, cT, xd, ps, hd, cd))
+        else:
+            probs = [(x.to(DEV).requires_grad_(True), *[_param(t) for t in (*w, *bb)]) for w, bb, x, _, _, _ in cases]
+            ys = Fn.lstm_layers_batched(probs)
+            sum((y * c[5].to(DEV)).sum() for y, c in zip(ys, cases)).backward()
+            outs = [(y, None, None, p[0], list(p[1:]), None, None) for y, p in zip(ys, probs)]
+        torch.cuda.synchronize()
+        Fn.check_errors()
+    finally:
+        lib.mrg_lstm_set_mx(prev, 0)
+    for (w, bb, x, h0, c0, dy), (y, hT, cT, xd, ps, hd, cd) in zip(cases, outs):
+        rs = [t.clone().requires_grad_(True) for t in (*w, *bb)]
+        xr = x.clone().requires_grad_(True)
+        hr = None if h0 is None else h0.clone().requires_grad_(True)
+        cr = None if c0 is None else c0.clone().requires_grad_(True)
+        yr, hTr, cTr = O.lstm_layer(xr, *rs, h0=hr, c0=cr)
+        loss = (yr * dy).sum()
+        if hT is not None:
+            loss = loss + hTr.sum() + cTr.square().sum()
+        loss.backward()
+        assert rel_err(y, yr) < TOL
+        if hT is not None:
+            assert rel_err(hT, hTr) < TOL and rel_err(cT, cTr) < TOL
+            assert rel_err(hd.grad, hr.grad) < TOL and rel_err(cd.grad, cr.grad) < TOL
+        assert rel_err(xd.grad, xr.grad) < TOL
+        for p, r in zip(ps, rs):
+            assert rel_err(p.grad, r.grad) < TOL
+
+
 @pytest.mark.parametrize("H,B", [(256, 64), (256, 24), (128, 16), (32, 5)])
 def test_lstm_local_handoff_is_bitwise_the_agent_one(H, B):
     """The hand-off store flavour (workgroup scope for groups verified on one XCD, agent scope

@@ -23,6 +23,8 @@ def main():
     nps = [int(v) for v in os.environ.get("NPROB", "1,2,3").split(",")]
     bss = [int(v) for v in os.environ.get("FORCE_BS", "0").split(",")]
     gs = [int(v) for v in os.environ.get("GROUPS", "8,16").split(",")]
+    if "MX" in os.environ:   # 0: VALU form only, 2: MFMA form whenever it fits (lstm_mx.hip)
+        lib.mrg_lstm_set_mx(int(os.environ["MX"]), 0)   # returns the previous mode
     for G, nprob, fbs in [(G, n, b) for G in gs for n in nps for b in bss]:
             _lib.check(lib.mrg_lstm_config(G), "cfg")
             probs = []
