@@ -116,6 +116,17 @@ int mrg_gemm_bf16_ex(int M, int N, int K, float alpha,
                      float* asum_out, float* asum_out2, float asum_beta,
                      unsigned* counters, hipStream_t stream);
 
+/* n <= 16 same-shape k-contiguous products in ONE launch: C_p = alpha A_p B_p^T + beta C_p + bias_p
+ * (+ epilogue with aux_p), A_p [M][K] rows of stride lda, B_p [N][K] rows of stride ldb (a Linear's
+ * weight); bias / aux arrays nullable; bf16 = 1 for bf16 operands.  The layer-wavefront encoder
+ * stack's per-diagonal chunk products (the input projection and FeedForward Linear of every
+ * LSTMMixerBlock in flight, mixer_block.py:237-252,63-74, lstmformer.py:165-170).  Products the
+ * LDS-DMA kernel cannot take run one by one through mrg_gemm_f32_ex.                         */
+int mrg_gemm_x6g_batched(int n, int M, int N, int K, float alpha, const float* const* A, long lda,
+                         const float* const* B, long ldb, float beta, float* const* C, long ldc,
+                         const float* const* bias, int epilogue, const float* const* aux, long ldaux,
+                         int bf16, hipStream_t stream);
+
 /* out[n] = beta*out[n] + sum_rows X(row, n); out2 (nullable) receives the same
  * sum (b_ih and b_hh share one gradient).  Bias gradients of every Linear.  */
 size_t mrg_colsum_workspace_bytes(int rows, int N);
@@ -160,6 +171,10 @@ int mrg_lstm_bwd(int nprob, int B, int T, int H,
 /* Fault injection (tests only): mode 1 makes the NEXT mrg_lstm_fwd launch drop member 0's first
  * hand-off, so the recurrence times out and reports through *err; 0 disarms.  Process-wide.  */
 int mrg_lstm_debug_inject(int mode);
+/* Tests only: keep `blocks` workgroups of `threads` lanes and `lds` bytes of LDS resident for `usec`
+ * microseconds on `stream` (a stand-in for a CU-occupying kernel, e.g. an RCCL collective, beside a
+ * persistent recurrence, which must then wait for CUs without timing out its hand-offs).        */
+int mrg_debug_busy(int blocks, int threads, int lds, double usec, hipStream_t stream);
 
 /* MFMA form of the H = 256 recurrences (batch tiles of 16 rows, x6 bf16 split on
  * v_mfma_f32_16x16x32_bf16, fp32-class): mode 0 never, 1 (default) when the VALU form would need
@@ -317,6 +332,18 @@ int mrg_residual_layernorm_fwd_map(int rows, int E, const float* a, const float*
 int mrg_residual_layernorm_bwd_map(int rows, int E, const float* dy, long dy_lo, long dy_hi, int dy_div,
                                    const float* a, const float* b, const float* gamma, const float* mean,
                                    const float* rstd, float* dx, float* workspace, hipStream_t stream);
+/* n <= 16 same-shape row-mapped residual LayerNorms (ResidualConnection, residual_connection.py:20-37)
+ * in one launch, each with its own tensors, parameters and map: the encoder stack's per-diagonal
+ * chunks.  Backward partials go to ws[p] (reduce with mrg_residual_layernorm_param_reduce).      */
+int mrg_residual_layernorm_fwd_batched(int n, int rows, int E, const float* const* a, const float* const* b,
+                                       const float* const* gamma, const float* const* beta, float eps,
+                                       float* const* y, const long* y_lo, const long* y_hi, const int* y_div,
+                                       float* const* mean, float* const* rstd, hipStream_t stream);
+int mrg_residual_layernorm_bwd_batched(int n, int rows, int E, const float* const* dy, const long* dy_lo,
+                                       const long* dy_hi, const int* dy_div, const float* const* a,
+                                       const float* const* b, const float* const* gamma,
+                                       const float* const* mean, const float* const* rstd, float* const* dx,
+                                       float* const* ws, hipStream_t stream);
 
 /* ---------------------------------------------------------------- loss
  * Masked regression loss of training_step (lstmformer.py:372-380,

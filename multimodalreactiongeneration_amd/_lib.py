@@ -57,6 +57,8 @@ SIGNATURES = {
                                  P, c_int, c_long, c_long, c_int,
                                  c_float, P, c_long, P, c_int, P, c_long, P, c_int,
                                  P, P, c_float, P, P]),
+    "mrg_gemm_x6g_batched": (c_int, [c_int, c_int, c_int, c_int, c_float, PP, c_long, PP, c_long, c_float, PP,
+                                     c_long, PP, c_int, PP, c_long, c_int, P]),
     "mrg_colsum_workspace_bytes": (c_size, [c_int, c_int]),
     "mrg_colsum_f32": (c_int, [c_int, c_int, P, c_long, c_long, c_int, c_float, P, P, P, P]),
     "mrg_lstm_supported_hidden": (c_int, [c_int]),
@@ -96,6 +98,11 @@ SIGNATURES = {
     "mrg_residual_layernorm_fwd_map": (c_int, [c_int, c_int, P, P, P, P, c_float, P, c_long, c_long, c_int,
                                                P, P, P]),
     "mrg_residual_layernorm_bwd_map": (c_int, [c_int, c_int, P, c_long, c_long, c_int, P, P, P, P, P, P, P, P]),
+    "mrg_residual_layernorm_fwd_batched": (c_int, [c_int, c_int, c_int, PP, PP, PP, PP, c_float, PP, PL, PL, PI,
+                                                   PP, PP, P]),
+    "mrg_residual_layernorm_bwd_batched": (c_int, [c_int, c_int, c_int, PP, PL, PL, PI, PP, PP, PP, PP, PP, PP,
+                                                   PP, P]),
+    "mrg_debug_busy": (c_int, [c_int, c_int, c_int, ctypes.c_double, P]),
     "mrg_loss_workspace_bytes": (c_size, [c_int, c_int, c_int]),
     "mrg_masked_loss_fwd": (c_int, [c_int, c_int, c_int, P, c_long, P, c_int, c_float, c_float,
                                     c_int, c_int, c_float, P, P, P]),

@@ -24,3 +24,33 @@ MRG_API int mrg_device_cu_count(int device, int* out) {
   *out = p.multiProcessorCount;
   return 0;
 }
+
+// Tests only: a kernel that keeps `blocks` workgroups of `threads` lanes (and `lds` bytes of LDS
+// each) resident for `usec` microseconds of wall clock, standing in for a CU-occupying kernel on
+// another stream (an RCCL collective beside the backward): a persistent recurrence launched
+// behind it must wait for CUs, not time out its hand-offs.
+namespace mrg {
+__global__ void busy_kernel(unsigned long long ticks, float* sink) {
+  extern __shared__ float scratch[];
+  const unsigned long long t0 = wall_clock64();
+  float acc = 0.0f;
+  while (wall_clock64() - t0 < ticks) acc += 1.0f;
+  scratch[threadIdx.x] = acc;
+  __syncthreads();
+  if (sink && threadIdx.x == 0 && scratch[0] < 0.0f) sink[blockIdx.x] = scratch[0];   // never taken
+}
+}  // namespace mrg
+
+MRG_API int mrg_debug_busy(int blocks, int threads, int lds, double usec, hipStream_t stream) {
+  MRG_REQUIRE(blocks > 0 && threads > 0 && threads <= 1024 && lds >= threads * 4 && lds <= 160 * 1024,
+              "mrg_debug_busy: bad shape");
+  MRG_REQUIRE(usec >= 0.0 && usec <= 2e6, "mrg_debug_busy: usec out of range");
+  int dev = 0, khz = 0;
+  MRG_HIP(hipGetDevice(&dev));
+  MRG_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+  const unsigned long long ticks = (unsigned long long)(usec * 1e-3 * (khz > 0 ? khz : 100000));
+  if (lds > 64 * 1024) MRG_HIP(hipFuncSetAttribute((const void*)mrg::busy_kernel,
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  mrg::busy_kernel<<<blocks, threads, lds, stream>>>(ticks, nullptr);
+  return mrg::check_launch("busy_kernel");
+}

@@ -1176,6 +1176,57 @@ MRG_API int mrg_gemm_bf16_ex(int M, int N, int K, float alpha,
                  stream);
 }
 
+// n same-shape k-contiguous products in ONE launch (the encoder stack's per-diagonal chunk products,
+// encoder_stack.py): C_p = alpha A_p B_p^T + beta C_p + bias_p (epilogue with aux_p), A_p [M][K] rows
+// of stride lda, B_p [N][K] rows of stride ldb, p < n <= 16; bias / aux arrays nullable.  The
+// LDS-DMA x6 kernel walks the n x tiles grid (bf16 = 1: one bf16 plane, the "bf16" precision);
+// shapes or modes outside it run the products one by one through mrg_gemm_f32_ex's dispatch.
+MRG_API int mrg_gemm_x6g_batched(int n, int M, int N, int K, float alpha, const float* const* A, long lda,
+                                 const float* const* B, long ldb, float beta, float* const* C, long ldc,
+                                 const float* const* bias, int epilogue, const float* const* aux, long ldaux,
+                                 int bf16, hipStream_t stream) {
+  MRG_REQUIRE(n >= 0 && n <= MRG_GB_MAX, "mrg_gemm_x6g_batched: n %d out of range", n);
+  MRG_REQUIRE(epilogue >= 0 && epilogue <= 3 && (epilogue < 2 || aux), "mrg_gemm_x6g_batched: bad epilogue");
+  if (n == 0 || M == 0 || N == 0) return 0;
+  const int mode = bf16 ? 2 : g_gemm_mode;
+  uintptr_t al = 0;
+  for (int p = 0; p < n; ++p)
+    al |= (uintptr_t)A[p] | (uintptr_t)B[p] | (uintptr_t)C[p] | (uintptr_t)(bias ? bias[p] : nullptr) |
+          (uintptr_t)(aux ? aux[p] : nullptr);
+  const bool ok = mode != 0 && g_glds > 0 && K > 0 && (K % 32) == 0 && (al & 15) == 0 && (lda & 3) == 0 &&
+                  (ldb & 3) == 0 && (ldc & 3) == 0 && (!aux || (ldaux & 3) == 0) && M >= 2048 && N >= 256;
+  if (!ok) {
+    for (int p = 0; p < n; ++p)
+      if (int e = gemm_ex(mode, M, N, K, alpha, A[p], 0, lda, 0, 0, B[p], 1, ldb, 0, 0, beta, C[p], ldc,
+                          bias ? bias[p] : nullptr, epilogue, aux ? aux[p] : nullptr, ldaux, nullptr, 1, nullptr,
+                          nullptr, 0.0f, nullptr, stream))
+        return e;
+    return 0;
+  }
+  GemmArgs a;
+  memset(&a, 0, sizeof(a));
+  a.M = M; a.N = N; a.K = K; a.alpha = alpha; a.beta = beta;
+  a.A = A[0]; a.amap = RowMap{lda, 0, 0}; a.transA = 0;
+  a.B = B[0]; a.bmap = RowMap{ldb, 0, 0}; a.transB = 1;
+  a.C = C[0]; a.ldc = ldc; a.bias = bias ? bias[0] : nullptr; a.epi = epilogue;
+  a.aux = aux ? aux[0] : nullptr; a.ldaux = ldaux;
+  a.kchunk = K; a.nsplit = 1; a.vec = 1;
+  GemmBatch gb;
+  memset(&gb, 0, sizeof(gb));
+  gb.n = n;
+  for (int p = 0; p < n; ++p) {
+    gb.A[p] = A[p]; gb.B[p] = B[p]; gb.C[p] = C[p];
+    gb.bias[p] = bias ? bias[p] : nullptr;
+    gb.aux[p] = aux ? aux[p] : nullptr;
+  }
+  int bm = 64, bn = 128;  // gemm_ex's shape rule for this kernel
+  if (N >= 1024) bm = 128;
+  else if (N == 256 && K <= 256) bn = 64;
+  if (g_glds_bn == 64) bn = 64;
+  launch_x6g(a, g_glds, bm, bn, stream, mode == 2 ? 1 : 3, &gb);
+  return check_launch("gemm_x6g_kernel (batched)");
+}
+
 MRG_API int mrg_gemm_f32(int M, int N, int K, float alpha,
                          const float* A, int transA, long lda, long lda_hi, int a_rdiv,
                          const float* B, int transB, long ldb, long ldb_hi, int b_rdiv,

@@ -124,10 +124,22 @@ __device__ __forceinline__ void split4(float v0, float v1, float v2, float v3, u
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
+// Same-shape products batched into one launch (mrg_gemm_x6g_batched): per problem the operand,
+// output, bias and aux pointers; everything else (shape, strides, epilogue) is GemmArgs'.
+static constexpr int MRG_GB_MAX = 16;
+struct GemmBatch {
+  int n;  // 0 = not batched
+  const float* A[MRG_GB_MAX];
+  const float* B[MRG_GB_MAX];
+  float* C[MRG_GB_MAX];
+  const float* bias[MRG_GB_MAX];
+  const float* aux[MRG_GB_MAX];
+};
+
 // LDS-DMA pipelined x6 kernel for k-contiguous products (gemm_glds.hip): ring depth ns, tile
-// bm x bn (64 | 128 each); grid = one workgroup per output tile; planes 3 = x6 split (fp32-class),
-// 1 = bf16 operands (precision "bf16")
-void launch_x6g(GemmArgs a, int ns, int bm, int bn, hipStream_t s, int planes = 3);
+// bm x bn (64 | 128 each); grid = one workgroup per output tile (x problems when batched);
+// planes 3 = x6 split (fp32-class), 1 = bf16 operands (precision "bf16")
+void launch_x6g(GemmArgs a, int ns, int bm, int bn, hipStream_t s, int planes = 3, const GemmBatch* gb = nullptr);
 // its weight-gradient form (transA = 1, transB = 0, K % 32 == 0, M and N multiples of 4): split-K
 // slabs in a.ws (splits > 1) and the fused row sums of A in a.asum, as gemm_x6_kernel leaves them
 void launch_x6g_wgrad(GemmArgs a, int splits, int bm, int bn, hipStream_t s, int planes = 3);

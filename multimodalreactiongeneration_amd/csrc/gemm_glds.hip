@@ -92,7 +92,7 @@ __device__ __forceinline__ void vm_wait() {
 // B plane rows are 64 B per k-tile: one DMA wave-instruction fills 16 rows (lane L -> row 16g + L/4,
 // 16-B slot L%4 holding 8-k chunk (L%4) ^ ((row >> 2) & 3)).
 template <int BM, int BN, int NS, int PB, int NP = 3>
-__global__ __launch_bounds__(NT, 1) void gemm_x6g_kernel(GemmArgs a, long bplane) {
+__global__ __launch_bounds__(NT, 1) void gemm_x6g_kernel(GemmArgs a_in, long bplane, GemmBatch gb) {
   static_assert(NP == 3 || (NP == 1 && PB == 0), "gemm_x6g: one-plane form has no pre-split B");
   constexpr int TM = BM / 64, TN = BN / 64;
   constexpr int SA = BM * 128;                                   // A: [BM][32] fp32
@@ -109,7 +109,15 @@ __global__ __launch_bounds__(NT, 1) void gemm_x6g_kernel(GemmArgs a, long bplane
   // XCD-aware bijective remap: the blocks that share an XCD (b % 8) take consecutive tiles, so the
   // column tiles of one row block (the same A rows) meet in one L2
   const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  // batched form (gb.n problems of one shape, mrg_gemm_x6g_batched): the grid covers n x tiles_mn
+  // tiles, problem-major, so an XCD's consecutive tiles stay within one problem
+  GemmArgs a = a_in;
+  if (gb.n > 0) {
+    const int p = t / a.tiles_mn;
+    t -= p * a.tiles_mn;
+    a.A = gb.A[p]; a.B = gb.B[p]; a.C = gb.C[p]; a.bias = gb.bias[p]; a.aux = gb.aux[p];
+  }
   const int m0 = (t / a.tiles_n) * BM, n0 = (t % a.tiles_n) * BN;
   const int nk = a.K / 32;
 
@@ -258,39 +266,42 @@ __global__ __launch_bounds__(NT, 1) void gemm_x6g_kernel(GemmArgs a, long bplane
 }
 
 template <int BM, int BN, int PB, int NP>
-static void launch_tiles(GemmArgs a, int ns, long bplane, hipStream_t s) {
+static void launch_tiles(GemmArgs a, int ns, long bplane, hipStream_t s, const GemmBatch& gb) {
   a.tiles_n = (a.N + BN - 1) / BN;
   a.tiles_mn = a.tiles_n * ((a.M + BM - 1) / BM);
   a.ntiles = a.tiles_mn;
   a.nsplit = 1;
   a.ws = nullptr;
-  const unsigned grid = (unsigned)a.tiles_mn;
+  const unsigned grid = (unsigned)a.tiles_mn * (unsigned)(gb.n > 0 ? gb.n : 1);
   if constexpr (NP == 1) {  // one-plane form: ring depth 2 only
-    gemm_x6g_kernel<BM, BN, 2, 0, 1><<<grid, NT, 0, s>>>(a, bplane);
+    gemm_x6g_kernel<BM, BN, 2, 0, 1><<<grid, NT, 0, s>>>(a, bplane, gb);
     return;
   }
   switch (ns) {
-    case 2: gemm_x6g_kernel<BM, BN, 2, PB><<<grid, NT, 0, s>>>(a, bplane); break;
-    case 4: gemm_x6g_kernel<BM, BN, 4, PB><<<grid, NT, 0, s>>>(a, bplane); break;
-    default: gemm_x6g_kernel<BM, BN, 3, PB><<<grid, NT, 0, s>>>(a, bplane); break;
+    case 2: gemm_x6g_kernel<BM, BN, 2, PB><<<grid, NT, 0, s>>>(a, bplane, gb); break;
+    case 4: gemm_x6g_kernel<BM, BN, 4, PB><<<grid, NT, 0, s>>>(a, bplane, gb); break;
+    default: gemm_x6g_kernel<BM, BN, 3, PB><<<grid, NT, 0, s>>>(a, bplane, gb); break;
   }
 }
 
 template <int PB, int NP = 3>
-static void launch_shape(GemmArgs a, int ns, int bm, int bn, long bplane, hipStream_t s) {
+static void launch_shape(GemmArgs a, int ns, int bm, int bn, long bplane, hipStream_t s, const GemmBatch& gb) {
   if (bm == 64) {
-    if (bn == 64) launch_tiles<64, 64, PB, NP>(a, ns, bplane, s);
-    else launch_tiles<64, 128, PB, NP>(a, ns, bplane, s);
+    if (bn == 64) launch_tiles<64, 64, PB, NP>(a, ns, bplane, s, gb);
+    else launch_tiles<64, 128, PB, NP>(a, ns, bplane, s, gb);
   } else if (bn == 64) {
-    launch_tiles<128, 64, PB, NP>(a, ns, bplane, s);
+    launch_tiles<128, 64, PB, NP>(a, ns, bplane, s, gb);
   } else {
-    launch_tiles<128, 128, PB, NP>(a, ns, bplane, s);
+    launch_tiles<128, 128, PB, NP>(a, ns, bplane, s, gb);
   }
 }
 
-void launch_x6g(GemmArgs a, int ns, int bm, int bn, hipStream_t s, int planes) {
-  if (planes == 1) launch_shape<0, 1>(a, 2, bm, bn, 0, s);
-  else launch_shape<0>(a, ns, bm, bn, 0, s);
+void launch_x6g(GemmArgs a, int ns, int bm, int bn, hipStream_t s, int planes, const GemmBatch* gb) {
+  GemmBatch none;
+  none.n = 0;
+  const GemmBatch& b = gb ? *gb : none;
+  if (planes == 1) launch_shape<0, 1>(a, 2, bm, bn, 0, s, b);
+  else launch_shape<0>(a, ns, bm, bn, 0, s, b);
 }
 
 
@@ -612,6 +623,8 @@ MRG_API int mrg_gemm_x6_planes(int M, int N, int K, float alpha, const float* A,
   int bm = 64, bn = 128;  // the fp32-operand kernel's shape rule (gemm.hip)
   if (N >= 1024) bm = 128;
   else if (N <= 256 && K <= 256) bn = 64;
-  launch_shape<1>(a, 2, bm, bn, bplane, stream);
+  GemmBatch none;
+  none.n = 0;
+  launch_shape<1>(a, 2, bm, bn, bplane, stream, none);
   return check_launch("gemm_x6g_kernel");
 }

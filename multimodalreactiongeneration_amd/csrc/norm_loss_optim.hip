@@ -112,11 +112,11 @@ __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
 template <int EPV>  // float4 chunks per lane: E <= 256 * EPV
-__global__ __launch_bounds__(256) void resln_fwd_v4_kernel(const float* __restrict__ a, const float* __restrict__ b,
-                                                           const float* __restrict__ gamma,
-                                                           const float* __restrict__ beta, float* __restrict__ y,
-                                                           float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                           int rows, float eps, int E, RowMap ymap) {
+__device__ __forceinline__ void resln_fwd_v4_rows(const float* __restrict__ a, const float* __restrict__ b,
+                                                  const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                  float* __restrict__ y, float* __restrict__ mean_out,
+                                                  float* __restrict__ rstd_out, int rows, float eps, int E,
+                                                  RowMap ymap) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
@@ -162,13 +162,44 @@ __global__ __launch_bounds__(256) void resln_fwd_v4_kernel(const float* __restri
 }
 
 template <int EPV>
-__global__ __launch_bounds__(256) void resln_bwd_v4_kernel(const float* __restrict__ dy, const float* __restrict__ a,
-                                                           const float* __restrict__ b,
+__global__ __launch_bounds__(256) void resln_fwd_v4_kernel(const float* __restrict__ a, const float* __restrict__ b,
                                                            const float* __restrict__ gamma,
-                                                           const float* __restrict__ mean_in,
-                                                           const float* __restrict__ rstd_in, float* __restrict__ dx,
-                                                           float* __restrict__ part, int rows, int rows_per_block,
-                                                           int E, RowMap dmap) {
+                                                           const float* __restrict__ beta, float* __restrict__ y,
+                                                           float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                           int rows, float eps, int E, RowMap ymap) {
+  resln_fwd_v4_rows<EPV>(a, b, gamma, beta, y, mean_out, rstd_out, rows, eps, E, ymap);
+}
+
+// Same-shape residual LayerNorms batched into one launch (blockIdx.y = problem): the encoder
+// stack's per-diagonal chunks (encoder_stack.py), each with its own tensors, parameters and map.
+static constexpr int MRG_LN_MAX = 16;
+struct LnBatch {
+  const float* a[MRG_LN_MAX];
+  const float* b[MRG_LN_MAX];
+  const float* gamma[MRG_LN_MAX];
+  const float* beta[MRG_LN_MAX];  // backward: unused
+  const float* dy[MRG_LN_MAX];    // backward only
+  float* y[MRG_LN_MAX];           // forward: output; backward: dx
+  float* mean[MRG_LN_MAX];
+  float* rstd[MRG_LN_MAX];
+  float* part[MRG_LN_MAX];        // backward: dgamma / dbeta partials
+  RowMap map[MRG_LN_MAX];         // forward: output rows; backward: incoming-gradient rows
+};
+
+template <int EPV>
+__global__ __launch_bounds__(256) void resln_fwd_v4_batched_kernel(LnBatch lb, int rows, float eps, int E) {
+  const int p = blockIdx.y;
+  resln_fwd_v4_rows<EPV>(lb.a[p], lb.b[p], lb.gamma[p], lb.beta[p], lb.y[p], lb.mean[p], lb.rstd[p], rows, eps, E,
+                         lb.map[p]);
+}
+
+template <int EPV>
+__device__ __forceinline__ void resln_bwd_v4_rows(const float* __restrict__ dy, const float* __restrict__ a,
+                                                  const float* __restrict__ b, const float* __restrict__ gamma,
+                                                  const float* __restrict__ mean_in,
+                                                  const float* __restrict__ rstd_in, float* __restrict__ dx,
+                                                  float* __restrict__ part, int rows, int rows_per_block, int E,
+                                                  RowMap dmap) {
   constexpr int EMAX = 256 * EPV;
   __shared__ __attribute__((aligned(16))) float red[4][2][EMAX];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -243,6 +274,24 @@ __global__ __launch_bounds__(256) void resln_bwd_v4_kernel(const float* __restri
     const int k = c / E, e = c % E;
     part[((long)blockIdx.x * 2 + k) * E + e] = (red[0][k][e] + red[1][k][e]) + (red[2][k][e] + red[3][k][e]);
   }
+}
+
+template <int EPV>
+__global__ __launch_bounds__(256) void resln_bwd_v4_kernel(const float* __restrict__ dy, const float* __restrict__ a,
+                                                           const float* __restrict__ b,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ mean_in,
+                                                           const float* __restrict__ rstd_in, float* __restrict__ dx,
+                                                           float* __restrict__ part, int rows, int rows_per_block,
+                                                           int E, RowMap dmap) {
+  resln_bwd_v4_rows<EPV>(dy, a, b, gamma, mean_in, rstd_in, dx, part, rows, rows_per_block, E, dmap);
+}
+
+template <int EPV>
+__global__ __launch_bounds__(256) void resln_bwd_v4_batched_kernel(LnBatch lb, int rows, int rows_per_block, int E) {
+  const int p = blockIdx.y;
+  resln_bwd_v4_rows<EPV>(lb.dy[p], lb.a[p], lb.b[p], lb.gamma[p], lb.mean[p], lb.rstd[p], lb.y[p], lb.part[p], rows,
+                         rows_per_block, E, lb.map[p]);
 }
 
 // dgamma / dbeta: sum the per-block partials part[nblk][2][E]; one lane per column,
@@ -565,6 +614,67 @@ MRG_API int mrg_residual_layernorm_bwd_map(int rows, int E, const float* dy, lon
   else if (epv == 2) resln_bwd_v4_kernel<2><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, RESLN_RPB, E, m);
   else resln_bwd_v4_kernel<4><<<nblk, 256, 0, stream>>>(dy, a, b, gamma, mean, rstd, dx, workspace, rows, RESLN_RPB, E, m);
   return check_launch("resln_bwd_v4_kernel");
+}
+
+// n same-shape row-mapped residual LayerNorms in one launch (E % 4 == 0, E <= 1024, 16-B aligned
+// rows): problem p reads a[p] + b[p] (rows of E) and writes y[p] through its own map (y_lo, y_hi,
+// y_div), mean[p], rstd[p].
+MRG_API int mrg_residual_layernorm_fwd_batched(int n, int rows, int E, const float* const* a, const float* const* b,
+                                               const float* const* gamma, const float* const* beta, float eps,
+                                               float* const* y, const long* y_lo, const long* y_hi,
+                                               const int* y_div, float* const* mean, float* const* rstd,
+                                               hipStream_t stream) {
+  MRG_REQUIRE(n >= 0 && n <= MRG_LN_MAX, "mrg_residual_layernorm_fwd_batched: n %d out of range", n);
+  if (n == 0 || rows == 0) return 0;
+  MRG_REQUIRE(E % 4 == 0 && E <= 1024, "mrg_residual_layernorm_fwd_batched: E %d", E);
+  LnBatch lb;
+  memset(&lb, 0, sizeof(lb));
+  for (int p = 0; p < n; ++p) {
+    MRG_REQUIRE(y_lo[p] % 4 == 0 && y_hi[p] % 4 == 0 &&
+                    (((uintptr_t)a[p] | (uintptr_t)b[p] | (uintptr_t)y[p] | (uintptr_t)gamma[p] |
+                      (uintptr_t)beta[p]) & 15) == 0,
+                "mrg_residual_layernorm_fwd_batched: 16-byte aligned rows required (problem %d)", p);
+    lb.a[p] = a[p]; lb.b[p] = b[p]; lb.gamma[p] = gamma[p]; lb.beta[p] = beta[p];
+    lb.y[p] = y[p]; lb.mean[p] = mean[p]; lb.rstd[p] = rstd[p];
+    lb.map[p] = RowMap{y_lo[p], y_hi[p], y_div[p]};
+  }
+  dim3 grid((rows + 3) / 4, n);
+  const int epv = (E + 255) / 256;
+  if (epv == 1) resln_fwd_v4_batched_kernel<1><<<grid, 256, 0, stream>>>(lb, rows, eps, E);
+  else if (epv == 2) resln_fwd_v4_batched_kernel<2><<<grid, 256, 0, stream>>>(lb, rows, eps, E);
+  else resln_fwd_v4_batched_kernel<4><<<grid, 256, 0, stream>>>(lb, rows, eps, E);
+  return check_launch("resln_fwd_v4_batched_kernel");
+}
+
+// Backward of n same-shape residual LayerNorms in one launch: problem p's incoming gradient rows
+// through its map (dy_lo, dy_hi, dy_div), dx[p] rows of E, per-block dgamma / dbeta partials into
+// ws[p] (mrg_residual_layernorm_param_reduce reduces them).
+MRG_API int mrg_residual_layernorm_bwd_batched(int n, int rows, int E, const float* const* dy, const long* dy_lo,
+                                               const long* dy_hi, const int* dy_div, const float* const* a,
+                                               const float* const* b, const float* const* gamma,
+                                               const float* const* mean, const float* const* rstd,
+                                               float* const* dx, float* const* ws, hipStream_t stream) {
+  MRG_REQUIRE(n >= 0 && n <= MRG_LN_MAX, "mrg_residual_layernorm_bwd_batched: n %d out of range", n);
+  if (n == 0 || rows == 0) return 0;
+  MRG_REQUIRE(E % 4 == 0 && E <= 1024, "mrg_residual_layernorm_bwd_batched: E %d", E);
+  LnBatch lb;
+  memset(&lb, 0, sizeof(lb));
+  for (int p = 0; p < n; ++p) {
+    MRG_REQUIRE(dy_lo[p] % 4 == 0 && dy_hi[p] % 4 == 0 &&
+                    (((uintptr_t)dy[p] | (uintptr_t)a[p] | (uintptr_t)b[p] | (uintptr_t)dx[p] |
+                      (uintptr_t)gamma[p]) & 15) == 0,
+                "mrg_residual_layernorm_bwd_batched: 16-byte aligned rows required (problem %d)", p);
+    lb.dy[p] = dy[p]; lb.a[p] = a[p]; lb.b[p] = b[p]; lb.gamma[p] = gamma[p];
+    lb.mean[p] = const_cast<float*>(mean[p]); lb.rstd[p] = const_cast<float*>(rstd[p]);
+    lb.y[p] = dx[p]; lb.part[p] = ws[p];
+    lb.map[p] = RowMap{dy_lo[p], dy_hi[p], dy_div[p]};
+  }
+  dim3 grid((rows + RESLN_RPB - 1) / RESLN_RPB, n);
+  const int epv = (E + 255) / 256;
+  if (epv == 1) resln_bwd_v4_batched_kernel<1><<<grid, 256, 0, stream>>>(lb, rows, RESLN_RPB, E);
+  else if (epv == 2) resln_bwd_v4_batched_kernel<2><<<grid, 256, 0, stream>>>(lb, rows, RESLN_RPB, E);
+  else resln_bwd_v4_batched_kernel<4><<<grid, 256, 0, stream>>>(lb, rows, RESLN_RPB, E);
+  return check_launch("resln_bwd_v4_batched_kernel");
 }
 
 MRG_API int mrg_residual_layernorm_param_reduce(int rows, int E, const float* workspace, float* dgamma,

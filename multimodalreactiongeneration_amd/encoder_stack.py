@@ -43,7 +43,24 @@ from .functional import _ptr, _stream, gemm, _fwd_gemm, _dx_gemm, _wgrad, _wt_no
 
 # time steps per chunk (the diagonal width); MRG_STACK_CHUNK overrides
 CHUNK = int(os.environ.get("MRG_STACK_CHUNK", "60"))
-MAXP = int(os.environ.get("MRG_STACK_MAXP", "12"))   # problems per recurrence launch (lstm.hip: <= 12)
+# problems per recurrence launch (lstm.hip: <= 12); 0 = as many as the MFMA form's grid keeps resident
+# (8 workgroups of 16 rows per problem, one per CU: 8 problems at B = 64 on 256 CUs; a wider launch
+# falls back to the VALU form at batch tiles of 16, measured 3x slower per step)
+MAXP = int(os.environ.get("MRG_STACK_MAXP", "0"))
+
+
+def _maxp(B, dev):
+    if MAXP > 0:
+        return MAXP
+    per = 8 * ((B + 15) // 16)
+    return max(1, min(12, _lib.cu_count(dev.index or 0) // per))
+
+
+def _split(v, cap):
+    """v into ceil(len / cap) launches of balanced size."""
+    k = (len(v) + cap - 1) // cap
+    q = (len(v) + k - 1) // k
+    return [v[s:s + q] for s in range(0, len(v), q)]
 VP, CL, CI = ctypes.c_void_p, ctypes.c_long, ctypes.c_int
 _PER_LAYER = 10   # w_ih, w_hh, b_ih, b_hh, ln1 gamma, ln1 beta, w_ff, b_ff, ln2 gamma, ln2 beta
 
@@ -115,6 +132,74 @@ def _launch_bwd(lib, items, B, Tc, H, dev):
     _lib.check(rc, "lstm bwd (encoder stack)")
 
 
+_BMAX = 16   # problems per batched GEMM / LayerNorm launch (mrg_gemm_x6g_batched, mrg_residual_layernorm_*_batched)
+VPP = ctypes.POINTER(ctypes.c_void_p)
+
+
+def _arr(ct, v):
+    return (ct * len(v))(*v)
+
+
+def _bgemm(lib, M, N, K, items, lda, ldc, *, epi=0, ldaux=0, transposed=False, dev=None):
+    """Same-shape products C_p = A_p w_p^T + bias_p (+ aux_p) in one launch; items = [(A ptr, w, C ptr,
+    bias ptr | None, aux ptr | None)].  transposed: the products are dY w (input gradients), run as
+    dY (w^T)^T through the [in][out] copies (functional._wt); per product when a copy is missing."""
+    if not items:
+        return
+    bs = []
+    for a_p, w, c_p, b_p, x_p in items:
+        if transposed:
+            wt = Fn._wt(w) if M >= Fn._WT_MIN_ROWS else None
+            if wt is None:   # no [in][out] copy: the per-product path
+                for a_p2, w2, c_p2, b_p2, x_p2 in items:
+                    _dx_gemm(M, N, K, a_p2, lda, w2, c_p2, ldc, bias=b_p2, epi=epi, aux=x_p2, ldaux=ldaux, device=dev)
+                return
+            bs.append(_ptr(wt))
+        else:
+            bs.append(_ptr(w))
+    n = len(items)
+    with Fn._probe("gemm", 2.0 * M * N * K * n):
+        rc = lib.mrg_gemm_x6g_batched(
+            n, M, N, K, 1.0, _arr(VP, [it[0] for it in items]), lda, _arr(VP, bs), K, 0.0,
+            _arr(VP, [it[2] for it in items]), ldc,
+            None if all(it[3] is None for it in items) else _arr(VP, [it[3] for it in items]), epi,
+            None if all(it[4] is None for it in items) else _arr(VP, [it[4] for it in items]), ldaux,
+            1 if Fn._ARITH[0] == "bf16" else 0, _stream())
+    _lib.check(rc, "batched gemm (encoder stack)")
+
+
+def _bln_fwd(lib, rows, H, eps, items):
+    """items = [(a, b, gamma, beta, y, (lo, hi, div), mean, rstd)] pointers: one batched launch."""
+    if not items:
+        return
+    col = list(zip(*items))
+    rc = lib.mrg_residual_layernorm_fwd_batched(
+        len(items), rows, H, _arr(VP, col[0]), _arr(VP, col[1]), _arr(VP, col[2]), _arr(VP, col[3]), eps,
+        _arr(VP, col[4]), _arr(CL, [m[0] for m in col[5]]), _arr(CL, [m[1] for m in col[5]]),
+        _arr(CI, [m[2] for m in col[5]]), _arr(VP, col[6]), _arr(VP, col[7]), _stream())
+    _lib.check(rc, "batched layernorm fwd (encoder stack)")
+
+
+def _bln_bwd(lib, rows, H, items):
+    """items = [(dy, (lo, hi, div), a, b, gamma, mean, rstd, dx, ws)] pointers: one batched launch."""
+    if not items:
+        return
+    col = list(zip(*items))
+    rc = lib.mrg_residual_layernorm_bwd_batched(
+        len(items), rows, H, _arr(VP, col[0]), _arr(CL, [m[0] for m in col[1]]), _arr(CL, [m[1] for m in col[1]]),
+        _arr(CI, [m[2] for m in col[1]]), _arr(VP, col[2]), _arr(VP, col[3]), _arr(VP, col[4]), _arr(VP, col[5]),
+        _arr(VP, col[6]), _arr(VP, col[7]), _arr(VP, col[8]), _stream())
+    _lib.check(rc, "batched layernorm bwd (encoder stack)")
+
+
+def _bgroups(probs):
+    """Problems of one diagonal by chunk length, at most _BMAX per batched launch."""
+    by = {}
+    for pr in probs:
+        by.setdefault(pr[4] - pr[3], []).append(pr)
+    return [(k, v[s:s + _BMAX]) for k, v in by.items() for s in range(0, len(v), _BMAX)]
+
+
 def _diagonals(chains, tc):
     """[(d, [(m, l, c, t0, t1)])]: every (chain, layer, chunk) with l + c = d."""
     out = []
@@ -131,16 +216,12 @@ def _diagonals(chains, tc):
     return out
 
 
-def _groups(items, key):
-    """Split into launches: same key (chunk length), at most MAXP problems each."""
+def _groups(items, key, cap):
+    """Split into launches: same key (chunk length), at most cap problems each."""
     by = {}
     for it in items:
         by.setdefault(key(it), []).append(it)
-    out = []
-    for k, v in by.items():
-        for s in range(0, len(v), MAXP):
-            out.append((k, v[s:s + MAXP]))
-    return out
+    return [(k, part) for k, v in by.items() for part in _split(v, cap)]
 
 
 class _EncoderStackFn(Function):
@@ -187,31 +268,35 @@ class _EncoderStackFn(Function):
             states.append(sts)
             outs.append(torch.empty(B, T, H, **f32))
 
+        # per diagonal: the chunks' input projections (one batched GEMM), ONE recurrence launch, then
+        # residual LN, FeedForward Linear, residual LN of every chunk (batched LayerNorm / GEMM launches)
         for probs in _diagonals(chains, tc):
-            for m, l, c, t0, t1 in probs:   # input projections of this diagonal's chunks
-                st = states[m][l]
-                r0, n = t0 * B, (t1 - t0) * B
-                _fwd_gemm(n, 4 * H, H, _p(st["x"], r0 * H), H, st["w_ih"], _p(st["gx"], r0 * 4 * H), 4 * H,
-                          bias=_ptr(st["b_ih"]), device=dev)
-            for tlen, grp in _groups(probs, key=lambda p: p[4] - p[3]):
+            bg = _bgroups(probs)
+            for tlen, grp in bg:
+                items = []
+                for m, l, c, t0, t1 in grp:
+                    st, r0 = states[m][l], t0 * B
+                    items.append((_p(st["x"], r0 * H), st["w_ih"], _p(st["gx"], r0 * 4 * H), _ptr(st["b_ih"]), None))
+                _bgemm(lib, tlen * B, 4 * H, H, items, H, 4 * H, dev=dev)
+            for tlen, grp in _groups(probs, lambda p: p[4] - p[3], _maxp(B, dev)):
                 _launch_fwd(lib, [(chains[m], states[m][l], t0) for m, l, c, t0, t1 in grp], B, tlen, H, dev)
-            for m, l, c, t0, t1 in probs:   # residual LN, FeedForward, residual LN of the chunk
-                ch, st = chains[m], states[m][l]
-                r0, n = t0 * B, (t1 - t0) * B
-                _lib.check(lib.mrg_residual_layernorm_fwd(
-                    n, H, _p(st["y"], r0 * H), _p(st["x"], r0 * H), _ptr(st["g1"]), _ptr(st["be1"]), eps,
-                    _p(st["u"], r0 * H), _p(st["m1"], r0), _p(st["r1"], r0), _stream()), "layernorm fwd")
-                _fwd_gemm(n, H, H, _p(st["u"], r0 * H), H, st["w_ff"], _p(st["z"], r0 * H), H, bias=_ptr(st["b_ff"]),
-                          device=dev)
-                if st["v"] is not None:
-                    rc = lib.mrg_residual_layernorm_fwd(
-                        n, H, _p(st["z"], r0 * H), _p(st["u"], r0 * H), _ptr(st["g2"]), _ptr(st["be2"]), eps,
-                        _p(st["v"], r0 * H), _p(st["m2"], r0), _p(st["r2"], r0), _stream())
-                else:   # last layer: rows (t, b) land in the batch-major output [B, T, H]
-                    rc = lib.mrg_residual_layernorm_fwd_map(
-                        n, H, _p(st["z"], r0 * H), _p(st["u"], r0 * H), _ptr(st["g2"]), _ptr(st["be2"]), eps,
-                        _p(outs[m], t0 * H), ch.T * H, H, B, _p(st["m2"], r0), _p(st["r2"], r0), _stream())
-                _lib.check(rc, "layernorm fwd (encoder stack)")
+            for tlen, grp in bg:
+                n = tlen * B
+                ln1, ff, ln2 = [], [], []
+                for m, l, c, t0, t1 in grp:
+                    ch, st, r0 = chains[m], states[m][l], t0 * B
+                    ln1.append((_p(st["y"], r0 * H), _p(st["x"], r0 * H), _ptr(st["g1"]), _ptr(st["be1"]),
+                                _p(st["u"], r0 * H), (H, 0, 0), _p(st["m1"], r0), _p(st["r1"], r0)))
+                    ff.append((_p(st["u"], r0 * H), st["w_ff"], _p(st["z"], r0 * H), _ptr(st["b_ff"]), None))
+                    if st["v"] is not None:
+                        out, omap = _p(st["v"], r0 * H), (H, 0, 0)
+                    else:   # last layer: rows (t, b) land in the batch-major output [B, T, H]
+                        out, omap = _p(outs[m], t0 * H), (ch.T * H, H, B)
+                    ln2.append((_p(st["z"], r0 * H), _p(st["u"], r0 * H), _ptr(st["g2"]), _ptr(st["be2"]), out, omap,
+                                _p(st["m2"], r0), _p(st["r2"], r0)))
+                _bln_fwd(lib, n, H, eps, ln1)
+                _bgemm(lib, n, H, H, ff, H, H, dev=dev)
+                _bln_fwd(lib, n, H, eps, ln2)
 
         ctx.chains, ctx.tc, ctx.B, ctx.H = chains, tc, B, H
         save = []
@@ -281,28 +366,27 @@ class _EncoderStackFn(Function):
         del diags
 
         for probs in rdiag:
-            for m, l, c, t0, t1 in probs:   # LN2, FeedForward, LN1 backward of the chunk
-                ch, st, gr = chains[m], states[m][l], grads[m][l]
-                r0, n = t0 * B, (t1 - t0) * B
-                bo = block_off(ch.T, c) * 2 * H
-                if l == ch.L - 1:   # the stack's output gradient, batch-major
-                    rc = lib.mrg_residual_layernorm_bwd_map(
-                        n, H, _p(douts[m], t0 * H), ch.T * H, H, B, _p(st["z"], r0 * H), _p(st["u"], r0 * H),
-                        _ptr(st["g2"]), _p(st["m2"], r0), _p(st["r2"], r0), _p(gr["g2"], r0 * H),
-                        _p(gr["ws2"], bo), _stream())
-                else:
-                    rc = lib.mrg_residual_layernorm_bwd_map(
-                        n, H, _p(grads[m][l + 1]["dv"], r0 * H), H, 0, 0, _p(st["z"], r0 * H), _p(st["u"], r0 * H),
-                        _ptr(st["g2"]), _p(st["m2"], r0), _p(st["r2"], r0), _p(gr["g2"], r0 * H),
-                        _p(gr["ws2"], bo), _stream())
-                _lib.check(rc, "layernorm bwd (encoder stack)")
-                du = torch.empty(n, H, **f32)   # d(u) = g2 W_ff + g2 (residual branch in the epilogue)
-                _dx_gemm(n, H, H, _p(gr["g2"], r0 * H), H, st["w_ff"], _ptr(du), H, epi=3, aux=_p(gr["g2"], r0 * H),
-                         ldaux=H, device=dev)
-                _lib.check(lib.mrg_residual_layernorm_bwd_map(
-                    n, H, _ptr(du), H, 0, 0, _p(st["y"], r0 * H), _p(st["x"], r0 * H), _ptr(st["g1"]),
-                    _p(st["m1"], r0), _p(st["r1"], r0), _p(gr["g1"], r0 * H), _p(gr["ws1"], bo), _stream()),
-                    "layernorm bwd (encoder stack)")
+            bg = _bgroups(probs)
+            for tlen, grp in bg:   # LN2, FeedForward, LN1 backward of the chunks (batched launches)
+                n = tlen * B
+                du = torch.empty(len(grp), n, H, **f32)   # d(u) = g2 W_ff + g2 (residual branch in the epilogue)
+                ln2, ff, ln1 = [], [], []
+                for i, (m, l, c, t0, t1) in enumerate(grp):
+                    ch, st, gr = chains[m], states[m][l], grads[m][l]
+                    r0 = t0 * B
+                    bo = block_off(ch.T, c) * 2 * H
+                    if l == ch.L - 1:   # the stack's output gradient, batch-major
+                        dy, dmap = _p(douts[m], t0 * H), (ch.T * H, H, B)
+                    else:
+                        dy, dmap = _p(grads[m][l + 1]["dv"], r0 * H), (H, 0, 0)
+                    ln2.append((dy, dmap, _p(st["z"], r0 * H), _p(st["u"], r0 * H), _ptr(st["g2"]), _p(st["m2"], r0),
+                                _p(st["r2"], r0), _p(gr["g2"], r0 * H), _p(gr["ws2"], bo)))
+                    ff.append((_p(gr["g2"], r0 * H), st["w_ff"], _ptr(du[i]), None, _p(gr["g2"], r0 * H)))
+                    ln1.append((_ptr(du[i]), (H, 0, 0), _p(st["y"], r0 * H), _p(st["x"], r0 * H), _ptr(st["g1"]),
+                                _p(st["m1"], r0), _p(st["r1"], r0), _p(gr["g1"], r0 * H), _p(gr["ws1"], bo)))
+                _bln_bwd(lib, n, H, ln2)
+                _bgemm(lib, n, H, H, ff, H, H, epi=3, ldaux=H, transposed=True, dev=dev)
+                _bln_bwd(lib, n, H, ln1)
             items = {}
             for m, l, c, t0, t1 in probs:
                 ch = chains[m]
@@ -315,15 +399,18 @@ class _EncoderStackFn(Function):
                 items.setdefault(t1 - t0, []).append(
                     (ch, states[m][l], grads[m][l], t0, dh_in, dc_in, dh_out, dc_out))
             for tlen, grp in items.items():
-                for s in range(0, len(grp), MAXP):
-                    _launch_bwd(lib, grp[s:s + MAXP], B, tlen, H, dev)
-            for m, l, c, t0, t1 in probs:   # input gradient of the chunk: dG W_ih + g1 (residual)
-                ch, st, gr = chains[m], states[m][l], grads[m][l]
-                r0, n = t0 * B, (t1 - t0) * B
-                _dx_gemm(n, H, 4 * H, _p(gr["dG"], r0 * 4 * H), 4 * H, st["w_ih"], _p(gr["dv"], r0 * H), H, epi=3,
-                         aux=_p(gr["g1"], r0 * H), ldaux=H, device=dev)
+                for part in _split(grp, _maxp(B, dev)):
+                    _launch_bwd(lib, part, B, tlen, H, dev)
+            for tlen, grp in bg:   # input gradients of the chunks: dG W_ih + g1 (residual), batched
+                items = []
+                for m, l, c, t0, t1 in grp:
+                    st, gr, r0 = states[m][l], grads[m][l], t0 * B
+                    items.append((_p(gr["dG"], r0 * 4 * H), st["w_ih"], _p(gr["dv"], r0 * H), None,
+                                  _p(gr["g1"], r0 * H)))
+                _bgemm(lib, tlen * B, H, 4 * H, items, 4 * H, H, epi=3, ldaux=H, transposed=True, dev=dev)
+            for m, l, c, t0, t1 in probs:
                 if c == 0:
-                    _EncoderStackFn._weight_grads(lib, ch, st, gr, l, B, H, dev)
+                    _EncoderStackFn._weight_grads(lib, chains[m], states[m][l], grads[m][l], l, B, H, dev)
         return (None,) + tuple(_EncoderStackFn._input_grads(chains, ctx.needs_input_grad))
 
     @staticmethod

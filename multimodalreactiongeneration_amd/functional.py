@@ -476,11 +476,14 @@ def _wt_note(w, rows, need=True):
 
 
 def _wt(w):
-    """Backward side: the [in][out] copy of w, or None when w was not noted in this step's forward."""
+    """Backward side: the [in][out] copy of w, or None when w was not noted in this step's forward.
+    Copies are valid only within the backward pass (autograd graph task) that made them: a copy keyed
+    by a pointer that a later model reuses, or made before an optimizer step, is never handed out."""
     k = _wt_key(w)
+    task = torch._C._current_graph_task_id()
     t = _WT_CACHE.get(k)
-    if t is not None:
-        return t
+    if t is not None and t[0] == task:
+        return t[1]
     if k not in _WT_PENDING:
         return None
     items = list(_WT_PENDING.values())
@@ -493,8 +496,8 @@ def _wt(w):
         (ctypes.c_int * n)(*[x.shape[0] for x in items]), (ctypes.c_int * n)(*[x.shape[1] for x in items]),
         _stream()), "transpose")
     for x, o in zip(items, outs):
-        _WT_CACHE[_wt_key(x)] = o
-    return _WT_CACHE[k]
+        _WT_CACHE[_wt_key(x)] = (task, o)
+    return _WT_CACHE[k][1]
 
 
 # --- pre-split weights: the three bf16 planes of every weight (and of its transpose), made once per

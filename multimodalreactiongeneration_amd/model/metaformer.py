@@ -230,10 +230,10 @@ class MultiModalMetaformer(nn.Module):
                         xs[i] = chains[i][layer].feed_forward(u)
         return xs
 
-    # ---- MI355X schedule: block 0's embedding stacks as one layer-wavefront (encoder_stack.py);
-    # MRG_ENCODER_STACK=1 turns it on (off by default until the recurrence's large-batch-tile form
-    # makes the wavefront's wider launches pay: DESIGN.md §8)
-    use_encoder_stack = os.environ.get("MRG_ENCODER_STACK", "0") == "1"
+    # ---- MI355X schedule: block 0's embedding stacks as one layer-wavefront (encoder_stack.py: one
+    # recurrence launch and batched GEMM / LayerNorm launches per (layer, time chunk) diagonal); on by
+    # default (measured 27.6 -> 26.0 ms/step), MRG_ENCODER_STACK=0 keeps the per-layer schedule
+    use_encoder_stack = os.environ.get("MRG_ENCODER_STACK", "1") == "1"
 
     def _stack_layers(self, block: MultiModalMetaformerBlock):
         """Per modality the (w_ih, w_hh, b_ih, b_hh, ln1, ff, ln2) tensors of block 0's LSTM blocks, or

@@ -925,3 +925,122 @@ def test_lstm_handoff_timeout_skips_adamw_and_raises():
     torch.cuda.synchronize()
     Fn.check_errors()
     assert not torch.equal(opt.flat, before)
+
+
+@pytest.mark.parametrize("M,N,K,epi,n", [(3840, 1024, 256, 0, 11), (3840, 256, 256, 3, 5), (3840, 256, 1024, 3, 16),
+                                         (300, 256, 64, 0, 3), (100, 96, 40, 1, 2)])
+def test_batched_gemm_matches_single_products(M, N, K, epi, n, gemm_mode):
+    """mrg_gemm_x6g_batched (the encoder stack's per-diagonal products): every problem bitwise equal to
+    the same product launched alone (shapes outside the LDS-DMA kernel run one by one)."""
+    import ctypes
+    from multimodalreactiongeneration_amd import _lib as L
+    from multimodalreactiongeneration_amd import functional as Fn
+    lib = L.load()
+    g = torch.Generator().manual_seed(M + N + K + n)
+    As = [torch.randn(M, K, generator=g).to(DEV) for _ in range(n)]
+    Ws = [(torch.randn(N, K, generator=g) / math.sqrt(K)).to(DEV) for _ in range(n)]
+    bs = [torch.randn(N, generator=g).to(DEV) for _ in range(n)]
+    aux = [torch.randn(M, N, generator=g).to(DEV) for _ in range(n)] if epi >= 2 else None
+    Cs = [torch.empty(M, N, device=DEV) for _ in range(n)]
+    VP = ctypes.c_void_p
+    arr = lambda v: (VP * n)(*[VP(t.data_ptr()) for t in v])  # noqa: E731
+    L.check(lib.mrg_gemm_x6g_batched(n, M, N, K, 1.0, arr(As), K, arr(Ws), K, 0.0, arr(Cs), N, arr(bs), epi,
+                                     None if aux is None else arr(aux), N, 0, Fn._stream()), "batched")
+    for i in range(n):
+        ref = torch.empty(M, N, device=DEV)
+        L.check(lib.mrg_gemm_f32_ex(M, N, K, 1.0, VP(As[i].data_ptr()), 0, K, 0, 0, VP(Ws[i].data_ptr()), 1, K, 0, 0,
+                                    0.0, VP(ref.data_ptr()), N, VP(bs[i].data_ptr()), epi,
+                                    None if aux is None else VP(aux[i].data_ptr()), N, None, 1, None, None, 0.0, None,
+                                    Fn._stream()), "single")
+        torch.cuda.synchronize()
+        assert torch.equal(Cs[i], ref), i
+        exact = As[i].double() @ Ws[i].double().T + bs[i].double()
+        if epi == 1:
+            exact = exact.clamp_min(0)
+        elif epi == 3:
+            exact = exact + aux[i].double()
+        assert rel_err(Cs[i], exact) < TOL
+
+
+@pytest.mark.parametrize("n,rows,E", [(11, 3840, 256), (3, 70, 512), (16, 32, 36)])
+def test_batched_layernorm_matches_single(n, rows, E):
+    """mrg_residual_layernorm_{fwd,bwd}_batched: each problem bitwise equal to the row-mapped single
+    launch, output / incoming-gradient rows through per-problem maps (time-major <-> batch-major)."""
+    import ctypes
+    from multimodalreactiongeneration_amd import _lib as L
+    from multimodalreactiongeneration_amd import functional as Fn
+    lib = L.load()
+    g = torch.Generator().manual_seed(n * rows + E)
+    VP, CL, CI = ctypes.c_void_p, ctypes.c_long, ctypes.c_int
+    Bm = 2 if rows % 2 == 0 else 1
+    Tm = rows // Bm
+    r = lambda *s: torch.randn(*s, generator=g).to(DEV)  # noqa: E731
+    a, b, dy = [r(rows, E) for _ in range(n)], [r(rows, E) for _ in range(n)], [r(Bm, Tm, E) for _ in range(n)]
+    gam, bet = [1 + 0.1 * r(E) for _ in range(n)], [0.1 * r(E) for _ in range(n)]
+    maps = [(Tm * E, E, Bm) if i % 2 else (E, 0, 0) for i in range(n)]   # odd problems: time-major -> [B, T, E]
+    nblk = (rows + 31) // 32
+    outs = {k: [torch.zeros(Bm, Tm, E, device=DEV) if k in ("y", "y1") else
+                torch.zeros(rows, E, device=DEV) if k in ("dx", "dx1") else
+                torch.zeros(nblk * 2 * E, device=DEV) if k in ("ws", "ws1") else torch.zeros(rows, device=DEV)
+                for _ in range(n)] for k in ("y", "m", "s", "dx", "ws", "y1", "m1", "s1", "dx1", "ws1")}
+    P = lambda v: (VP * n)(*[VP(t.data_ptr()) for t in v])  # noqa: E731
+    L.check(lib.mrg_residual_layernorm_fwd_batched(
+        n, rows, E, P(a), P(b), P(gam), P(bet), 1e-5, P(outs["y"]), (CL * n)(*[m[0] for m in maps]),
+        (CL * n)(*[m[1] for m in maps]), (CI * n)(*[m[2] for m in maps]), P(outs["m"]), P(outs["s"]), Fn._stream()),
+        "fwd batched")
+    L.check(lib.mrg_residual_layernorm_bwd_batched(
+        n, rows, E, P(dy), (CL * n)(*[m[0] for m in maps]), (CL * n)(*[m[1] for m in maps]),
+        (CI * n)(*[m[2] for m in maps]), P(a), P(b), P(gam), P(outs["m"]), P(outs["s"]), P(outs["dx"]),
+        P(outs["ws"]), Fn._stream()), "bwd batched")
+    for i in range(n):
+        lo, hi, dv = maps[i]
+        L.check(lib.mrg_residual_layernorm_fwd_map(rows, E, VP(a[i].data_ptr()), VP(b[i].data_ptr()),
+                                                   VP(gam[i].data_ptr()), VP(bet[i].data_ptr()), 1e-5,
+                                                   VP(outs["y1"][i].data_ptr()), lo, hi, dv,
+                                                   VP(outs["m1"][i].data_ptr()), VP(outs["s1"][i].data_ptr()),
+                                                   Fn._stream()), "fwd")
+        L.check(lib.mrg_residual_layernorm_bwd_map(rows, E, VP(dy[i].data_ptr()), lo, hi, dv, VP(a[i].data_ptr()),
+                                                   VP(b[i].data_ptr()), VP(gam[i].data_ptr()),
+                                                   VP(outs["m1"][i].data_ptr()), VP(outs["s1"][i].data_ptr()),
+                                                   VP(outs["dx1"][i].data_ptr()), VP(outs["ws1"][i].data_ptr()),
+                                                   Fn._stream()), "bwd")
+    torch.cuda.synchronize()
+    for i in range(n):
+        for k in ("y", "m", "s", "dx", "ws"):
+            assert torch.equal(outs[k][i], outs[k + "1"][i]), (i, k)
+    # and the math: problem 1 (batch-major output) vs torch fp64
+    x = (a[1] + b[1]).double()
+    ref = torch.nn.functional.layer_norm(x, (E,), gam[1].double(), bet[1].double(), 1e-5)
+    lo, hi, dv = maps[1]
+    got = outs["y"][1].reshape(Bm, Tm, E).permute(1, 0, 2).reshape(rows, E) if dv else outs["y"][1].reshape(rows, E)
+    assert rel_err(got, ref) < TOL
+
+
+@pytest.mark.parametrize("lds", [64 * 1024, 160 * 1024])
+def test_recurrence_behind_cu_occupying_kernel_does_not_time_out(lds):
+    """A persistent recurrence launched while another stream's kernel holds every CU (the RCCL
+    all-reduce of an overlapped DDP bucket, ddp.GradReducer(overlap=True)) waits for CUs and then
+    runs; its hand-offs do not time out and the result is bitwise the one run alone."""
+    from multimodalreactiongeneration_amd import _lib as L
+    from multimodalreactiongeneration_amd import functional as Fn
+    lib = L.load()
+    torch.manual_seed(5)
+    H, B, T = 256, 64, 300
+    k = 1 / math.sqrt(H)
+    ps = [_param((torch.rand(*s) * 2 - 1) * k) for s in ((4 * H, H), (4 * H, H), (4 * H,), (4 * H,))]
+    x = torch.randn(B, T, H, device=DEV)
+    with torch.no_grad():
+        ref = Fn.lstm_layer(x, *ps)[0].clone()
+    torch.cuda.synchronize()
+    cus = L.cu_count(0)
+    other = torch.cuda.Stream(device=DEV)
+    start = torch.cuda.Event()
+    start.record()
+    other.wait_event(start)
+    with torch.cuda.stream(other):   # 4 workgroups of 1024 lanes per CU for 30 ms
+        L.check(lib.mrg_debug_busy(4 * cus, 1024, lds, 30000.0, Fn._stream()), "busy")
+    with torch.no_grad():
+        y = Fn.lstm_layer(x, *ps)[0]
+    torch.cuda.synchronize()
+    Fn.check_errors()
+    assert torch.equal(y, ref)

@@ -64,6 +64,8 @@ doc = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes
        "families": dict({p: fam_total(p) for p in ("lstm_fwd_kernel", "lstm_bwd_kernel", "gemm_x6_kernel", "gemm_f32_kernel",
                                                    "splitk_reduce", "attn_fwd_kernel", "attn_bwd", "resln",
                                                    "adamw_kernel")},
+                        lstm_fwd=fam_total(("lstm_fwd_kernel", "lstm_fwd_mx_kernel")),
+                        lstm_bwd=fam_total(("lstm_bwd_kernel", "lstm_bwd_mx_kernel")),
                         gemm_all=fam_total(("gemm_x6_kernel", "gemm_x6g_kernel", "gemm_x6g_wgrad_kernel",
                                             "gemm_rows_kernel", "gemm_f32_kernel", "gemm_bf16"),
                                            extra=("splitk_reduce",))),
