@@ -39,7 +39,7 @@ from torch.autograd import Function
 
 from . import _lib
 from . import functional as Fn
-from .functional import _ptr, _stream, gemm, _fwd_gemm, _dx_gemm, _wgrad, _wt_note, _gbuf, _on_side
+from .functional import _ptr, _stream, gemm, _dx_gemm, _wt_note, _gbuf, _on_side
 
 # time steps per chunk (the diagonal width); MRG_STACK_CHUNK overrides
 CHUNK = int(os.environ.get("MRG_STACK_CHUNK", "60"))
@@ -415,34 +415,44 @@ class _EncoderStackFn(Function):
 
     @staticmethod
     def _weight_grads(lib, ch, st, gr, l, B, H, dev):
-        """Every parameter gradient of layer l over the whole sequence (its last chunk is done)."""
+        """Every parameter gradient of layer l over the whole sequence (its last chunk is done), issued
+        as ONE fork onto the weight-gradient side stream (functional._side)."""
         T = ch.T
         rows = T * B
-        dG, g2, g1 = gr["dG"], gr["g2"], gr["g1"]
+        dG, g2, g1, dx0 = gr["dG"], gr["g2"], gr["g1"], gr["dv"]
         gbi, gbh = _gbuf(st["b_ih"]), _gbuf(st["b_hh"])
         first = gbi if gbi is not None else gbh
-        _wgrad(_ptr(dG), 4 * H, _ptr(st["x"]), H, rows, 4 * H, H, _gbuf(st["w_ih"]), dev, gb=first,
-               gb2=gbh if gbi is not None else None, keep=(dG, st["x"]))
-        gw = _gbuf(st["w_hh"])
-        if gw is not None and T > 1:   # sum_t dG_t^T y_{t-1}: time-major rows shifted by one step (B rows)
-            _wgrad(_p(dG, B * 4 * H), 4 * H, _ptr(st["y"]), H, (T - 1) * B, 4 * H, H, gw, dev, keep=(dG, st["y"]))
-        _wgrad(_ptr(g2), H, _ptr(st["u"]), H, rows, H, H, _gbuf(st["w_ff"]), dev, gb=_gbuf(st["b_ff"]),
-               keep=(g2, st["u"]))
-        for ws, gam, bet in ((gr["ws1"], st["g1"], st["be1"]), (gr["ws2"], st["g2"], st["be2"])):
-            gg, gb = _gbuf(gam), _gbuf(bet)
-            if gg is None and gb is None:
-                continue
+        gw_ih, gw_hh, gw_ff, gb_ff = _gbuf(st["w_ih"]), _gbuf(st["w_hh"]), _gbuf(st["w_ff"]), _gbuf(st["b_ff"])
+        lns = [(gr["ws1"], _gbuf(st["g1"]), _gbuf(st["be1"])), (gr["ws2"], _gbuf(st["g2"]), _gbuf(st["be2"]))]
+        emb = (_gbuf(ch.emb_w), _gbuf(ch.emb_b)) if l == 0 else (None, None)
+        keep = (dG, g2, g1, dx0, st["x"], st["y"], st["u"], gr["ws1"], gr["ws2"], ch.feat)
 
-            def reduce(ws=ws, gg=gg, gb=gb, nblk=gr["nblk"]):
-                scratch = torch.empty(2, H, device=dev, dtype=torch.float32) if (gg is None or gb is None) else None
+        def wg(dY, ldy, X, ldx, n, Nout, Nin, gw, **kw):
+            if gw is None:
+                gb = kw.get("gb")
+                if gb is not None:
+                    Fn.colsum(n, Nout, dY, ldy, _ptr(gb), out2=_ptr(kw.get("gb2")), device=dev)
+                return
+            gemm(Nout, Nin, n, dY, 1, ldy, X, 0, ldx, _ptr(gw), Nin, beta=1.0, b_hi=kw.get("x_hi", 0),
+                 b_div=kw.get("x_div", 0), splits=Fn.wgrad_splits(Nout, Nin, n), device=dev,
+                 asum_out=_ptr(kw.get("gb")), asum_out2=_ptr(kw.get("gb2")))
+
+        def issue():
+            wg(_ptr(dG), 4 * H, _ptr(st["x"]), H, rows, 4 * H, H, gw_ih, gb=first,
+               gb2=gbh if gbi is not None else None)
+            if gw_hh is not None and T > 1:   # sum_t dG_t^T y_{t-1}: time-major rows shifted by one step
+                wg(_p(dG, B * 4 * H), 4 * H, _ptr(st["y"]), H, (T - 1) * B, 4 * H, H, gw_hh)
+            wg(_ptr(g2), H, _ptr(st["u"]), H, rows, H, H, gw_ff, gb=gb_ff)
+            for ws, gg, gb in lns:
+                if gg is None and gb is None:
+                    continue
+                scratch = Fn._ws(2 * H * 4, dev).view(2, H) if (gg is None or gb is None) else None
                 _lib.check(lib.mrg_residual_layernorm_param_reduce(
-                    nblk * 32, H, _ptr(ws), _ptr(gg if gg is not None else scratch[0]),
+                    gr["nblk"] * 32, H, _ptr(ws), _ptr(gg if gg is not None else scratch[0]),
                     _ptr(gb if gb is not None else scratch[1]), 1, _stream()), "layernorm param reduce")
-            _on_side(dev, rows, (ws,), reduce)
-        if l == 0:   # the embedding: dW_emb = sum dx0^T feat (features read time-major through a row map)
-            dx0 = gr["dv"]
-            _wgrad(_ptr(dx0), H, _ptr(ch.feat), T * ch.F, rows, H, ch.F, _gbuf(ch.emb_w), dev, x_hi=ch.F, x_div=B,
-                   gb=_gbuf(ch.emb_b), keep=(dx0, ch.feat))
+            if l == 0:   # the embedding: dW_emb = sum dx0^T feat (features read time-major through a row map)
+                wg(_ptr(dx0), H, _ptr(ch.feat), T * ch.F, rows, H, ch.F, emb[0], x_hi=ch.F, x_div=B, gb=emb[1])
+        _on_side(dev, rows, keep, issue)
 
     @staticmethod
     def _input_grads(chains, need):

@@ -92,7 +92,24 @@ def _stream():
 
 
 def _ws(nbytes: int, device) -> torch.Tensor:
-    return torch.empty(max(1, (int(nbytes) + 3) // 4), dtype=torch.float32, device=device)
+    t = torch.empty(max(1, (int(nbytes) + 3) // 4), dtype=torch.float32, device=device)
+    _hold_if_side(t)
+    return t
+
+
+def _hold_if_side(t: torch.Tensor):
+    """A scratch tensor allocated on the weight-gradient side stream stays referenced until the
+    backward's join (see _ensure_join).  Freed earlier, its block could go to an allocation on the
+    main stream while the side-stream kernel that uses it has not run yet: inside a HIP-graph capture
+    the private pool does not keep the two streams' blocks apart (measured: the encoder stack's
+    replayed gradients were corrupted by split-K slabs reused as main-stream temporaries)."""
+    if not _SIDE:
+        return
+    dev = t.device.index or 0
+    s = _SIDE.get(dev)
+    if (s is not None and torch.cuda.current_stream(t.device) == s and dev in _JOIN_PENDING
+            and torch.cuda.is_current_stream_capturing()):
+        _SIDE_HOLD.setdefault(dev, []).append(t)
 
 
 def _counters(device) -> torch.Tensor:
@@ -272,6 +289,7 @@ def colsum(rows, N, X, ld, out, *, out2=None, beta=1.0, ld_hi=0, rdiv=0, device=
 _WGRAD_SIDE = [os.environ.get("MRG_WGRAD_STREAM", "1") != "0"]
 _SIDE_MIN_ROWS = 2048
 _SIDE = {}
+_SIDE_HOLD = {}   # device -> side-stream scratch tensors kept alive until the join (_hold_if_side)
 # device -> autograd graph-task id whose final callback will join the side stream back.  Keyed by
 # the task (torch._C._current_graph_task_id), not a bare flag: a backward that raised after a fork
 # never ran its callback, and a stale flag would make every later backward skip the join.
@@ -312,6 +330,7 @@ def _ensure_join(key, cur, s, task):
             _flush_deferred(key, cur.device)
             cur.wait_stream(s)
             _JOIN_PENDING.pop(key, None)
+            _SIDE_HOLD.pop(key, None)   # their blocks are reusable now: later work is ordered after the wait
         torch.autograd.Variable._execution_engine.queue_callback(join)
         _JOIN_PENDING[key] = task
 
@@ -759,7 +778,7 @@ def _resln_bwd(dy2, a2, b2, gamma, beta, mean, rstd):
         def reduce():
             scratch = None
             if gg is None or gb is None:
-                scratch = torch.empty(2, E, device=dev, dtype=torch.float32)
+                scratch = _ws(2 * E * 4, dev).view(2, E)
             _lib.check(lib.mrg_residual_layernorm_param_reduce(
                 rows, E, _ptr(ws), _ptr(gg if gg is not None else scratch[0]),
                 _ptr(gb if gb is not None else scratch[1]), 1, _stream()), "layernorm param reduce")

@@ -10,6 +10,8 @@ TAG=${1:-v1}
 O=$R/gpurun_out/r03_$TAG
 mkdir -p $O
 cd $R
+timeout -k 10 120 python -u tools/tools_capture_forks.py > $O/forks.log 2>&1 || { tail -5 $O/forks.log; exit 1; }
+grep between $O/forks.log
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread \
   > $O/gpu_tests.log 2>&1 || { tail -30 $O/gpu_tests.log; exit 1; }
 tail -1 $O/gpu_tests.log
