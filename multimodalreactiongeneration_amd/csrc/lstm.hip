@@ -441,7 +441,7 @@ template <int H, int G>
 static int launch_fwd(const LstmFwdArgs& a, int force_bs, int cus, hipStream_t s) {
   constexpr int NT = LstmNT<H, G>::value;
   const long groups1 = a.B;
-  if (H == 256 && G == 8 && g_mx && force_bs <= 0 && !a.inject && !a.stamps) {
+  if (H == 256 && G == 8 && g_mx && force_bs <= 0 && !a.inject && (!a.stamps || g_mx == 2)) {
     const int bs = valu_bs(lstm_fwd_kernel<H, G, 1>, lstm_fwd_kernel<H, G, 2>, lstm_fwd_kernel<H, G, 4>,
                            lstm_fwd_kernel<H, G, 8>, lstm_fwd_kernel<H, G, 16>, NT, a.nprob, a.B, G, cus);
     if (g_mx == 2 || bs == 0 || bs >= g_mx_min_bs) {
@@ -472,7 +472,8 @@ static int g_bwd_blocks_per_cu = 0;  // cap on resident workgroups per CU (mrg_l
 template <int H, int G>
 static int launch_bwd(const LstmBwdArgs& a, int force_bs, int cus, hipStream_t s) {
   constexpr int NT = LstmNT<H, G>::value;
-  if (H == 256 && G == 8 && g_mx && force_bs <= 0 && !a.stamps && g_bwd_blocks_per_cu == 0) {
+  // (the MFMA form runs one workgroup per CU, within a cap of one: mrg_lstm_set_blocks_per_cu)
+  if (H == 256 && G == 8 && g_mx && force_bs <= 0 && (!a.stamps || g_mx == 2) && g_bwd_blocks_per_cu <= 1) {
     const int bs = valu_bs(lstm_bwd_kernel<H, G, 1>, lstm_bwd_kernel<H, G, 2>, lstm_bwd_kernel<H, G, 4>,
                            lstm_bwd_kernel<H, G, 8>, lstm_bwd_kernel<H, G, 16>, NT, a.nprob, a.B, G, cus);
     if (g_mx == 2 || bs == 0 || bs >= g_mx_min_bs) {

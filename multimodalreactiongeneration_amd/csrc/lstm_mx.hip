@@ -117,6 +117,7 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_fwd_mx_kernel(LstmFwdArgs args)
 
   for (int tt = 0; tt < T; ++tt) {
     const int t = P.reverse ? T - 1 - tt : tt;
+    MRG_STAMP(0);
     // 1. pre[b][r] = sum_k h[b][k] W[r][k] for this wave's 16 rows
     f32x4mx acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -128,7 +129,9 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_fwd_mx_kernel(LstmFwdArgs args)
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) pre[4 * (lane >> 4) + i][16 * wave + ar] = acc[i];
+    MRG_STAMP(1);
     __syncthreads();
+    MRG_STAMP(2);
     // 2. gates + cell, 3. publish, store, prefetch
     const int par = tt & 1;
     if (cvalid) {
@@ -146,6 +149,7 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_fwd_mx_kernel(LstmFwdArgs args)
       P.cs[(long)bg * P.cs_bs + (long)t * P.cs_ts + hcol] = c;
       if (tt + 1 < T) load_gx(P.reverse ? t - 1 : t + 1);
     }
+    MRG_STAMP(3);
     // 4. gather h_t of the group (BS x H granules, 8 per thread)
     if (tt + 1 < T) {
       constexpr int NG = BS * H / MX_NT;  // 8 granules: pairs (k, k + 1) at 4 rows
@@ -162,7 +166,9 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_fwd_mx_kernel(LstmFwdArgs args)
         put_pair(b, k, ok ? gv[2 * m] : 0.0f, ok ? gv[2 * m + 1] : 0.0f);
       }
     }
+    MRG_STAMP(4);
     __syncthreads();
+    MRG_STAMP(5);
   }
   if (cvalid) {
     if (P.hT) P.hT[(long)bg * H + hcol] = h;
@@ -237,6 +243,7 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_bwd_mx_kernel(LstmBwdArgs args)
 
   for (int tt = 0; tt < T; ++tt) {
     const int t = P.reverse ? tt : T - 1 - tt;
+    MRG_STAMP(0);
     if (cvalid) {
       if (tt > 0) {
         const int par = (tt - 1) & 1;
@@ -248,6 +255,7 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_bwd_mx_kernel(LstmBwdArgs args)
         for (int src = 0; src < G; ++src) s += gv[src];
         dhrec = s;
       }
+      MRG_STAMP(1);
       const int sl = tt & 1;
       const float ig = sv[sl][0][tid], fg = sv[sl][1][tid], gg = sv[sl][2][tid], og = sv[sl][3][tid];
       const float cc = sv[sl][4][tid], cp = sv[sl][5][tid], dyv = sv[sl][6][tid];
@@ -274,7 +282,9 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_bwd_mx_kernel(LstmBwdArgs args)
         dgp[p][cb][(q + 1) * U + cu] = __builtin_bit_cast(__bf16, (unsigned short)(pw[p] >> 16));
       }
     }
+    MRG_STAMP(2);
     __syncthreads();
+    MRG_STAMP(3);
     // partial dh_{t-1}[b][n] = sum over this member's rows of dG[b][row] W[row][n], n in this wave's
     // two column tiles; lane holds rows 4 (lane >> 4) + i, column 16 ct' + (lane & 15)
     {
@@ -288,6 +298,7 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_bwd_mx_kernel(LstmBwdArgs args)
         acc[0] = mx_mfma6(fa, wf[0][s], acc[0]);
         acc[1] = mx_mfma6(fa, wf[1][s], acc[1]);
       }
+      MRG_STAMP(4);
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct) {
         const int n = 16 * (2 * wave + ct) + ar;
@@ -308,7 +319,9 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_bwd_mx_kernel(LstmBwdArgs args)
       io_stage(tt + 1);
       io_load(tt + 2);
     }
+    MRG_STAMP(5);
     __syncthreads();
+    MRG_STAMP(6);
   }
   if (cvalid) {
     if (P.dh0) {

@@ -124,6 +124,8 @@ def _launch_bwd(lib, items, B, Tc, H, dev):
         lay += [4 * H, B * 4 * H, H, B * H, H, 4 * H, B * 4 * H, 0]
         rev.append(0)
     A = lambda ct, v: (ct * n)(*v)  # noqa: E731
+    # deferred weight gradients (functional._DEFER) run beside this recurrence, as in _LSTMFn.backward
+    lib.mrg_lstm_set_blocks_per_cu(Fn.flush_beside_recurrence(dev))
     with Fn._probe("lstm_bwd", 8.0 * H * H * B * Tc * n):
         rc = lib.mrg_lstm_bwd(n, B, Tc, H, A(VP, whh), A(VP, gates), A(VP, cs), A(VP, c0), A(VP, dy),
                               A(CL, dybs), A(CL, dyts), A(VP, dhT), A(VP, dcT), A(VP, dG), A(VP, dh0), A(VP, dc0),

@@ -84,8 +84,67 @@ class IntegrateModalBlock(nn.Module):
         hx = [None] * (self.modal_num - 1) if hx is None else hx
         return other_modals, attn_mask, hx
 
+    # ---- MI355X schedule: every integrator + the concat + cat_linear as one fused op (integrate.py)
+    use_fused = os.environ.get("MRG_FUSED_INTEGRATOR", "1") == "1"
+
+    def _fused(self, main_modal, other_modals, attn_mask, hxs):
+        """integrate.integrate(...) when the block is inside its form (single-block MHA layerds with
+        residual LN, one-Linear residual-LN FeedForward, block-causal or no mask, no state), else None."""
+        from .masks import BlockCausalMask
+        from ..integrate import integrate
+        if not (self.use_fused and isinstance(main_modal, torch.Tensor) and main_modal.is_cuda
+                and main_modal.dim() == 3 and main_modal.shape[1] > 1 and all(h is None for h in hxs)):
+            return None
+        B, T, E = main_modal.shape
+        n = len(self.integrators)
+        cw = self.cat_linear.weight
+        if self.cat_linear.bias is None or tuple(cw.shape) != (E, n * E):
+            return None
+        params, heads, eps, masks = [], set(), set(), []
+        for integ, kv, m in zip(self.integrators, other_modals, attn_mask):
+            if (integ.input_projection is not None or integ.output_projection is not None or integ.self_attention
+                    or len(integ.mixer) != 1):
+                return None
+            blk = integ.mixer[0]
+            res, ffw = blk.mixer, getattr(blk.feed_forward, "feed_forward", None)
+            if not (isinstance(res, ResidualConnection) and res.layer_norm is not None and len(res.module.mixer) == 1):
+                return None
+            mha = res.module.mixer[0].mha
+            if (not mha.batch_first or (mha.dropout and mha.training) or mha.in_proj_bias is None
+                    or tuple(mha.in_proj_weight.shape) != (3 * E, E) or mha.out_proj.bias is None
+                    or getattr(mha, "bias_k", None) is not None):
+                return None
+            if not (isinstance(ffw, ResidualConnection) and ffw.layer_norm is not None):
+                return None
+            mods = list(ffw.module.children())
+            if len(mods) != 1 or not isinstance(mods[0], nn.Linear) or mods[0].bias is None:
+                return None
+            if not (isinstance(kv, torch.Tensor) and kv.dim() == 3 and kv.shape[0] == B and kv.shape[2] == E
+                    and kv.is_cuda):
+                return None
+            if m is not None and not isinstance(m, BlockCausalMask):
+                return None
+            heads.add(mha.num_heads)
+            eps.update((res.layer_norm.eps, ffw.layer_norm.eps))
+            masks.append(m)
+            params.append((mha.in_proj_weight, mha.in_proj_bias, mha.out_proj.weight, mha.out_proj.bias,
+                           res.layer_norm.weight, res.layer_norm.bias, mods[0].weight, mods[0].bias,
+                           ffw.layer_norm.weight, ffw.layer_norm.bias))
+        if len(heads) != 1 or len(eps) != 1 or E % next(iter(heads)) != 0:
+            return None
+        causal = masks[0] is not None
+        if any((m is not None) != causal for m in masks):
+            return None
+        qpads = [m.main_pad if causal else None for m in masks]
+        kpads = [m.other_pad if causal else None for m in masks]
+        return integrate(main_modal, list(other_modals), qpads, kpads, params, cw, self.cat_linear.bias,
+                         heads.pop(), causal, eps.pop())
+
     def forward(self, main_modal, other_modals, attn_mask=None, hxs=None):
         other_modals, attn_mask, hxs = self.check_form_input(other_modals, attn_mask, hxs)
+        out = self._fused(main_modal, other_modals, attn_mask, hxs)
+        if out is not None:
+            return (out, [None] * (self.modal_num - 1))
         ys, states = [], []
         for i, integ in enumerate(self.integrators):
             y, st, _ = integ(main_modal, hxs[i], other_modals[i], other_modals[i], attn_mask[i])

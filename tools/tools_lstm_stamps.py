@@ -17,6 +17,10 @@ dev = "cuda:0"
 lib = _lib.load()
 FWD = ["gemv", "reduce+pre", "sync1", "cell+publish", "gather", "sync2"]
 BWD = ["gather", "cell-bwd", "sync1", "gemv", "reduce+publish", "sync2"]
+if os.environ.get("MX") == "2":   # the MFMA form's phases (lstm_mx.hip)
+    lib.mrg_lstm_set_mx(2, 0)
+    FWD = ["mfma+pre", "sync1", "cell+publish", "gather+split", "sync2", "-"]
+    BWD = ["gather", "cell-bwd+split", "sync1", "mfma", "publish+io", "sync2"]
 
 
 def report(name, st, labels):

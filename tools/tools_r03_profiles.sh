@@ -24,7 +24,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/tra
   python3 $R/bench.py --steps 5 --warmup 2 --cpu-baseline 0 --secondary 0 > $O/trace.log 2>&1 \
   || { echo "trace failed"; tail -20 $O/trace.log; exit 1; }
 echo "trace ok"
-for c in FETCH_SIZE WRITE_SIZE; do
+for c in $([ "${PMC:-1}" = "1" ] && echo FETCH_SIZE WRITE_SIZE); do
   timeout -k 10 400 rocprofv3 --pmc $c -d $O/pmc/$c -o pmc --output-format csv -- \
     python3 $R/bench.py --graph 0 --wgrad-stream 0 --cpu-baseline 0 --secondary 0 --steps 1 --warmup 1 \
     > $O/pmc_$c.log 2>&1 || { echo "pmc $c failed"; tail -20 $O/pmc_$c.log; exit 1; }
@@ -36,6 +36,8 @@ python3 tools/tools_trace_roofline.py $T $O/trace_roofline.json > /dev/null
 python3 tools/tools_timeline.py $T 2 > $O/timeline.txt
 S=$(ls $O/trace/*/run_kernel_stats.csv $O/trace/run_kernel_stats.csv 2>/dev/null | head -1)
 python3 tools/tools_prof_summary.py $S > $O/kernel_summary.txt 2>/dev/null || cp $S $O/kernel_stats.csv
-P=$(dirname $(ls $O/pmc/FETCH_SIZE/*/pmc_counter_collection.csv $O/pmc/FETCH_SIZE/pmc_counter_collection.csv 2>/dev/null | head -1))
-echo "pmc dir $P"
 cat $O/timeline.txt | head -30
+[ "${STAMPS:-1}" = "1" ] || exit 0
+timeout -k 10 200 env MX=2 STAMP_CFGS=1:0,3:0,8:0 python -u tools/tools_lstm_stamps.py > $O/mx_stamps.log 2>&1 || { tail -5 $O/mx_stamps.log; exit 1; }
+timeout -k 10 200 env STAMP_CFGS=1:0,2:0 python -u tools/tools_lstm_stamps.py > $O/valu_stamps.log 2>&1 || { tail -5 $O/valu_stamps.log; exit 1; }
+grep -E "fwd|bwd" $O/mx_stamps.log $O/valu_stamps.log
