@@ -301,36 +301,30 @@ def _timed_replay(replay, steps, warm, pre=None):
 def _preroll(ms):
     """Hold the current stream for `ms` with one tiny busy kernel (mrg_debug_busy: one 64-lane
     workgroup), so the host queues the eager probe steps that follow while the GPU waits: the
-    probed launches then run back to back as in the graph replay, and a bracket never contains host
-    submission time (without it, brackets of the short GEMMs measured 16 % above the kernels' own
-    rocprof durations)."""
+    probed launches then run back to back beside each other as in the graph replay, not spaced out
+    by host submission (r03: without it the eager step ran host-bound)."""
     from multimodalreactiongeneration_amd import _lib
     from multimodalreactiongeneration_amd import functional as Fn
     _lib.check(_lib.load().mrg_debug_busy(1, 64, 256, float(ms) * 1e3, Fn._stream()), "preroll")
 
 
 def _probe_steps(step, n=1, preroll_ms=150.0):
-    """Family brackets over n eager steps on ONE stream (weight gradients inline), queued behind a
-    pre-roll (see _preroll), so a bracket holds exactly its kernels' own execution: with the replay's
-    side stream a bracket also held the time its kernels waited for CUs that the other stream's
-    kernels occupied (r03: GEMM brackets summed to 17.8 ms/step against 15.0 ms of kernel time in the
-    replay's rocprof trace).  The committed trace of the same command has these probe steps too
-    (tools/tools_trace_roofline.py "probe"), so the live figure and the trace's agree launch for
-    launch; the replayed steps' figures (kernels beside the side stream's) are reported next to it.
+    """Per-family kernel time over n eager steps with the replay's stream schedule (weight gradients
+    on the side stream, as in the captured graph), every kernel of a probed library call timed by
+    events bound to that kernel (functional.probe_start(kernel=True): hipExtLaunchKernelGGL), i.e.
+    its own execution beside whatever runs beside it, as rocprofv3 reports it; queued behind a
+    pre-roll (see _preroll).  The committed trace of the same command holds these probe steps
+    (tools/tools_trace_roofline.py "probe") and the graph-replayed ones ("replay").
     Returns (kernels, roofline)."""
     from multimodalreactiongeneration_amd import functional as Fn
     torch.cuda.synchronize()
-    prev = Fn.set_wgrad_stream(False)
-    try:
-        _preroll(preroll_ms * n)
-        t0 = time.perf_counter()
-        Fn.probe_start(*FAMILIES)
-        for _ in range(n):
-            step()
-        host_ms = (time.perf_counter() - t0) * 1e3
-        per = Fn.probe_stop(with_work=True)
-    finally:
-        Fn.set_wgrad_stream(prev)
+    _preroll(preroll_ms * n)
+    t0 = time.perf_counter()
+    Fn.probe_start(*FAMILIES, kernel=True)
+    for _ in range(n):
+        step()
+    host_ms = (time.perf_counter() - t0) * 1e3
+    per = Fn.probe_stop(with_work=True)
     kernels, roof = families(per, n)
     ahead = host_ms < preroll_ms * n
     if roof is not None:

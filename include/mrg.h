@@ -175,6 +175,12 @@ int mrg_lstm_debug_inject(int mode);
  * microseconds on `stream` (a stand-in for a CU-occupying kernel, e.g. an RCCL collective, beside a
  * persistent recurrence, which must then wait for CUs without timing out its hand-offs).        */
 int mrg_debug_busy(int blocks, int threads, int lds, double usec, hipStream_t stream);
+/* Measurement (bench.py): while on, every kernel launched for a tagged library call (tag >= 0) is
+ * timed by start / stop events bound to that kernel (hipExtLaunchKernelGGL): its own execution,
+ * as rocprofv3 reports it.  stop waits, writes (ms, tag) per launch and returns the count. */
+int mrg_probe_start(int cap);
+int mrg_probe_tag(int tag);
+int mrg_probe_stop(float* ms, int* tags, int cap);
 
 /* MFMA form of the H = 256 recurrences (batch tiles of 16 rows, x6 bf16 split on
  * v_mfma_f32_16x16x32_bf16, fp32-class): mode 0 never, 1 (default) when the VALU form would need
@@ -344,6 +350,13 @@ int mrg_residual_layernorm_bwd_batched(int n, int rows, int E, const float* cons
                                        const float* const* b, const float* const* gamma,
                                        const float* const* mean, const float* const* rstd, float* const* dx,
                                        float* const* ws, hipStream_t stream);
+
+/* Padding helpers: flags[b][t] = (x[b][t][0] == value) as uint8 (gen_attention_mask's padding test,
+ * multi_modal_metaformer.py:67-73; x rows at b * bs + t * ts); y = x * (x != value) (training_step's
+ * zeroing of padded motion_self frames, lstmformer.py:365-366). */
+int mrg_padding_flags(int B, int T, const float* x, long bs, long ts, float value, unsigned char* out,
+                      hipStream_t stream);
+int mrg_zero_padding(long n, const float* x, float value, float* y, hipStream_t stream);
 
 /* ---------------------------------------------------------------- loss
  * Masked regression loss of training_step (lstmformer.py:372-380,

@@ -103,6 +103,11 @@ SIGNATURES = {
     "mrg_residual_layernorm_bwd_batched": (c_int, [c_int, c_int, c_int, PP, PL, PL, PI, PP, PP, PP, PP, PP, PP,
                                                    PP, P]),
     "mrg_debug_busy": (c_int, [c_int, c_int, c_int, ctypes.c_double, P]),
+    "mrg_padding_flags": (c_int, [c_int, c_int, P, c_long, c_long, c_float, P, P]),
+    "mrg_zero_padding": (c_int, [c_long, P, c_float, P, P]),
+    "mrg_probe_start": (c_int, [c_int]),
+    "mrg_probe_tag": (c_int, [c_int]),
+    "mrg_probe_stop": (c_int, [ctypes.POINTER(ctypes.c_float), PI, c_int]),
     "mrg_loss_workspace_bytes": (c_size, [c_int, c_int, c_int]),
     "mrg_masked_loss_fwd": (c_int, [c_int, c_int, c_int, P, c_long, P, c_int, c_float, c_float,
                                     c_int, c_int, c_float, P, P, P]),

@@ -617,10 +617,10 @@ static int attn_check(int D, int Tq, int Tk, int causal) {
 
 #define MRG_ATTN_DISPATCH(KERNEL, grid, args)                          \
   switch (D) {                                                         \
-    case 8: KERNEL<8><<<grid, 256, 0, stream>>>(args); break;         \
-    case 16: KERNEL<16><<<grid, 256, 0, stream>>>(args); break;       \
-    case 32: KERNEL<32><<<grid, 256, 0, stream>>>(args); break;       \
-    case 64: KERNEL<64><<<grid, 256, 0, stream>>>(args); break;       \
+    case 8: klaunch(KERNEL<8>, grid, 256, 0, stream, args); break;         \
+    case 16: klaunch(KERNEL<16>, grid, 256, 0, stream, args); break;       \
+    case 32: klaunch(KERNEL<32>, grid, 256, 0, stream, args); break;       \
+    case 64: klaunch(KERNEL<64>, grid, 256, 0, stream, args); break;       \
   }
 
 MRG_API int mrg_attention_fwd(int B, int Hh, int Tq, int Tk, int D,

@@ -4,6 +4,7 @@
 
 namespace mrg {
 static thread_local char g_err[1024] = "";
+ProbeState g_probe;
 
 void set_error(const char* fmt, ...) {
   va_list ap;
@@ -53,4 +54,48 @@ MRG_API int mrg_debug_busy(int blocks, int threads, int lds, double usec, hipStr
                                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds));
   mrg::busy_kernel<<<blocks, threads, lds, stream>>>(ticks, nullptr);
   return mrg::check_launch("busy_kernel");
+}
+
+using mrg::g_probe;
+
+// Live per-kernel timing (bench.py): up to `cap` launches of the tagged library calls are timed
+// with kernel-bound events (klaunch, mrg_common.h).  Not for graph capture.
+MRG_API int mrg_probe_start(int cap) {
+  MRG_REQUIRE(cap > 0 && cap <= (1 << 16), "mrg_probe_start: cap %d out of range", cap);
+  if (g_probe.cap < cap) {
+    for (int i = 0; i < 2 * g_probe.cap; ++i) (void)hipEventDestroy(g_probe.ev[i]);
+    delete[] g_probe.ev;
+    delete[] g_probe.tags;
+    g_probe.ev = new hipEvent_t[2 * cap];
+    g_probe.tags = new int[cap];
+    for (int i = 0; i < 2 * cap; ++i) MRG_HIP(hipEventCreate(&g_probe.ev[i]));
+    g_probe.cap = cap;
+  }
+  g_probe.n = 0;
+  g_probe.tag = -1;
+  g_probe.on = 1;
+  return 0;
+}
+
+// Tag of the following launches (the host's library-call index), -1 = not timed.
+MRG_API int mrg_probe_tag(int tag) {
+  g_probe.tag = tag;
+  return 0;
+}
+
+// Stop; waits for the timed launches and writes (kernel ms, tag) per launch; returns the count.
+MRG_API int mrg_probe_stop(float* ms, int* tags, int cap) {
+  g_probe.on = 0;
+  g_probe.tag = -1;
+  const int n = g_probe.n < cap ? g_probe.n : cap;
+  for (int i = 0; i < n; ++i) {
+    if (hipEventSynchronize(g_probe.ev[2 * i + 1]) != hipSuccess ||
+        hipEventElapsedTime(&ms[i], g_probe.ev[2 * i], g_probe.ev[2 * i + 1]) != hipSuccess) {
+      mrg::set_error("mrg_probe_stop: event %d failed", i);
+      return -1;
+    }
+    tags[i] = g_probe.tags[i];
+  }
+  g_probe.n = 0;
+  return n;
 }

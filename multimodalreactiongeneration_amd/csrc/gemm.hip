@@ -721,7 +721,7 @@ static void launch_tile(GemmArgs a, int ta, int tb, bool va, bool vb, int splits
     case (TA << 3) | (TB << 2) | (VA << 1) | VB: {                                               \
       auto k = gemm_f32_kernel<BM, BN, BK, TA, TB, (bool)VA, (bool)VB>;                              \
       const int grid = a.ntiles < resident_blocks(k) ? a.ntiles : resident_blocks(k);           \
-      k<<<grid, NT, 0, s>>>(a);                                                                  \
+      klaunch(k, grid, NT, 0, s, a);                                                                  \
     } break;
     MRG_G(0, 0, 0, 0) MRG_G(0, 0, 0, 1) MRG_G(0, 0, 1, 0) MRG_G(0, 0, 1, 1)
     MRG_G(0, 1, 0, 0) MRG_G(0, 1, 0, 1) MRG_G(0, 1, 1, 0) MRG_G(0, 1, 1, 1)
@@ -743,7 +743,7 @@ static void launch_tile_x6(GemmArgs a, int ta, int tb, bool va, bool vb, int spl
     case (TA << 3) | (TB << 2) | (VA << 1) | VB: {                                               \
       auto k = gemm_x6_kernel<BM, BN, TA, TB, (bool)VA, (bool)VB, VAR>;                           \
       const int grid = a.ntiles < resident_blocks(k) ? a.ntiles : resident_blocks(k);           \
-      k<<<grid, NT, 0, s>>>(a);                                                                  \
+      klaunch(k, grid, NT, 0, s, a);                                                                  \
     } break;
     MRG_G(0, 0, 0, 0) MRG_G(0, 0, 0, 1) MRG_G(0, 0, 1, 0) MRG_G(0, 0, 1, 1)
     MRG_G(0, 1, 0, 0) MRG_G(0, 1, 0, 1) MRG_G(0, 1, 1, 0) MRG_G(0, 1, 1, 1)
@@ -852,8 +852,8 @@ static void launch_rows(const GemmArgs& a, hipStream_t s) {
   const bool big = (a.K + 15) / 16 > 16;
 #define MRG_R(TA, TB)                                                                            \
   if (a.transA == TA && a.transB == TB) {                                                        \
-    if (big) gemm_rows_kernel<TA, TB, 64><<<grid, 256, 0, s>>>(a);                               \
-    else gemm_rows_kernel<TA, TB, 16><<<grid, 256, 0, s>>>(a);                                   \
+    if (big) klaunch(gemm_rows_kernel<TA, TB, 64>, grid, 256, 0, s, a);                               \
+    else klaunch(gemm_rows_kernel<TA, TB, 16>, grid, 256, 0, s, a);                                   \
     return;                                                                                      \
   }
   MRG_R(0, 0) MRG_R(0, 1) MRG_R(1, 0) MRG_R(1, 1)
@@ -960,7 +960,7 @@ MRG_API int mrg_transpose_batched(int n, const float* const* src, float* const* 
     }
     tb.first[tb.n] = blocks;
     if (blocks == 0) continue;
-    transpose_batched_kernel<<<blocks, 256, 0, stream>>>(tb);
+    klaunch(transpose_batched_kernel, blocks, 256, 0, stream, tb);
     if (check_launch("transpose_batched_kernel")) return 1;
   }
   return 0;
@@ -989,7 +989,7 @@ MRG_API int mrg_gemm_x6_variant(int var, int M, int N, int K, const float* A, co
     case V: {                                                                               \
       auto k = gemm_x6_kernel<128, 128, 0, 1, true, true, V>;                               \
       const int grid = a.ntiles < resident_blocks(k) ? a.ntiles : resident_blocks(k);      \
-      k<<<grid, NT, 0, stream>>>(a);                                                        \
+      klaunch(k, grid, NT, 0, stream, a);                                                        \
     } break;
     MRG_V(0) MRG_V(1) MRG_V(2) MRG_V(3)
 #undef MRG_V
@@ -1125,15 +1125,15 @@ static int gemm_ex(int mode, int M, int N, int K, float alpha,
     long total = (long)M * N;
     if (a.vec && (N & 3) == 0) {
       const long cb = (total / 4 + RPB - 1) / RPB, ab = a.asum ? (M + RPB - 1) / RPB : 0;
-      splitk_reduce4_kernel<<<(unsigned)(cb + ab), 256, 0, stream>>>(a, splits);
+      klaunch(splitk_reduce4_kernel, (unsigned)(cb + ab), 256, 0, stream, a, splits);
       asum_done = a.asum != nullptr;
     } else {
-      splitk_reduce_kernel<<<(unsigned)((total + 255) / 256), 256, 0, stream>>>(a, splits);
+      klaunch(splitk_reduce_kernel, (unsigned)((total + 255) / 256), 256, 0, stream, a, splits);
     }
     if (check_launch("splitk_reduce_kernel")) return 1;
   }
   if (a.asum && !asum_done) {
-    asum_reduce_kernel<<<(unsigned)((M + RPB - 1) / RPB), 256, 0, stream>>>(a, splits);
+    klaunch(asum_reduce_kernel, (unsigned)((M + RPB - 1) / RPB), 256, 0, stream, a, splits);
     if (check_launch("asum_reduce_kernel")) return 1;
   } else if (asum_out && !a.asum) {
     // not fusable here (exact-f32 mode or A not k-major): the two-pass column-sum kernels
@@ -1256,8 +1256,8 @@ MRG_API int mrg_colsum_f32(int rows, int N, const float* X, long ld, long ld_hi,
   int rows_per = (rows + S - 1) / S;
   if (rows_per == 0) rows_per = 1;
   dim3 grid((N + 63) / 64, S);
-  colsum_partial_kernel<<<grid, 256, 0, stream>>>(X, RowMap{ld, ld_hi, rdiv}, rows, N, rows_per, workspace);
+  klaunch(colsum_partial_kernel, grid, 256, 0, stream, X, RowMap{ld, ld_hi, rdiv}, rows, N, rows_per, workspace);
   if (check_launch("colsum_partial_kernel")) return 1;
-  colsum_final_kernel<<<(N + 63) / 64, 1024, 0, stream>>>(workspace, S, N, beta, out, out2);
+  klaunch(colsum_final_kernel, (N + 63) / 64, 1024, 0, stream, workspace, S, N, beta, out, out2);
   return check_launch("colsum_final_kernel");
 }

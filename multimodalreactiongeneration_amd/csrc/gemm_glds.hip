@@ -274,13 +274,13 @@ static void launch_tiles(GemmArgs a, int ns, long bplane, hipStream_t s, const G
   a.ws = nullptr;
   const unsigned grid = (unsigned)a.tiles_mn * (unsigned)(gb.n > 0 ? gb.n : 1);
   if constexpr (NP == 1) {  // one-plane form: ring depth 2 only
-    gemm_x6g_kernel<BM, BN, 2, 0, 1><<<grid, NT, 0, s>>>(a, bplane, gb);
+    klaunch(gemm_x6g_kernel<BM, BN, 2, 0, 1>, grid, NT, 0, s, a, bplane, gb);
     return;
   }
   switch (ns) {
-    case 2: gemm_x6g_kernel<BM, BN, 2, PB><<<grid, NT, 0, s>>>(a, bplane, gb); break;
-    case 4: gemm_x6g_kernel<BM, BN, 4, PB><<<grid, NT, 0, s>>>(a, bplane, gb); break;
-    default: gemm_x6g_kernel<BM, BN, 3, PB><<<grid, NT, 0, s>>>(a, bplane, gb); break;
+    case 2: klaunch(gemm_x6g_kernel<BM, BN, 2, PB>, grid, NT, 0, s, a, bplane, gb); break;
+    case 4: klaunch(gemm_x6g_kernel<BM, BN, 4, PB>, grid, NT, 0, s, a, bplane, gb); break;
+    default: klaunch(gemm_x6g_kernel<BM, BN, 3, PB>, grid, NT, 0, s, a, bplane, gb); break;
   }
 }
 
@@ -481,7 +481,7 @@ void launch_x6g_wgrad(GemmArgs a, int splits, int bm, int bn, hipStream_t s, int
     a.tiles_mn = a.tiles_n * ((a.M + BM_ - 1) / BM_);
     a.ntiles = a.tiles_mn * splits;
     a.nsplit = splits;
-    kern<<<(unsigned)a.ntiles, NT, 0, s>>>(a);
+    klaunch(kern, (unsigned)a.ntiles, NT, 0, s, a);
   };
   if (planes == 1) go(gemm_x6g_wgrad_kernel<128, 128, 2, 1>, 128, 128);
   else if (bm == 64 && bn == 64) go(gemm_x6g_wgrad_kernel<64, 64, 2>, 64, 64);
@@ -590,7 +590,7 @@ MRG_API int mrg_split_planes_batched(int n, const float* const* src, void* const
     }
     pb.first[pb.n] = blocks;
     if (blocks == 0) continue;
-    split_planes_kernel<<<blocks, 256, 0, stream>>>(pb);
+    klaunch(split_planes_kernel, blocks, 256, 0, stream, pb);
     if (check_launch("split_planes_kernel")) return 1;
   }
   return 0;

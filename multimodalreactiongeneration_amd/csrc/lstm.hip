@@ -454,11 +454,11 @@ static int launch_fwd(const LstmFwdArgs& a, int force_bs, int cus, hipStream_t s
     long nblk = (long)a.nprob * ((groups1 + bs - 1) / bs) * G;
     bool ok;
     switch (bs) {
-      case 1: ok = fits(lstm_fwd_kernel<H, G, 1>, NT, nblk, cus); if (ok) lstm_fwd_kernel<H, G, 1><<<nblk, NT, 0, s>>>(a); break;
-      case 2: ok = fits(lstm_fwd_kernel<H, G, 2>, NT, nblk, cus); if (ok) lstm_fwd_kernel<H, G, 2><<<nblk, NT, 0, s>>>(a); break;
-      case 4: ok = fits(lstm_fwd_kernel<H, G, 4>, NT, nblk, cus); if (ok) lstm_fwd_kernel<H, G, 4><<<nblk, NT, 0, s>>>(a); break;
-      case 8: ok = fits(lstm_fwd_kernel<H, G, 8>, NT, nblk, cus); if (ok) lstm_fwd_kernel<H, G, 8><<<nblk, NT, 0, s>>>(a); break;
-      default: ok = fits(lstm_fwd_kernel<H, G, 16>, NT, nblk, cus); if (ok) lstm_fwd_kernel<H, G, 16><<<nblk, NT, 0, s>>>(a); break;
+      case 1: ok = fits(lstm_fwd_kernel<H, G, 1>, NT, nblk, cus); if (ok) klaunch(lstm_fwd_kernel<H, G, 1>, nblk, NT, 0, s, a); break;
+      case 2: ok = fits(lstm_fwd_kernel<H, G, 2>, NT, nblk, cus); if (ok) klaunch(lstm_fwd_kernel<H, G, 2>, nblk, NT, 0, s, a); break;
+      case 4: ok = fits(lstm_fwd_kernel<H, G, 4>, NT, nblk, cus); if (ok) klaunch(lstm_fwd_kernel<H, G, 4>, nblk, NT, 0, s, a); break;
+      case 8: ok = fits(lstm_fwd_kernel<H, G, 8>, NT, nblk, cus); if (ok) klaunch(lstm_fwd_kernel<H, G, 8>, nblk, NT, 0, s, a); break;
+      default: ok = fits(lstm_fwd_kernel<H, G, 16>, NT, nblk, cus); if (ok) klaunch(lstm_fwd_kernel<H, G, 16>, nblk, NT, 0, s, a); break;
     }
     if (ok) return check_launch("lstm_fwd_kernel");
   }
@@ -487,11 +487,11 @@ static int launch_bwd(const LstmBwdArgs& a, int force_bs, int cus, hipStream_t s
     if (force_bs <= 0 && g_bwd_blocks_per_cu > 0 && bs < 16 && nblk > (long)g_bwd_blocks_per_cu * cus) continue;
     bool ok;
     switch (bs) {
-      case 1: ok = fits(lstm_bwd_kernel<H, G, 1>, NT, nblk, cus); if (ok) lstm_bwd_kernel<H, G, 1><<<nblk, NT, 0, s>>>(a); break;
-      case 2: ok = fits(lstm_bwd_kernel<H, G, 2>, NT, nblk, cus); if (ok) lstm_bwd_kernel<H, G, 2><<<nblk, NT, 0, s>>>(a); break;
-      case 4: ok = fits(lstm_bwd_kernel<H, G, 4>, NT, nblk, cus); if (ok) lstm_bwd_kernel<H, G, 4><<<nblk, NT, 0, s>>>(a); break;
-      case 8: ok = fits(lstm_bwd_kernel<H, G, 8>, NT, nblk, cus); if (ok) lstm_bwd_kernel<H, G, 8><<<nblk, NT, 0, s>>>(a); break;
-      default: ok = fits(lstm_bwd_kernel<H, G, 16>, NT, nblk, cus); if (ok) lstm_bwd_kernel<H, G, 16><<<nblk, NT, 0, s>>>(a); break;
+      case 1: ok = fits(lstm_bwd_kernel<H, G, 1>, NT, nblk, cus); if (ok) klaunch(lstm_bwd_kernel<H, G, 1>, nblk, NT, 0, s, a); break;
+      case 2: ok = fits(lstm_bwd_kernel<H, G, 2>, NT, nblk, cus); if (ok) klaunch(lstm_bwd_kernel<H, G, 2>, nblk, NT, 0, s, a); break;
+      case 4: ok = fits(lstm_bwd_kernel<H, G, 4>, NT, nblk, cus); if (ok) klaunch(lstm_bwd_kernel<H, G, 4>, nblk, NT, 0, s, a); break;
+      case 8: ok = fits(lstm_bwd_kernel<H, G, 8>, NT, nblk, cus); if (ok) klaunch(lstm_bwd_kernel<H, G, 8>, nblk, NT, 0, s, a); break;
+      default: ok = fits(lstm_bwd_kernel<H, G, 16>, NT, nblk, cus); if (ok) klaunch(lstm_bwd_kernel<H, G, 16>, nblk, NT, 0, s, a); break;
     }
     if (ok) return check_launch("lstm_bwd_kernel");
   }
@@ -726,7 +726,7 @@ MRG_API int mrg_lstm_cell_fwd(int B, int H, const float* pre, long pre_ld, const
                               float* gates, float* c, float* h, long h_ld, float* h2, hipStream_t stream) {
   if (B == 0 || H == 0) return 0;
   const long n = (long)B * H;
-  lstm_cell_fwd_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(B, H, pre, pre_ld, b_hh, c0, gates, c, h,
+  klaunch(lstm_cell_fwd_kernel, (unsigned)((n + 255) / 256), 256, 0, stream, B, H, pre, pre_ld, b_hh, c0, gates, c, h,
                                                                         h_ld, h2);
   return check_launch("lstm_cell_fwd_kernel");
 }
@@ -738,6 +738,6 @@ MRG_API int mrg_lstm_cell_bwd(int B, int H, const float* gates, const float* c, 
                               hipStream_t stream) {
   if (B == 0 || H == 0) return 0;
   const long n = (long)B * H;
-  lstm_cell_bwd_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(B, H, gates, c, c0, dh, dh_ld, dh2, dc, dG, dc0);
+  klaunch(lstm_cell_bwd_kernel, (unsigned)((n + 255) / 256), 256, 0, stream, B, H, gates, c, c0, dh, dh_ld, dh2, dc, dG, dc0);
   return check_launch("lstm_cell_bwd_kernel");
 }

@@ -342,14 +342,14 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_bwd_mx_kernel(LstmBwdArgs args)
 int launch_fwd_mx(const LstmFwdArgs& a, int cus, hipStream_t s) {
   const long nblk = (long)a.nprob * ((a.B + MX_BS - 1) / MX_BS) * MX_G;
   if (!fits(lstm_fwd_mx_kernel, MX_NT, nblk, cus)) return 0;
-  lstm_fwd_mx_kernel<<<(unsigned)nblk, MX_NT, 0, s>>>(a);
+  klaunch(lstm_fwd_mx_kernel, (unsigned)nblk, MX_NT, 0, s, a);
   return check_launch("lstm_fwd_mx_kernel") ? -1 : 1;
 }
 
 int launch_bwd_mx(const LstmBwdArgs& a, int cus, hipStream_t s) {
   const long nblk = (long)a.nprob * ((a.B + MX_BS - 1) / MX_BS) * MX_G;
   if (!fits(lstm_bwd_mx_kernel, MX_NT, nblk, cus)) return 0;
-  lstm_bwd_mx_kernel<<<(unsigned)nblk, MX_NT, 0, s>>>(a);
+  klaunch(lstm_bwd_mx_kernel, (unsigned)nblk, MX_NT, 0, s, a);
   return check_launch("lstm_bwd_mx_kernel") ? -1 : 1;
 }
 

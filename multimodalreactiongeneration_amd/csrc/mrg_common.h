@@ -11,11 +11,36 @@
 #include <cstring>
 #include <cmath>
 
+#include <hip/hip_ext.h>
+
 #define MRG_API extern "C" __attribute__((visibility("default")))
 
 namespace mrg {
 
 void set_error(const char* fmt, ...);
+
+// Live kernel timing for bench.py (mrg_probe_*): while a probe is on and the host has tagged the
+// current library call (tag >= 0), every launch of the probed kernels goes through
+// hipExtLaunchKernelGGL with a start / stop event pair that the runtime ties to THAT kernel's own
+// execution, so the time per launch is the kernel's, as rocprofv3 reports it (an event recorded on
+// the stream before / after a launch also holds the dispatch of the next packet).
+struct ProbeState {
+  int on = 0, tag = -1, n = 0, cap = 0;
+  hipEvent_t* ev = nullptr;  // [cap][2]
+  int* tags = nullptr;       // [cap]
+};
+extern ProbeState g_probe;
+
+template <typename K, typename... A>
+inline void klaunch(K kernel, dim3 grid, dim3 block, unsigned shmem, hipStream_t s, A... args) {
+  if (g_probe.on && g_probe.tag >= 0 && g_probe.n < g_probe.cap) {
+    const int i = g_probe.n++;
+    g_probe.tags[i] = g_probe.tag;
+    hipExtLaunchKernelGGL(kernel, grid, block, shmem, s, g_probe.ev[2 * i], g_probe.ev[2 * i + 1], 0, args...);
+    return;
+  }
+  kernel<<<grid, block, shmem, s>>>(args...);
+}
 
 inline int check_launch(const char* what) {
   hipError_t e = hipGetLastError();

@@ -801,3 +801,47 @@ MRG_API int mrg_adamw_step(float* params, const float* grads, float* exp_avg, fl
   adamw_step_inc_kernel<<<1, 1, 0, stream>>>(step_lr, err);
   return check_launch("adamw_step_inc_kernel");
 }
+
+// ------------------------------------------------------------------ padding helpers
+// flags[b][t] = (x[b][t][0] == value): the padding test of gen_attention_mask
+// (multi_modal_metaformer.py:67-73, `x[:, :, 0] == -100`), uint8; x rows at b * bs + t * ts.
+namespace mrg {
+__global__ __launch_bounds__(256) void padding_flags_kernel(int B, int T, const float* __restrict__ x, long bs,
+                                                            long ts, float value, unsigned char* __restrict__ out) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)B * T) return;
+  const long b = i / T, t = i - b * T;
+  out[i] = x[b * bs + t * ts] == value ? 1 : 0;
+}
+
+// y = x * (x != value) elementwise: training_step's zeroing of padded motion_self frames
+// (lstmformer.py:365-366, `batch[2] * (batch[2] != -100)`), float4 where aligned
+__global__ __launch_bounds__(256) void zero_padding_kernel(long n, const float* __restrict__ x, float value,
+                                                           float* __restrict__ y) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (4 * i + 3 < n) {
+    float4 v = reinterpret_cast<const float4*>(x)[i];
+    v.x = v.x != value ? v.x : 0.0f; v.y = v.y != value ? v.y : 0.0f;
+    v.z = v.z != value ? v.z : 0.0f; v.w = v.w != value ? v.w : 0.0f;
+    reinterpret_cast<float4*>(y)[i] = v;
+  } else {
+    for (long j = 4 * i; j < n; ++j) y[j] = x[j] != value ? x[j] : 0.0f;
+  }
+}
+}  // namespace mrg
+
+MRG_API int mrg_padding_flags(int B, int T, const float* x, long bs, long ts, float value, unsigned char* out,
+                              hipStream_t stream) {
+  if (B == 0 || T == 0) return 0;
+  const long n = (long)B * T;
+  padding_flags_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(B, T, x, bs, ts, value, out);
+  return check_launch("padding_flags_kernel");
+}
+
+MRG_API int mrg_zero_padding(long n, const float* x, float value, float* y, hipStream_t stream) {
+  if (n == 0) return 0;
+  MRG_REQUIRE((((uintptr_t)x | (uintptr_t)y) & 15) == 0, "mrg_zero_padding: 16-byte aligned buffers required");
+  const long nv = (n + 3) / 4;
+  zero_padding_kernel<<<(unsigned)((nv + 255) / 256), 256, 0, stream>>>(n, x, value, y);
+  return check_launch("zero_padding_kernel");
+}

@@ -83,10 +83,27 @@ class _Chain:
         self.L = len(layers)
 
 
-def _launch_fwd(lib, items, B, Tc, H, dev):
+class _RingPool:
+    """Hand-off rings of every recurrence launch of one pass, zeroed by ONE fill up front (each launch
+    needs its rings zero at its start; a fill per launch was one more kernel on the critical path)."""
+
+    def __init__(self, n, elems, dev):
+        self.buf = torch.zeros(max(1, n), elems, dtype=torch.int64, device=dev)
+        self.next = 0
+
+    def take(self, n):
+        if self.next + n > self.buf.shape[0]:
+            raise RuntimeError("encoder stack: ring pool exhausted")
+        out = self.buf[self.next:self.next + n]
+        self.next += n
+        return out
+
+
+def _launch_fwd(lib, items, B, Tc, H, dev, pool=None):
     """One persistent forward launch over `items` = [(chain, layer state dict, t0)]."""
     n = len(items)
-    xb = torch.zeros(n, lib.mrg_lstm_fwd_xbuf_bytes(B, H) // 8, dtype=torch.int64, device=dev)
+    xb = pool.take(n) if pool is not None else \
+        torch.zeros(n, lib.mrg_lstm_fwd_xbuf_bytes(B, H) // 8, dtype=torch.int64, device=dev)
     gx, gbs, gts, whh, bhh, h0, c0, y, ybs, yts, gates, cs, lay, rev = ([] for _ in range(14))
     for ch, st, t0 in items:
         r0 = t0 * B
@@ -108,10 +125,11 @@ def _launch_fwd(lib, items, B, Tc, H, dev):
     _lib.check(rc, "lstm fwd (encoder stack)")
 
 
-def _launch_bwd(lib, items, B, Tc, H, dev):
+def _launch_bwd(lib, items, B, Tc, H, dev, pool=None):
     """One persistent backward launch over `items` = [(chain, state, grads, t0, dhT, dcT, dh0, dc0)]."""
     n = len(items)
-    xb = torch.zeros(n, lib.mrg_lstm_bwd_xbuf_bytes(B, H) // 8, dtype=torch.int64, device=dev)
+    xb = pool.take(n) if pool is not None else \
+        torch.zeros(n, lib.mrg_lstm_bwd_xbuf_bytes(B, H) // 8, dtype=torch.int64, device=dev)
     whh, gates, cs, c0, dy, dybs, dyts, dhT, dcT, dG, dh0, dc0, lay, rev = ([] for _ in range(14))
     for ch, st, gr, t0, dh_in, dc_in, dh_out, dc_out in items:
         r0 = t0 * B
@@ -272,7 +290,9 @@ class _EncoderStackFn(Function):
 
         # per diagonal: the chunks' input projections (one batched GEMM), ONE recurrence launch, then
         # residual LN, FeedForward Linear, residual LN of every chunk (batched LayerNorm / GEMM launches)
-        for probs in _diagonals(chains, tc):
+        diags = _diagonals(chains, tc)
+        pool = _RingPool(sum(len(p) for p in diags), lib.mrg_lstm_fwd_xbuf_bytes(B, H) // 8, dev)
+        for probs in diags:
             bg = _bgroups(probs)
             for tlen, grp in bg:
                 items = []
@@ -281,7 +301,7 @@ class _EncoderStackFn(Function):
                     items.append((_p(st["x"], r0 * H), st["w_ih"], _p(st["gx"], r0 * 4 * H), _ptr(st["b_ih"]), None))
                 _bgemm(lib, tlen * B, 4 * H, H, items, H, 4 * H, dev=dev)
             for tlen, grp in _groups(probs, lambda p: p[4] - p[3], _maxp(B, dev)):
-                _launch_fwd(lib, [(chains[m], states[m][l], t0) for m, l, c, t0, t1 in grp], B, tlen, H, dev)
+                _launch_fwd(lib, [(chains[m], states[m][l], t0) for m, l, c, t0, t1 in grp], B, tlen, H, dev, pool)
             for tlen, grp in bg:
                 n = tlen * B
                 ln1, ff, ln2 = [], [], []
@@ -367,6 +387,7 @@ class _EncoderStackFn(Function):
             rdiag.append(probs)
         del diags
 
+        pool = _RingPool(sum(len(p) for p in rdiag), lib.mrg_lstm_bwd_xbuf_bytes(B, H) // 8, dev)
         for probs in rdiag:
             bg = _bgroups(probs)
             for tlen, grp in bg:   # LN2, FeedForward, LN1 backward of the chunks (batched launches)
@@ -402,7 +423,7 @@ class _EncoderStackFn(Function):
                     (ch, states[m][l], grads[m][l], t0, dh_in, dc_in, dh_out, dc_out))
             for tlen, grp in items.items():
                 for part in _split(grp, _maxp(B, dev)):
-                    _launch_bwd(lib, part, B, tlen, H, dev)
+                    _launch_bwd(lib, part, B, tlen, H, dev, pool)
             for tlen, grp in bg:   # input gradients of the chunks: dG W_ih + g1 (residual), batched
                 items = []
                 for m, l, c, t0, t1 in grp:

@@ -33,46 +33,80 @@ F32 = 4
 _ERR = {}
 _CNT = {}
 
-# --- optional live kernel timing (bench.py): HIP events recorded on the launch stream
+# --- optional live kernel timing (bench.py).  Default: HIP events recorded on the launch stream
+# around each library call.  kernel=True: the library times every kernel of a tagged call with
+# kernel-bound events (mrg_probe_*, hipExtLaunchKernelGGL), i.e. the kernels' own execution as
+# rocprofv3 reports it, without the packet dispatch a stream event pair also holds.
 _PROBE_ON = set()
 _PROBES = {}
+_NATIVE = [False]
+_CALLS = []          # native mode: (name, work) per tagged library call
+_PROBE_CAP = 1 << 15
 
 
 class _probe:
     """Bracket one library launch with timing events when ``name`` is being probed.
 
     ``work``: the launch's algorithmic FLOPs (or bytes), kept with its time for rooflines."""
-    __slots__ = ("name", "e0", "work")
+    __slots__ = ("name", "e0", "work", "tagged")
 
     def __init__(self, name, work=0.0):
         self.name = name
         self.e0 = None
         self.work = work
+        self.tagged = False
 
     def __enter__(self):
         if self.name in _PROBE_ON:
-            self.e0 = torch.cuda.Event(enable_timing=True)
-            self.e0.record()
+            if _NATIVE[0]:
+                _lib.load().mrg_probe_tag(len(_CALLS))
+                _CALLS.append((self.name, self.work))
+                self.tagged = True
+            else:
+                self.e0 = torch.cuda.Event(enable_timing=True)
+                self.e0.record()
         return self
 
     def __exit__(self, *exc):
-        if self.e0 is not None:
+        if self.tagged:
+            _lib.load().mrg_probe_tag(-1)
+        elif self.e0 is not None:
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record()
             _PROBES.setdefault(self.name, []).append((self.e0, e1, self.work))
         return False
 
 
-def probe_start(*names):
+def probe_start(*names, kernel=False):
     _PROBE_ON.clear()
     _PROBE_ON.update(names)
     _PROBES.clear()
+    _CALLS.clear()
+    _NATIVE[0] = bool(kernel)
+    if kernel:
+        _lib.check(_lib.load().mrg_probe_start(_PROBE_CAP), "probe start")
 
 
 def probe_stop(with_work=False):
-    """Stop probing; returns {name: [ms per launch]} or, with_work, {name: [(ms, work)]} (synchronises)."""
+    """Stop probing; returns {name: [ms per launch]} or, with_work, {name: [(ms, work)]} (synchronises).
+    In kernel mode a launch's ms is the sum of its kernels' own execution times."""
     _PROBE_ON.clear()
     torch.cuda.synchronize()
+    if _NATIVE[0]:
+        _NATIVE[0] = False
+        ms = (ctypes.c_float * _PROBE_CAP)()
+        tags = (ctypes.c_int * _PROBE_CAP)()
+        n = _lib.load().mrg_probe_stop(ms, tags, _PROBE_CAP)
+        if n < 0:
+            raise RuntimeError(f"probe stop: {_lib.load().mrg_last_error().decode()}")
+        per_call = [0.0] * len(_CALLS)
+        for i in range(n):
+            per_call[tags[i]] += ms[i]
+        out = {}
+        for (name, work), t in zip(_CALLS, per_call):
+            out.setdefault(name, []).append((t, work) if with_work else t)
+        _CALLS.clear()
+        return out
     if with_work:
         out = {k: [(a.elapsed_time(b), w) for a, b, w in v] for k, v in _PROBES.items()}
     else:
@@ -886,6 +920,9 @@ class _LSTMFn(Function):
     @_keeps_precision
     def forward(ctx, spec, *tensors):
         nprob, concat, reverse, force_bs, eps = spec
+        # unused outputs (hT, cT of the stateless mixers) get no gradient: None, not a
+        # zero-filled tensor (the recurrence takes null dhT / dcT as zero)
+        ctx.set_materialize_grads(False)
         resln = eps is not None  # per problem LN(y + x) (ResidualConnection around LSTMMixer)
         K = 9 if resln else 7
         probs = [tensors[K * i:K * i + K] for i in range(nprob)]
@@ -1507,8 +1544,25 @@ def mha_residual_layernorm(q, kv, in_proj_weight, in_proj_bias, out_weight, out_
 
 
 def padding_flags(x: torch.Tensor, padding_value: float = -100.0) -> torch.Tensor:
-    """uint8 [B, T]: frame is padding (x[:, :, 0] == -100), as gen_attention_mask tests it."""
-    return (x[:, :, 0] == padding_value).to(torch.uint8).contiguous()
+    """uint8 [B, T]: frame is padding (x[:, :, 0] == -100), as gen_attention_mask tests it
+    (one library kernel on the device; torch on the host, e.g. for the CPU mask goldens)."""
+    if not (x.is_cuda and x.dtype == torch.float32 and x.dim() == 3):
+        return (x[:, :, 0] == padding_value).to(torch.uint8).contiguous()
+    B, T, _ = x.shape
+    out = torch.empty(B, T, dtype=torch.uint8, device=x.device)
+    _lib.check(_lib.load().mrg_padding_flags(B, T, _ptr(x), x.stride(0), x.stride(1), float(padding_value), _ptr(out),
+                                             _stream()), "padding flags")
+    return out
+
+
+def zero_padding(x: torch.Tensor, padding_value: float = -100.0) -> torch.Tensor:
+    """x * (x != -100) (training_step's zeroing of padded motion_self frames, lstmformer.py:365-366)."""
+    if not (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and x.data_ptr() % 16 == 0):
+        return x * (x != padding_value).to(x.dtype)
+    y = torch.empty_like(x)
+    _lib.check(_lib.load().mrg_zero_padding(x.numel(), _ptr(x), float(padding_value), _ptr(y), _stream()),
+               "zero padding")
+    return y
 
 
 # ------------------------------------------------------------------ loss

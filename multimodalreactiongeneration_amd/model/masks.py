@@ -52,6 +52,7 @@ def gen_attention_mask(main_modal: torch.Tensor, other_modal: torch.Tensor, head
     if tk % tq != 0 and tq % tk != 0:
         raise ValueError(f"other_modal_len must be divisible by main_modal_len. "
                          f"main_modal_len: {tq}, other_modal_len: {tk}")
-    mp = (main_modal[:, :, 0] == padding_value).to(torch.uint8).contiguous()
-    op = (other_modal[:, :, 0] == padding_value).to(torch.uint8).contiguous()
+    from .. import functional as Fn
+    mp = Fn.padding_flags(main_modal, padding_value)
+    op = mp if other_modal is main_modal else Fn.padding_flags(other_modal, padding_value)
     return BlockCausalMask(mp, op, head_num)

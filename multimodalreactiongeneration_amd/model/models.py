@@ -261,7 +261,7 @@ class Metaformer(LightningSurface):
             lead = batch[4][0].shape[1]
             target = batch[-1][0]
             ms = batch[2][0].to(self.device)
-            batch[2] = (ms * (ms != PADDING_VALUE).to(ms.dtype), batch[2][1])
+            batch[2] = (Fn.zero_padding(ms, PADDING_VALUE), batch[2][1])
             y, _ = self.forward(*batch[:-1])
             loss = self._masked_loss(y, target, lead)
         self.log("train_loss", loss, prog_bar=True, logger=True)

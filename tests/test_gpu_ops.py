@@ -1044,3 +1044,28 @@ def test_recurrence_behind_cu_occupying_kernel_does_not_time_out(lds):
     torch.cuda.synchronize()
     Fn.check_errors()
     assert torch.equal(y, ref)
+
+
+def test_kernel_bound_probe_times_the_kernels():
+    """functional.probe_start(kernel=True) (mrg_probe_*: hipExtLaunchKernelGGL events bound to each
+    kernel) reports every launch of a probed call, no more than the stream-event bracket of the same
+    call and most of it for a large GEMM; untagged launches are not timed."""
+    from multimodalreactiongeneration_amd import functional as Fn
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(19200, 256, generator=g).to(DEV)
+    w = torch.randn(1024, 256, generator=g).to(DEV) / 16
+    b = torch.zeros(1024, device=DEV)
+    Fn.linear(x, w, b)
+    torch.cuda.synchronize()
+    res = {}
+    for kernel in (False, True):
+        Fn.probe_start("gemm", kernel=kernel)
+        for _ in range(5):
+            Fn.linear(x, w, b)
+        Fn.residual_layernorm(x, x, torch.ones(256, device=DEV), torch.zeros(256, device=DEV))  # not probed
+        res[kernel] = Fn.probe_stop(with_work=True)["gemm"]
+    assert len(res[True]) == len(res[False]) == 5
+    for (tk, wk), (te, we) in zip(res[True], res[False]):
+        assert wk == we == 2.0 * 19200 * 1024 * 256
+        assert 0.0 < tk <= te * 1.02
+    assert sum(t for t, _ in res[True]) >= 0.5 * sum(t for t, _ in res[False])
