@@ -337,7 +337,8 @@ def set_wgrad_stream(on: bool) -> bool:
     return prev
 
 
-# Deferred weight gradients (MRG_WGRAD_DEFER=1; off by default: measured neutral): a side-stream product is not issued
+# Deferred weight gradients (on by default, MRG_WGRAD_DEFER=0 turns it off; neutral in round 2, -0.34 ms/step
+# with round 3's encoder wavefront, whose MFMA recurrences leave room on every CU): a side-stream product is not issued
 # when its operands are ready but queued until the backward reaches its next persistent recurrence
 # (_LSTMFn.backward calls flush_beside_recurrence right before mrg_lstm_bwd), then issued on the
 # side stream with the GEMM grids capped at one block per CU while the recurrence runs at one
@@ -347,7 +348,7 @@ def set_wgrad_stream(on: bool) -> bool:
 # side-stream order, so the writes into each gradient buffer keep their order; a write issued on the
 # current stream (fewer than _SIDE_MIN_ROWS rows) first flushes the queue.  Not used while a
 # gradient-ready listener (DDP bucket overlap) needs each write issued when it is reported.
-_DEFER = [os.environ.get("MRG_WGRAD_DEFER", "0") == "1"]
+_DEFER = [os.environ.get("MRG_WGRAD_DEFER", "1") == "1"]
 _PENDING = {}
 
 
