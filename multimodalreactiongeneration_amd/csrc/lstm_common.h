@@ -157,6 +157,64 @@ __device__ __forceinline__ void get_granules_idx(unsigned long long* base, const
   for (int i = 0; i < N; ++i) out[i] = __uint_as_float((unsigned)v[i]);
 }
 
+// Pair granules (the MFMA form, lstm_mx.hip): one 8-byte word carries TWO fp32 values, each with a
+// 2-bit step tag in its two lowest mantissa bits ((step + 1) & 3; a ring slot is rewritten every
+// second step, so the stale tag differs by 2).  Half the bytes of {tag, value} granules for the
+// gathers that bound the MFMA form's step; a published value is off by at most 3 ulp (2^-21.4
+// relative), far inside the fp32-class error of the x6 products it feeds.  A slot is fresh when both
+// halves carry the tag (the word is written and read as one 64-bit access, single-copy atomic).
+__device__ __forceinline__ unsigned long long make_pair(unsigned tag2, float v0, float v1) {
+  const unsigned a = (__float_as_uint(v0) & ~3u) | tag2, b = (__float_as_uint(v1) & ~3u) | tag2;
+  return ((unsigned long long)b << 32) | (unsigned long long)a;
+}
+__device__ __forceinline__ void put_pair(unsigned long long* g, unsigned tag2, float v0, float v1, int local) {
+  if (local) __hip_atomic_store(g, make_pair(tag2, v0, v1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  else __hip_atomic_store(g, make_pair(tag2, v0, v1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool pair_fresh(unsigned long long v, unsigned tag2) {
+  return (((unsigned)v & 3u) == tag2) && (((unsigned)(v >> 32) & 3u) == tag2);
+}
+// Poll N pair granules at base + idx[i] (all loads in flight, then only the stale ones again).
+template <int N>
+__device__ __forceinline__ void get_pairs_idx(unsigned long long* base, const int (&idx)[N], unsigned tag2,
+                                              float (&v0)[N], float (&v1)[N], int* err, bool& dead) {
+  unsigned long long v[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = __hip_atomic_load(base + idx[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned spins = 0;
+  while (!dead) {
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < N; ++i) ok &= pair_fresh(v[i], tag2);
+    if (ok) break;
+    if (++spins > SPIN_LIMIT) {
+      atomicOr(err, 1);
+      dead = true;
+      break;
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      if (!pair_fresh(v[i], tag2)) v[i] = __hip_atomic_load(base + idx[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    v0[i] = __uint_as_float((unsigned)v[i]);
+    v1[i] = __uint_as_float((unsigned)(v[i] >> 32));
+  }
+}
+// N pair granules at base + i * stride; returns half `hi` (0: low value, 1: high value) of each.
+template <int N>
+__device__ __forceinline__ void get_pair_halves(unsigned long long* base, long stride, int hi, unsigned tag2,
+                                                float (&out)[N], int* err, bool& dead) {
+  int idx[N];
+  float a[N], b[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) idx[i] = (int)(i * stride);
+  get_pairs_idx<N>(base, idx, tag2, a, b, err, dead);
+#pragma unroll
+  for (int i = 0; i < N; ++i) out[i] = hi ? b[i] : a[i];
+}
+
 // Local hand-offs are used only where every member of a group verified, at launch start, that it
 // runs on the same XCD as the others: each member publishes its HW_REG_XCC_ID with an agent-scope
 // store into the ring slot `slots[member]` (parity-1 slots, first written with step data at step
@@ -170,14 +228,18 @@ __device__ __forceinline__ int group_on_one_xcd(unsigned long long* slots, int m
                                                 int* flag) {
   unsigned xcc;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  // the id travels shifted left by 2: its low half's 2-bit tag is 0, so a pair-granule reader
+  // (pair_fresh, the MFMA form's ring) never takes this word for step data (the high half,
+  // XCC_TAG, carries tag 2); 32-bit-tag readers never match XCC_TAG
+  const unsigned code = xcc << 2;
   if (threadIdx.x == 0) {
-    __hip_atomic_store(slots + member, make_granule(XCC_TAG, __uint_as_float(xcc)), __ATOMIC_RELAXED,
+    __hip_atomic_store(slots + member, make_granule(XCC_TAG, __uint_as_float(code)), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
     float ids[G];
     get_granules<G>(slots, 1, XCC_TAG, ids, err, dead);
     int same = 1;
 #pragma unroll
-    for (int m = 0; m < G; ++m) same &= __float_as_uint(ids[m]) == xcc;
+    for (int m = 0; m < G; ++m) same &= __float_as_uint(ids[m]) == code;
     *flag = same;
   }
   __syncthreads();

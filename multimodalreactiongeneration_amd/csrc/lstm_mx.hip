@@ -91,7 +91,7 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_fwd_mx_kernel(LstmFwdArgs args)
     if (P.c0) c = P.c0[(long)bg * P.c0_bs + hcol];
   }
   // h lands in LDS as three bf16 planes (x6 split), one 32-bit word = the pair (k, k + 1) of a row
-  auto put_pair = [&](int b, int k, float v0, float v1) {
+  auto put_planes = [&](int b, int k, float v0, float v1) {
     unsigned p0, p1, p2;
     split2(v0, v1, p0, p1, p2);
     hp[0][b][k >> 1] = p0; hp[1][b][k >> 1] = p1; hp[2][b][k >> 1] = p2;
@@ -99,7 +99,8 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_fwd_mx_kernel(LstmFwdArgs args)
   for (int e = 2 * tid; e < BS * H; e += 2 * MX_NT) {
     const int b = e / H, k = e % H;
     const bool ok = P.h0 && b0 + b < B;
-    put_pair(b, k, ok ? P.h0[(long)(b0 + b) * P.h0_bs + k] : 0.0f, ok ? P.h0[(long)(b0 + b) * P.h0_bs + k + 1] : 0.0f);
+    put_planes(b, k, ok ? P.h0[(long)(b0 + b) * P.h0_bs + k] : 0.0f,
+               ok ? P.h0[(long)(b0 + b) * P.h0_bs + k + 1] : 0.0f);
   }
   auto load_gx = [&](int t) {
     if (cvalid) {
@@ -110,10 +111,12 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_fwd_mx_kernel(LstmFwdArgs args)
   };
   load_gx(P.reverse ? T - 1 : 0);
   __syncthreads();
+  // ring: [parity][B][H / 2] pair granules (units 2p, 2p + 1 of a row)
   unsigned long long* xb = P.xbuf;
-  const int local = args.local ? group_on_one_xcd<G>(xb + ((long)B + b0) * H, j, args.err, dead, &xcc_flag) : 0;
+  constexpr int HP = H / 2;
+  const int local = args.local ? group_on_one_xcd<G>(xb + ((long)B + b0) * HP, j, args.err, dead, &xcc_flag) : 0;
   const int ar = lane & 15, ak = 8 * (lane >> 4);
-  const int nvalid = min(BS, B - b0) * H;
+  const int nvalidp = min(BS, B - b0) * HP;
 
   for (int tt = 0; tt < T; ++tt) {
     const int t = P.reverse ? T - 1 - tt : tt;
@@ -134,15 +137,22 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_fwd_mx_kernel(LstmFwdArgs args)
     MRG_STAMP(2);
     // 2. gates + cell, 3. publish, store, prefetch
     const int par = tt & 1;
+    float ig = 0.0f, fg = 0.0f, gg = 0.0f, og = 0.0f;
     if (cvalid) {
       const float zi = pre[cb][0 * U + cu] + gxv[0] + bh[0];
       const float zf = pre[cb][1 * U + cu] + gxv[1] + bh[1];
       const float zg = pre[cb][2 * U + cu] + gxv[2] + bh[2];
       const float zo = pre[cb][3 * U + cu] + gxv[3] + bh[3];
-      const float ig = sigmoidf_(zi), fg = sigmoidf_(zf), gg = tanhf_(zg), og = sigmoidf_(zo);
+      ig = sigmoidf_(zi); fg = sigmoidf_(zf); gg = tanhf_(zg); og = sigmoidf_(zo);
       c = fg * c + ig * gg;
       h = og * tanhf_(c);
-      put_granule(xb + ((long)par * B + bg) * H + hcol, (unsigned)(tt + 1), h, local);
+    }
+    {  // publish h of units (cu, cu + 1) from the even lane of each pair (lanes l, l ^ 1 hold cu, cu ^ 1)
+      const float hn = dpp_f<0xB1>(h);
+      if (cvalid && (cu & 1) == 0)
+        put_pair(xb + ((long)par * B + bg) * HP + (hcol >> 1), (unsigned)(tt + 1) & 3u, h, hn, local);
+    }
+    if (cvalid) {
       P.y[(long)bg * P.y_bs + (long)t * P.y_ts + hcol] = h;
       float* gs = P.gates + (long)bg * P.g_bs + (long)t * P.g_ts + hcol;
       gs[0] = ig; gs[H] = fg; gs[2 * H] = gg; gs[3 * H] = og;
@@ -150,20 +160,20 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_fwd_mx_kernel(LstmFwdArgs args)
       if (tt + 1 < T) load_gx(P.reverse ? t - 1 : t + 1);
     }
     MRG_STAMP(3);
-    // 4. gather h_t of the group (BS x H granules, 8 per thread)
+    // 4. gather h_t of the group (BS x H / 2 pair granules, 4 per thread)
     if (tt + 1 < T) {
-      constexpr int NG = BS * H / MX_NT;  // 8 granules: pairs (k, k + 1) at 4 rows
-      unsigned long long* rb = xb + ((long)par * B + b0) * H;
-      float gv[NG];
+      constexpr int NG = BS * HP / MX_NT;  // 4 pair granules: units (k, k + 1) at 4 rows
+      unsigned long long* rb = xb + ((long)par * B + b0) * HP;
+      float g0[NG], g1[NG];
       int idx[NG];
 #pragma unroll
-      for (int i = 0; i < NG; ++i) idx[i] = min(2 * tid + (i & 1) + 2 * MX_NT * (i >> 1), nvalid - 1);
-      get_granules_idx<NG>(rb, idx, (unsigned)(tt + 1), gv, args.err, dead);
+      for (int i = 0; i < NG; ++i) idx[i] = min(tid + MX_NT * i, nvalidp - 1);
+      get_pairs_idx<NG>(rb, idx, (unsigned)(tt + 1) & 3u, g0, g1, args.err, dead);
 #pragma unroll
-      for (int m = 0; m < NG / 2; ++m) {
-        const int e = 2 * tid + 2 * MX_NT * m, b = e / H, k = e % H;
+      for (int m = 0; m < NG; ++m) {
+        const int e = tid + MX_NT * m, b = e / HP, k = 2 * (e % HP);
         const bool ok = b0 + b < B;
-        put_pair(b, k, ok ? gv[2 * m] : 0.0f, ok ? gv[2 * m + 1] : 0.0f);
+        put_planes(b, k, ok ? g0[m] : 0.0f, ok ? g1[m] : 0.0f);
       }
     }
     MRG_STAMP(4);
@@ -236,7 +246,7 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_bwd_mx_kernel(LstmBwdArgs args)
   io_load(1);
   __syncthreads();
   unsigned long long* xb = P.xbuf;
-  const long xstride_b = (long)G * H;  // per batch row: [dest G][src G][U]
+  const long xstride_b = (long)G * H / 2;  // per batch row: [dest G][src G][U / 2] pair granules
   const int local = args.local ? group_on_one_xcd<G>(xb + ((long)B + b0) * xstride_b, j, args.err, dead, &xcc_flag)
                                : 0;
   const int ar = lane & 15, ak = 8 * (lane >> 4);
@@ -247,9 +257,9 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_bwd_mx_kernel(LstmBwdArgs args)
     if (cvalid) {
       if (tt > 0) {
         const int par = (tt - 1) & 1;
-        unsigned long long* g = xb + ((long)par * B + bg) * xstride_b + (long)j * H + cu;
+        unsigned long long* g = xb + ((long)par * B + bg) * xstride_b + (long)j * (H / 2) + (cu >> 1);
         float gv[G];
-        get_granules<G>(g, U, (unsigned)tt, gv, args.err, dead);
+        get_pair_halves<G>(g, U / 2, cu & 1, (unsigned)tt & 3u, gv, args.err, dead);
         float s = 0.0f;
 #pragma unroll
         for (int src = 0; src < G; ++src) s += gv[src];
@@ -300,15 +310,16 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_bwd_mx_kernel(LstmBwdArgs args)
       }
       MRG_STAMP(4);
 #pragma unroll
-      for (int ct = 0; ct < 2; ++ct) {
+      for (int ct = 0; ct < 2; ++ct) {  // pairs (n, n + 1) from the even lane (lanes l, l ^ 1 hold n, n ^ 1)
         const int n = 16 * (2 * wave + ct) + ar;
         const int dest = n / U, du = n % U;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int b = 4 * (lane >> 4) + i;
-          if (b0 + b < B)
-            put_granule(xb + ((long)par * B + b0 + b) * xstride_b + (long)dest * H + (long)j * U + du,
-                        (unsigned)(tt + 1), acc[ct][i], local);
+          const float vn = dpp_f<0xB1>(acc[ct][i]);
+          if (b0 + b < B && (ar & 1) == 0)
+            put_pair(xb + ((long)par * B + b0 + b) * xstride_b + (long)dest * (H / 2) + (long)j * (U / 2) + (du >> 1),
+                     (unsigned)(tt + 1) & 3u, acc[ct][i], vn, local);
         }
       }
     }
@@ -326,9 +337,9 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_bwd_mx_kernel(LstmBwdArgs args)
   if (cvalid) {
     if (P.dh0) {
       const int par = (T - 1) & 1;
-      unsigned long long* g = xb + ((long)par * B + bg) * xstride_b + (long)j * H + cu;
+      unsigned long long* g = xb + ((long)par * B + bg) * xstride_b + (long)j * (H / 2) + (cu >> 1);
       float gv[G];
-      get_granules<G>(g, U, (unsigned)T, gv, args.err, dead);
+      get_pair_halves<G>(g, U / 2, cu & 1, (unsigned)T & 3u, gv, args.err, dead);
       float s = 0.0f;
 #pragma unroll
       for (int src = 0; src < G; ++src) s += gv[src];
