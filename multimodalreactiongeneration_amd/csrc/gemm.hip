@@ -709,6 +709,20 @@ static int resident_blocks(K kernel) {
   return per_cu * cus[dev];
 }
 
+// CU count of the current device (cached per device)
+static int resident_cus() {
+  static int cus[16] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 16) dev = 0;
+  if (cus[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1) n = 256;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
 template <int BM, int BN, int BK>
 static void launch_tile(GemmArgs a, int ta, int tb, bool va, bool vb, int splits, hipStream_t s) {
   a.tiles_n = (a.N + BN - 1) / BN;
@@ -1114,7 +1128,8 @@ static int gemm_ex(int mode, int M, int N, int K, float alpha,
                   (K % 32) == 0 && (M % 4) == 0 && (N % 4) == 0 && M >= 64 && N >= 64 && !a.cnt;
   if (wg) {
     tile = 0;
-    launch_x6g_wgrad(a, splits, 128, 128, stream, mode == 2 ? 1 : 3);
+    launch_x6g_wgrad(a, splits, 128, 128, stream, mode == 2 ? 1 : 3,
+                     g_blocks_per_cu > 0 ? g_blocks_per_cu * resident_cus() : 0);
   } else if (launch_gemm(mode, a, tile, bk, transA, transB, va, vb, splits, stream)) {
     return 2;
   }

@@ -142,7 +142,8 @@ struct GemmBatch {
 void launch_x6g(GemmArgs a, int ns, int bm, int bn, hipStream_t s, int planes = 3, const GemmBatch* gb = nullptr);
 // its weight-gradient form (transA = 1, transB = 0, K % 32 == 0, M and N multiples of 4): split-K
 // slabs in a.ws (splits > 1) and the fused row sums of A in a.asum, as gemm_x6_kernel leaves them
-void launch_x6g_wgrad(GemmArgs a, int splits, int bm, int bn, hipStream_t s, int planes = 3);
+// max_grid > 0: at most that many workgroups (a multiple of 8), walking the items
+void launch_x6g_wgrad(GemmArgs a, int splits, int bm, int bn, hipStream_t s, int planes = 3, int max_grid = 0);
 
 static constexpr int MRG_TP_MAX = 32;
 struct TransposeBatch {

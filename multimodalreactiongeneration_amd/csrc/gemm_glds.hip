@@ -318,20 +318,17 @@ __device__ __forceinline__ int wg_off(int k, int c) {  // byte offset of chunk c
   return k * X * 4 + ((c ^ (((k >> 3) & 1) << 3)) << 4);
 }
 
-template <int BM, int BN, int NS, int NP = 3>
-__global__ __launch_bounds__(NT, 1) void gemm_x6g_wgrad_kernel(GemmArgs a) {
+// one (tile, K slice) of the weight-gradient product; lds = the kernel's ring
+template <int BM, int BN, int NS, int NP>
+__device__ __forceinline__ void wgrad_tile(const GemmArgs& a, int t, unsigned char* lds) {
   constexpr int TM = BM / 64, TN = BN / 64;
   constexpr int SA = 32 * BM * 4, SS = SA + 32 * BN * 4;
   constexpr int GA = SA / 4096, GB = (32 * BN * 4) / 4096;  // 1-KB DMA instructions per wave per k-tile
   constexpr int GT = GA + GB;
   constexpr int RA = 1024 / (BM * 4), RB = 1024 / (BN * 4);  // k-rows per DMA instruction
-  static_assert(NS >= 2 && NS <= 4 && (BM == 64 || BM == 128) && (BN == 64 || BN == 128), "wgrad tile");
-  __shared__ __attribute__((aligned(16))) unsigned char lds[NS * SS];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = (wave >> 1) * (BM / 2), wn = (wave & 1) * (BN / 2);
   const int lr = lane & 31, lh = lane >> 5;
-  const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   const int z = t / a.tiles_mn, tr = t - z * a.tiles_mn;
   const int m0 = (tr / a.tiles_n) * BM, n0 = (tr % a.tiles_n) * BN;
   const int kbeg = z * a.kchunk, kend = min(a.K, kbeg + a.kchunk);
@@ -475,13 +472,33 @@ __global__ __launch_bounds__(NT, 1) void gemm_x6g_wgrad_kernel(GemmArgs a) {
   }
 }
 
-void launch_x6g_wgrad(GemmArgs a, int splits, int bm, int bn, hipStream_t s, int planes) {
+// Weight-gradient kernel: (tile, K slice) work items t < a.ntiles; grid = ntiles, or fewer blocks
+// that walk the items in strides of the grid (a capped grid: one block per CU beside a recurrence,
+// mrg_gemm_set_blocks_per_cu).  XCD-aware bijective item order either way (a multiple-of-8 grid keeps
+// a block on one XCD's items).
+template <int BM, int BN, int NS, int NP = 3>
+__global__ __launch_bounds__(NT, 1) void gemm_x6g_wgrad_kernel(GemmArgs a) {
+  constexpr int SS = 32 * BM * 4 + 32 * BN * 4;
+  static_assert(NS >= 2 && NS <= 4 && (BM == 64 || BM == 128) && (BN == 64 || BN == 128), "wgrad tile");
+  __shared__ __attribute__((aligned(16))) unsigned char lds[NS * SS];
+  const int total = a.ntiles, q8 = total >> 3, r8 = total & 7;
+  for (int vb = blockIdx.x; vb < total; vb += gridDim.x) {
+    const int xcd = vb & 7;
+    const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (vb >> 3);
+    wgrad_tile<BM, BN, NS, NP>(a, t, lds);
+    __syncthreads();  // the ring / epilogue stage is reused by the next item
+  }
+}
+
+void launch_x6g_wgrad(GemmArgs a, int splits, int bm, int bn, hipStream_t s, int planes, int max_grid) {
   auto go = [&](auto kern, int BM_, int BN_) {
     a.tiles_n = (a.N + BN_ - 1) / BN_;
     a.tiles_mn = a.tiles_n * ((a.M + BM_ - 1) / BM_);
     a.ntiles = a.tiles_mn * splits;
     a.nsplit = splits;
-    klaunch(kern, (unsigned)a.ntiles, NT, 0, s, a);
+    unsigned grid = (unsigned)a.ntiles;
+    if (max_grid > 0 && grid > (unsigned)max_grid) grid = (unsigned)max_grid & ~7u ? (unsigned)max_grid & ~7u : 8u;
+    klaunch(kern, grid, NT, 0, s, a);
   };
   if (planes == 1) go(gemm_x6g_wgrad_kernel<128, 128, 2, 1>, 128, 128);
   else if (bm == 64 && bn == 64) go(gemm_x6g_wgrad_kernel<64, 64, 2>, 64, 64);

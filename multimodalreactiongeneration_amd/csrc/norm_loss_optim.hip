@@ -296,22 +296,29 @@ __global__ __launch_bounds__(256) void resln_bwd_v4_batched_kernel(LnBatch lb, i
 
 // dgamma / dbeta: sum the per-block partials part[nblk][2][E]; one lane per column,
 // 16 waves interleave over the blocks, then combine in LDS (fixed order -> deterministic)
-__global__ __launch_bounds__(1024) void resln_param_reduce_kernel(const float* part, int nblk, int E, float* dgamma,
-                                                                  float* dbeta, int accumulate) {
-  __shared__ float red[16][64];
+__global__ __launch_bounds__(256) void resln_param_reduce_kernel(const float* part, int nblk, int E, float* dgamma,
+                                                                 float* dbeta, int accumulate) {
+  // 4 waves (one per SIMD, ~65 VGPRs): small enough to sit beside a persistent recurrence when it
+  // runs as a deferred parameter-gradient product (a 1024-lane block waited for the recurrence to end)
+  __shared__ float red[4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
-  float s = 0.0f;
+  float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
   if (c < 2 * E) {
-#pragma unroll 16  // 16 loads in flight per wave: the 8-block grid is latency-bound
-    for (int i = wave; i < nblk; i += 16) s += part[(long)i * 2 * E + c];
+    int i = wave;
+#pragma unroll 4  // 16 loads in flight per wave: the 8-block grid is latency-bound
+    for (; i + 12 < nblk; i += 16) {
+      s0 += part[(long)i * 2 * E + c];
+      s1 += part[(long)(i + 4) * 2 * E + c];
+      s2 += part[(long)(i + 8) * 2 * E + c];
+      s3 += part[(long)(i + 12) * 2 * E + c];
+    }
+    for (; i < nblk; i += 4) s0 += part[(long)i * 2 * E + c];
   }
-  red[wave][lane] = s;
+  red[wave][lane] = (s0 + s1) + (s2 + s3);
   __syncthreads();
   if (wave == 0 && c < 2 * E) {
-    float v = 0.0f;
-#pragma unroll
-    for (int w = 0; w < 16; ++w) v += red[w][lane];
+    const float v = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
     float* out = c < E ? dgamma + c : dbeta + (c - E);
     *out = accumulate ? *out + v : v;
   }
@@ -683,7 +690,7 @@ MRG_API int mrg_residual_layernorm_param_reduce(int rows, int E, const float* wo
   MRG_REQUIRE(E >= 1 && E <= 1024 && dgamma && dbeta && workspace,
               "mrg_residual_layernorm_param_reduce: bad arguments (E=%d)", E);
   const int nblk = (rows + RESLN_RPB - 1) / RESLN_RPB;
-  resln_param_reduce_kernel<<<(2 * E + 63) / 64, 1024, 0, stream>>>(workspace, nblk, E, dgamma, dbeta,
+  resln_param_reduce_kernel<<<(2 * E + 63) / 64, 256, 0, stream>>>(workspace, nblk, E, dgamma, dbeta,
                                                                    accumulate);
   return check_launch("resln_param_reduce_kernel");
 }
