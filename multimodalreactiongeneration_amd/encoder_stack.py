@@ -143,13 +143,15 @@ def _launch_bwd(lib, items, B, Tc, H, dev, pool=None):
         rev.append(0)
     A = lambda ct, v: (ct * n)(*v)  # noqa: E731
     # deferred weight gradients (functional._DEFER) run beside this recurrence, as in _LSTMFn.backward
-    lib.mrg_lstm_set_blocks_per_cu(Fn.flush_beside_recurrence(dev))
+    cap, mark = Fn.fork_beside_recurrence(dev)
+    lib.mrg_lstm_set_blocks_per_cu(cap)
     with Fn._probe("lstm_bwd", 8.0 * H * H * B * Tc * n):
         rc = lib.mrg_lstm_bwd(n, B, Tc, H, A(VP, whh), A(VP, gates), A(VP, cs), A(VP, c0), A(VP, dy),
                               A(CL, dybs), A(CL, dyts), A(VP, dhT), A(VP, dcT), A(VP, dG), A(VP, dh0), A(VP, dc0),
                               A(CI, rev), A(VP, [_p(xb[i]) for i in range(n)]), (CL * (8 * n))(*lay),
                               _ptr(Fn._err_flag(dev)), _lib.cu_count(dev.index or 0), 0, _stream())
     _lib.check(rc, "lstm bwd (encoder stack)")
+    Fn.flush_beside_recurrence(dev, mark)
 
 
 _BMAX = 16   # problems per batched GEMM / LayerNorm launch (mrg_gemm_x6g_batched, mrg_residual_layernorm_*_batched)

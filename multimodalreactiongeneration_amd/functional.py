@@ -340,7 +340,8 @@ def set_wgrad_stream(on: bool) -> bool:
 # Deferred weight gradients (on by default, MRG_WGRAD_DEFER=0 turns it off; neutral in round 2, -0.34 ms/step
 # with round 3's encoder wavefront, whose MFMA recurrences leave room on every CU): a side-stream product is not issued
 # when its operands are ready but queued until the backward reaches its next persistent recurrence
-# (_LSTMFn.backward calls flush_beside_recurrence right before mrg_lstm_bwd), then issued on the
+# (_LSTMFn.backward marks the current stream right before mrg_lstm_bwd and issues the queue right
+# after it, ordered after the mark only: fork_beside_recurrence / flush_beside_recurrence), on the
 # side stream with the GEMM grids capped at one block per CU while the recurrence runs at one
 # workgroup per CU (mrg_lstm_set_blocks_per_cu): the latency-bound recurrence leaves most of each
 # CU idle, and the dW products fill it instead of running beside the dX chain's GEMMs (which
@@ -375,16 +376,20 @@ def _defers(device, rows) -> bool:
             and torch._C._current_graph_task_id() >= 0)
 
 
-def _flush_deferred(key, device, cap=0):
+def _flush_deferred(key, device, cap=0, after=None):
     """Issue the queued weight-gradient products on the side stream (GEMM grids capped at `cap`
-    blocks per CU while they run beside a recurrence)."""
+    blocks per CU while they run beside a recurrence), ordered after event `after` when given, else
+    after the current stream's work so far."""
     items = _PENDING.pop(key, None)
     if not items:
         return
     dev = torch.device(device)
     cur = torch.cuda.current_stream(dev)
     s = _SIDE[key]
-    s.wait_stream(cur)
+    if after is None:
+        s.wait_stream(cur)
+    else:
+        s.wait_event(after)
     lib = _lib.load()
     prev = lib.mrg_gemm_set_blocks_per_cu(cap) if cap else None
     try:
@@ -404,14 +409,27 @@ def _flush_deferred(key, device, cap=0):
             lib.mrg_gemm_set_blocks_per_cu(prev)
 
 
-def flush_beside_recurrence(device) -> int:
-    """Called right before a backward recurrence launch: issues the queued weight-gradient products so
-    they run beside it; returns the recurrence's workgroups-per-CU cap (1 when deferring, else 0)."""
+def fork_beside_recurrence(device):
+    """Called right before a backward recurrence launch: returns (the recurrence's workgroups-per-CU
+    cap: 1 when deferring, else 0; a fork mark for flush_beside_recurrence, or None)."""
     if not (_WGRAD_SIDE[0] and _DEFER[0] and _GRAD_LISTENER[0] is None):
-        return 0
-    key = torch.device(device).index or 0
-    _flush_deferred(key, device, cap=1)
-    return 1
+        return 0, None
+    dev = torch.device(device)
+    if not _PENDING.get(dev.index or 0):
+        return 1, None
+    mark = torch.cuda.Event()
+    mark.record(torch.cuda.current_stream(dev))
+    return 1, mark
+
+
+def flush_beside_recurrence(device, mark) -> None:
+    """Called right after the recurrence launch: issues the queued weight-gradient products on the side
+    stream, ordered after `mark` (the work before the recurrence) but not after the recurrence.  Issued
+    after it so the recurrence's workgroups are dispatched first (a HIP graph launches its nodes in
+    capture order) and the capped weight-gradient grids fill the CUs' remaining slots around them."""
+    if mark is None:
+        return
+    _flush_deferred(torch.device(device).index or 0, device, cap=1, after=mark)
 
 
 def _on_side(device, rows, keep, fn):
@@ -1059,7 +1077,8 @@ class _LSTMFn(Function):
         def arr(ctype, vals):
             return (ctype * nprob)(*vals)
         VP = ctypes.c_void_p
-        lib.mrg_lstm_set_blocks_per_cu(flush_beside_recurrence(dev))
+        cap, mark = fork_beside_recurrence(dev)
+        lib.mrg_lstm_set_blocks_per_cu(cap)
         pr = _probe("lstm_bwd", 8.0 * H * H * B * T * nprob).__enter__()  # dG W_hh FLOPs
         rc = lib.mrg_lstm_bwd(
             nprob, B, T, H,
@@ -1073,6 +1092,7 @@ class _LSTMFn(Function):
             _lib.cu_count(dev.index or 0), force_bs, _stream())
         pr.__exit__()
         _lib.check(rc, "lstm bwd")
+        flush_beside_recurrence(dev, mark)
 
         out = [None]
         dx_first = None
