@@ -282,6 +282,12 @@ def act_splits(M, N, K):
 
 
 _WG_TARGET = int(os.environ.get("MRG_WGRAD_TARGET_WG", "512"))  # workgroups a weight-gradient product aims at
+# ... while it runs beside a recurrence with its grid capped at one block per CU (_flush_deferred):
+# fewer split-K slices measured faster there (tools/tools_wgrad_sweep.py, capped grid: LSTM dW 1024 x 256
+# 102 -> 98 us at 16 instead of 32 slices, 256 x 256 41 -> 36 us at 64 instead of 128, 512 x 256
+# 62 -> 55 us at 32 instead of 64), and the slab reduce reads half the slabs
+_WG_TARGET_BESIDE = int(os.environ.get("MRG_WGRAD_TARGET_WG_BESIDE", "256"))
+_BESIDE = [False]
 
 
 def wgrad_splits(M, N, K):
@@ -292,7 +298,7 @@ def wgrad_splits(M, N, K):
     """
     if _lib.load().mrg_gemm_get_mode() == 1 or _ARITH[0] == "bf16":
         tiles = ((M + 127) // 128) * ((N + 127) // 128)
-        s = max(1, _WG_TARGET // max(1, tiles))
+        s = max(1, (_WG_TARGET_BESIDE if _BESIDE[0] else _WG_TARGET) // max(1, tiles))
         return int(max(1, min(s, K // 128, 128)))
     tiles = ((M + 63) // 64) * ((N + 63) // 64)
     s = max(1, 512 // max(1, tiles))
@@ -392,6 +398,7 @@ def _flush_deferred(key, device, cap=0, after=None):
         s.wait_event(after)
     lib = _lib.load()
     prev = lib.mrg_gemm_set_blocks_per_cu(cap) if cap else None
+    _BESIDE[0] = bool(cap)
     try:
         with torch.cuda.stream(s):
             for fn, keep, arith in items:
@@ -405,6 +412,7 @@ def _flush_deferred(key, device, cap=0, after=None):
                 finally:
                     _ARITH[0] = old
     finally:
+        _BESIDE[0] = False
         if cap:
             lib.mrg_gemm_set_blocks_per_cu(prev)
 
