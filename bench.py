@@ -508,10 +508,12 @@ def main():
     reducer = GradReducer(opt.flat_grad, comm=comm)
     batch = make_batch(B=args.batch, T=args.seq, ratio=args.ratio, seed=1234 + rank, device=dev)
 
+    one = torch.ones((), device=dev)   # d loss / d loss, made once (backward() would fill a new one per step)
+
     def fwd_bwd():
         opt.zero_grad()
         loss = model.training_step(list(batch))["loss"]
-        loss.backward()
+        loss.backward(one)
         return loss
 
     def step():

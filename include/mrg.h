@@ -357,6 +357,10 @@ int mrg_residual_layernorm_bwd_batched(int n, int rows, int E, const float* cons
 int mrg_padding_flags(int B, int T, const float* x, long bs, long ts, float value, unsigned char* out,
                       hipStream_t stream);
 int mrg_zero_padding(long n, const float* x, float value, float* y, hipStream_t stream);
+/* bytes of zeros at p (any alignment): the training step's buffer clears (gradient buffer, hand-off
+ * rings, loss-gradient lead frames) without a torch fill kernel.  Replaces the `zero_grad` /
+ * `torch.zeros` of the reference's step (lstmformer.py:313-322 loss, Lightning's optimizer zero_grad). */
+int mrg_fill_zero(void* p, long bytes, hipStream_t stream);
 
 /* ---------------------------------------------------------------- loss
  * Masked regression loss of training_step (lstmformer.py:372-380,

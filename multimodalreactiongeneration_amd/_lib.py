@@ -105,6 +105,7 @@ SIGNATURES = {
     "mrg_debug_busy": (c_int, [c_int, c_int, c_int, ctypes.c_double, P]),
     "mrg_padding_flags": (c_int, [c_int, c_int, P, c_long, c_long, c_float, P, P]),
     "mrg_zero_padding": (c_int, [c_long, P, c_float, P, P]),
+    "mrg_fill_zero": (c_int, [P, c_long, P]),
     "mrg_probe_start": (c_int, [c_int]),
     "mrg_probe_tag": (c_int, [c_int]),
     "mrg_probe_stop": (c_int, [ctypes.POINTER(ctypes.c_float), PI, c_int]),

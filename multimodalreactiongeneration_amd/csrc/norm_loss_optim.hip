@@ -845,6 +845,36 @@ MRG_API int mrg_padding_flags(int B, int T, const float* x, long bs, long ts, fl
   return check_launch("padding_flags_kernel");
 }
 
+namespace mrg {
+
+// bytes of zeros at p (16-B stores over the aligned body, byte stores at the ends): the step's
+// buffer clears (gradient buffer, hand-off rings, loss-gradient lead frames) as a library kernel
+__global__ __launch_bounds__(256) void fill_zero_kernel(unsigned char* p, long head, long nv, long bytes) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride)
+    reinterpret_cast<float4*>(p + head)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  const long tail0 = head + nv * 16;
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < head) p[t] = 0;
+  if (t < bytes - tail0) p[tail0 + t] = 0;
+}
+
+}  // namespace mrg
+
+MRG_API int mrg_fill_zero(void* p, long bytes, hipStream_t stream) {
+  MRG_REQUIRE(bytes >= 0 && (bytes == 0 || p), "mrg_fill_zero: bad arguments");
+  if (bytes == 0) return 0;
+  unsigned char* b = reinterpret_cast<unsigned char*>(p);
+  long head = (16 - (long)((uintptr_t)b & 15)) & 15;
+  if (head > bytes) head = bytes;
+  const long nv = (bytes - head) / 16;
+  long blocks = (nv + 255) / 256;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 2048) blocks = 2048;
+  klaunch(mrg::fill_zero_kernel, (unsigned)blocks, 256, 0, stream, b, head, nv, bytes);
+  return check_launch("fill_zero_kernel");
+}
+
 MRG_API int mrg_zero_padding(long n, const float* x, float value, float* y, hipStream_t stream) {
   if (n == 0) return 0;
   MRG_REQUIRE((((uintptr_t)x | (uintptr_t)y) & 15) == 0, "mrg_zero_padding: 16-byte aligned buffers required");

@@ -88,7 +88,7 @@ class _RingPool:
     needs its rings zero at its start; a fill per launch was one more kernel on the critical path)."""
 
     def __init__(self, n, elems, dev):
-        self.buf = torch.zeros(max(1, n), elems, dtype=torch.int64, device=dev)
+        self.buf = Fn.zeros(max(1, n), elems, dtype=torch.int64, device=dev)
         self.next = 0
 
     def take(self, n):
@@ -103,7 +103,7 @@ def _launch_fwd(lib, items, B, Tc, H, dev, pool=None):
     """One persistent forward launch over `items` = [(chain, layer state dict, t0)]."""
     n = len(items)
     xb = pool.take(n) if pool is not None else \
-        torch.zeros(n, lib.mrg_lstm_fwd_xbuf_bytes(B, H) // 8, dtype=torch.int64, device=dev)
+        Fn.zeros(n, lib.mrg_lstm_fwd_xbuf_bytes(B, H) // 8, dtype=torch.int64, device=dev)
     gx, gbs, gts, whh, bhh, h0, c0, y, ybs, yts, gates, cs, lay, rev = ([] for _ in range(14))
     for ch, st, t0 in items:
         r0 = t0 * B
@@ -129,7 +129,7 @@ def _launch_bwd(lib, items, B, Tc, H, dev, pool=None):
     """One persistent backward launch over `items` = [(chain, state, grads, t0, dhT, dcT, dh0, dc0)]."""
     n = len(items)
     xb = pool.take(n) if pool is not None else \
-        torch.zeros(n, lib.mrg_lstm_bwd_xbuf_bytes(B, H) // 8, dtype=torch.int64, device=dev)
+        Fn.zeros(n, lib.mrg_lstm_bwd_xbuf_bytes(B, H) // 8, dtype=torch.int64, device=dev)
     whh, gates, cs, c0, dy, dybs, dyts, dhT, dcT, dG, dh0, dc0, lay, rev = ([] for _ in range(14))
     for ch, st, gr, t0, dh_in, dc_in, dh_out, dc_out in items:
         r0 = t0 * B
@@ -368,7 +368,7 @@ class _EncoderStackFn(Function):
             grads.append(gl)
             if douts[m] is None:
                 douts = list(douts)
-                douts[m] = torch.zeros(B, T, H, **f32)
+                douts[m] = Fn.zeros(B, T, H, **f32)
         douts = [d.contiguous() for d in douts]
 
         def block_off(T, c):

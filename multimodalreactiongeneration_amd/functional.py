@@ -281,24 +281,25 @@ def act_splits(M, N, K):
     return int(max(1, min(4, K // 64, 128 // tiles)))
 
 
-_WG_TARGET = int(os.environ.get("MRG_WGRAD_TARGET_WG", "512"))  # workgroups a weight-gradient product aims at
-# ... while it runs beside a recurrence with its grid capped at one block per CU (_flush_deferred):
-# fewer split-K slices measured faster there (tools/tools_wgrad_sweep.py, capped grid: LSTM dW 1024 x 256
-# 102 -> 98 us at 16 instead of 32 slices, 256 x 256 41 -> 36 us at 64 instead of 128, 512 x 256
-# 62 -> 55 us at 32 instead of 64), and the slab reduce reads half the slabs
-_WG_TARGET_BESIDE = int(os.environ.get("MRG_WGRAD_TARGET_WG_BESIDE", "256"))
-_BESIDE = [False]
+# Workgroups a weight-gradient product aims at.  256 (half the split-K slices of round 2's 512): most
+# products run beside a recurrence with the grid capped at one block per CU (_DEFER), where fewer
+# slices measured faster (tools/tools_wgrad_sweep.py, capped grid: LSTM dW 1024 x 256 102 -> 98 us at
+# 16 instead of 32 slices, 256 x 256 41 -> 36 us at 64 instead of 128, 512 x 256 62 -> 55 us at 32
+# instead of 64) and the slab reduce reads half the slabs: 22.93 -> 22.48 ms/step on one box (128:
+# 23.7).  One target for every schedule, so the split (and the summation order) depends on the shape
+# only and the side-stream / deferred schedules stay bitwise equal to the single-stream one.
+_WG_TARGET = int(os.environ.get("MRG_WGRAD_TARGET_WG", "256"))
 
 
 def wgrad_splits(M, N, K):
     """split-K factor for weight-gradient GEMMs (small M x N output, long B*T reduction).
 
-    About 512 workgroups: 128x128 tiles under the x6 arithmetic (chunks of >= 128 rows),
+    About _WG_TARGET workgroups: 128x128 tiles under the x6 arithmetic (chunks of >= 128 rows),
     64x64 tiles under exact f32 (chunks of >= 256 rows); tools/tools_gemm_sweep.py measured both.
     """
     if _lib.load().mrg_gemm_get_mode() == 1 or _ARITH[0] == "bf16":
         tiles = ((M + 127) // 128) * ((N + 127) // 128)
-        s = max(1, (_WG_TARGET_BESIDE if _BESIDE[0] else _WG_TARGET) // max(1, tiles))
+        s = max(1, _WG_TARGET // max(1, tiles))
         return int(max(1, min(s, K // 128, 128)))
     tiles = ((M + 63) // 64) * ((N + 63) // 64)
     s = max(1, 512 // max(1, tiles))
@@ -398,7 +399,6 @@ def _flush_deferred(key, device, cap=0, after=None):
         s.wait_event(after)
     lib = _lib.load()
     prev = lib.mrg_gemm_set_blocks_per_cu(cap) if cap else None
-    _BESIDE[0] = bool(cap)
     try:
         with torch.cuda.stream(s):
             for fn, keep, arith in items:
@@ -412,7 +412,6 @@ def _flush_deferred(key, device, cap=0, after=None):
                 finally:
                     _ARITH[0] = old
     finally:
-        _BESIDE[0] = False
         if cap:
             lib.mrg_gemm_set_blocks_per_cu(prev)
 
@@ -990,7 +989,7 @@ class _LSTMFn(Function):
         hT = [torch.empty(B, H, device=dev, dtype=torch.float32) for _ in range(nprob)]
         cT = [torch.empty(B, H, device=dev, dtype=torch.float32) for _ in range(nprob)]
         xb_elems = lib.mrg_lstm_fwd_xbuf_bytes(B, H) // 8
-        xbuf = torch.zeros(nprob, xb_elems, dtype=torch.int64, device=dev)
+        xbuf = zeros(nprob, xb_elems, dtype=torch.int64, device=dev)
         h0 = [None if p[5] is None else p[5].contiguous() for p in probs]
         c0 = [None if p[6] is None else p[6].contiguous() for p in probs]
 
@@ -1083,7 +1082,7 @@ class _LSTMFn(Function):
         dc0 = [torch.empty(B, H, device=dev, dtype=torch.float32)
                if ctx.has_c0[i] and need[1 + K * i + 6] else None for i in range(nprob)]
         xb_elems = lib.mrg_lstm_bwd_xbuf_bytes(B, H) // 8
-        xbuf = torch.zeros(nprob, xb_elems, dtype=torch.int64, device=dev)
+        xbuf = zeros(nprob, xb_elems, dtype=torch.int64, device=dev)
 
         def arr(ctype, vals):
             return (ctype * nprob)(*vals)
@@ -1597,6 +1596,20 @@ def zero_padding(x: torch.Tensor, padding_value: float = -100.0) -> torch.Tensor
     return y
 
 
+def zero_(t: torch.Tensor) -> torch.Tensor:
+    """In-place zero of a contiguous device tensor on the current stream (mrg_fill_zero)."""
+    if t.numel():
+        if not (t.is_cuda and t.is_contiguous()):
+            raise ValueError("functional.zero_: contiguous device tensor required")
+        _lib.check(_lib.load().mrg_fill_zero(_ptr(t), t.numel() * t.element_size(), _stream()), "fill zero")
+    return t
+
+
+def zeros(*shape, dtype=torch.float32, device=None) -> torch.Tensor:
+    """torch.zeros through the library's fill kernel (no at::native kernel in the replayed step)."""
+    return zero_(torch.empty(*shape, dtype=dtype, device=device))
+
+
 # ------------------------------------------------------------------ loss
 _LOSS_TYPES = {"huber": 0, "mse": 1, "mae": 2, "smoothl1": 3}
 
@@ -1625,7 +1638,7 @@ class _LossFn(Function):
         y, target = ctx.saved_tensors
         B, Ttot, F = y.shape
         T = target.shape[1]
-        dy = torch.zeros_like(y)
+        dy = zeros(y.shape, dtype=y.dtype, device=y.device)
         go = gout.reshape(1).contiguous()
         _lib.check(_lib.load().mrg_masked_loss_bwd(B, T, F, _ptr(y, ctx.lead * F), Ttot * F, _ptr(target),
                                                    *ctx.spec, _ptr(go), _ptr(dy, ctx.lead * F), _stream()),

@@ -123,4 +123,8 @@ class FusedAdamW(torch.optim.Optimizer):
 
     def zero_grad(self, set_to_none: bool = False):
         # gradients stay views of the flat buffer (set_to_none would detach them from it)
-        self.flat_grad.zero_()
+        if self.flat_grad.is_cuda:
+            from . import functional as Fn
+            Fn.zero_(self.flat_grad)
+        else:
+            self.flat_grad.zero_()

@@ -1069,3 +1069,20 @@ def test_kernel_bound_probe_times_the_kernels():
         assert wk == we == 2.0 * 19200 * 1024 * 256
         assert 0.0 < tk <= te * 1.02
     assert sum(t for t, _ in res[True]) >= 0.5 * sum(t for t, _ in res[False])
+
+
+def test_fill_zero_any_alignment_and_size():
+    """mrg_fill_zero clears exactly [p, p + bytes) at every byte alignment (16-B body, byte ends)."""
+    from multimodalreactiongeneration_amd import _lib as L
+    from multimodalreactiongeneration_amd import functional as Fn
+    lib = L.load()
+    buf = torch.empty(70000, dtype=torch.uint8, device=DEV)
+    for off in (0, 1, 3, 8, 15, 16, 17):
+        for n in (0, 1, 5, 15, 16, 17, 31, 33, 4096, 65537):
+            buf.fill_(0xAB)
+            L.check(lib.mrg_fill_zero(Fn._ptr(buf, off), n, Fn._stream()), "fill")
+            host = buf.cpu()
+            assert int(host[off:off + n].sum()) == 0, (off, n)
+            assert bool((host[:off] == 0xAB).all()) and bool((host[off + n:] == 0xAB).all()), (off, n)
+    z = Fn.zeros(3, 5, dtype=torch.int64, device=DEV)
+    assert z.dtype == torch.int64 and int(z.abs().sum()) == 0
