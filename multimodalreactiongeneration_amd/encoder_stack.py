@@ -41,8 +41,10 @@ from . import _lib
 from . import functional as Fn
 from .functional import _ptr, _stream, gemm, _dx_gemm, _wt_note, _gbuf, _on_side
 
-# time steps per chunk (the diagonal width); MRG_STACK_CHUNK overrides
-CHUNK = int(os.environ.get("MRG_STACK_CHUNK", "60"))
+# time steps per chunk (the diagonal width); MRG_STACK_CHUNK overrides.  100 since the deferred weight
+# gradients run beside the backward recurrences (longer recurrences leave them more room): A/B on one
+# box 50 / 60 / 75 / 100 / 150 / 300 -> 21.80 / 21.68 / 21.53 / 21.29 / 21.55 / 23.05 ms/step (r03)
+CHUNK = int(os.environ.get("MRG_STACK_CHUNK", "100"))
 # problems per recurrence launch (lstm.hip: <= 12); 0 = as many as the MFMA form's grid keeps resident
 # (8 workgroups of 16 rows per problem, one per CU: 8 problems at B = 64 on 256 CUs; a wider launch
 # falls back to the VALU form at batch tiles of 16, measured 3x slower per step)
