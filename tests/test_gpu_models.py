@@ -425,7 +425,8 @@ def test_simple_lstm_bf16_gate_vs_fp32_oracle():
             assert torch.nn.functional.cosine_similarity(g, r, dim=0) >= 0.99, k
 
 
-@pytest.mark.parametrize("chunk,ratio,B,T", [(60, 1, 64, 300), (7, 2, 6, 40), (300, 1, 8, 50)])
+@pytest.mark.parametrize("chunk,ratio,B,T", [(100, 1, 64, 300), (60, 1, 16, 300), (100, 1, 16, 250), (7, 2, 6, 40),
+                                             (300, 1, 8, 50)])
 def test_encoder_stack_matches_per_layer_schedule(chunk, ratio, B, T):
     """Block 0's embedding stacks as a (layer, time chunk) wavefront (encoder_stack.py) vs the
     per-layer schedule: same loss, output and every parameter gradient (fp32 reorderings only:
