@@ -99,9 +99,14 @@ def progress(msg):
     print(f"[bench {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (= ranks) of this node; without torch.distributed.run's env, N > 1 makes this "
+                         "process the launcher of N ranks; under it, N must equal WORLD_SIZE (default: WORLD_SIZE or 1)")
+    ap.add_argument("--dry-run", type=int, default=0,
+                    help="1 = exercise the launch / rendezvous / barrier / max-over-ranks timing / JSON on the CPU "
+                         "(gloo, a flat-buffer all-reduce as the step), no GPU")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=64)
@@ -121,7 +126,125 @@ def parse():
     ap.add_argument("--comm", default="torch", choices=["torch", "native"],
                     help="N>1 gradient all-reduce: torch.distributed (RCCL) or libmrg's mrg_comm_* RCCL communicator")
     ap.add_argument("--lstm-group", type=int, default=0, help="workgroups per LSTM row group at H=256 (8|16; 0 = library default)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_or_check(args, argv=None):
+    """Make ``--gpus N`` mean N ranks (the reference trains with Lightning DDP on every listed GPU,
+    mr_gen/model/lstmformer/config.yaml:121,127).
+
+    * Under torch.distributed.run (WORLD_SIZE set): N must equal WORLD_SIZE, else exit 2.
+    * Without it and N > 1: this process becomes the launcher.  It makes no HIP call (the device count
+      comes from torch.cuda.device_count(), which does not initialise the runtime on this image), exits 2
+      when fewer than N GPUs are visible, and otherwise starts ``torch.distributed.run --nproc-per-node N``
+      on this same script as a CHILD process (never exec) and exits with its return code.
+    Returns None when this process should run the benchmark itself."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if args.gpus is None:
+            args.gpus = int(env_world)
+        if int(env_world) != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but torch.distributed.run started WORLD_SIZE={env_world} ranks; "
+                  "pass the same N to both", file=sys.stderr, flush=True)
+            sys.exit(2)
+        return None
+    if args.gpus is None:
+        args.gpus = 1
+    if args.gpus <= 1:
+        return None
+    if not args.dry_run:
+        visible = torch.cuda.device_count()
+        if visible < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} asks for {args.gpus} ranks (one per GPU) but only {visible} "
+                  "GPU(s) are visible; refusing to time fewer GPUs than asked", file=sys.stderr, flush=True)
+            sys.exit(2)
+    import subprocess
+    argv = sys.argv[1:] if argv is None else argv
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    progress(f"launching {args.gpus} ranks: {' '.join(cmd[1:6])} ...")
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "4")
+    rc = subprocess.call(cmd, env=env)
+    if rc != 0:
+        print(f"bench.py: torch.distributed.run exited {rc}", file=sys.stderr, flush=True)
+    sys.exit(rc)
+
+
+def ranks_seen(rank, world, dev):
+    """Every rank's (rank, local rank, device) as RCCL / gloo initialised them, gathered to all ranks;
+    raises when two ranks share one GPU (the timing would then not be of N GPUs)."""
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if dev is not None and dev.type == "cuda":
+        p = torch.cuda.get_device_properties(dev)
+        ident = str(getattr(p, "uuid", "")) or f"{p.name}:{dev.index}"
+    else:
+        ident = f"cpu:{local}"
+    mine = {"rank": rank, "local_rank": local, "device": ident, "host": os.uname().nodename}
+    if world <= 1:
+        return {"world_size": 1, "backend": None, "ranks": [mine]}
+    allr = [None] * world
+    dist.all_gather_object(allr, mine)
+    devs = {(r["host"], r["device"]) for r in allr}
+    if dev is not None and dev.type == "cuda" and len(devs) != world:
+        raise RuntimeError(f"bench.py: {world} ranks but only {len(devs)} distinct GPUs: {allr}")
+    return {"world_size": dist.get_world_size(), "backend": dist.get_backend(), "distinct_devices": len(devs),
+            "ranks": allr}
+
+
+def timed_region(run, steps, world, dev):
+    """K steps bracketed by barrier + synchronize on both sides; the MAX elapsed over ranks (seconds)."""
+    cuda = dev is not None and dev.type == "cuda"
+    if world > 1:
+        dist.barrier()
+    if cuda:
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        run()
+    if cuda:
+        torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if cuda else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    return elapsed
+
+
+def dry_run(args):
+    """--dry-run: the launch, rendezvous, barrier / max-over-ranks timing and the JSON line of the real
+    benchmark on the CPU (gloo), with one all-reduce of a flat buffer the size of the benchmark model's
+    gradients (13,052,678 fp32) as the "step".  Used by tests/test_bench_launch.py."""
+    from multimodalreactiongeneration_amd.ddp import init_from_env
+    rank, world = init_from_env(backend="gloo")
+    seen = ranks_seen(rank, world, None)
+    buf = torch.full((13_052_678,), float(rank + 1))
+
+    def run():
+        if world > 1:
+            dist.all_reduce(buf)
+            buf.mul_(1.0 / world)
+    for _ in range(args.warmup):
+        run()
+    elapsed = timed_region(run, args.steps, world, None)
+    ok = bool(torch.allclose(buf[:4], torch.full((4,), (world + 1) / 2.0)))
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "frames/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(1000.0 * elapsed / max(1, args.steps), 3), "dry_run": True,
+                          "allreduce_mean_ok": ok, "ranks_seen": seen}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def model_flops_per_frame(cfg, ratio):
@@ -483,6 +606,9 @@ def secondary(args, dev):
 
 def main():
     args = parse()
+    launch_or_check(args)          # N > 1 without torch.distributed.run: launches N ranks and exits
+    if args.dry_run:
+        return dry_run(args)
     from multimodalreactiongeneration_amd import configs as C
     from multimodalreactiongeneration_amd import functional as Fn
     from multimodalreactiongeneration_amd.graphs import capture
@@ -494,6 +620,9 @@ def main():
     torch.cuda.set_device(local)    # before the process group, so RCCL binds rank -> its own GPU
     rank, world = init_from_env()
     dev = torch.device("cuda", local)
+    seen = ranks_seen(rank, world, dev)
+    if world != args.gpus:
+        raise RuntimeError(f"bench.py: --gpus {args.gpus} but {world} ranks initialised")
     mc, oc, me = C.lstmformer_config(ratio=args.ratio)
     if args.lstm_group:
         from multimodalreactiongeneration_amd import _lib
@@ -542,20 +671,7 @@ def main():
     torch.cuda.synchronize()
     Fn.check_errors()
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        run()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+    elapsed = timed_region(run, args.steps, world, dev)
     Fn.check_errors()
     ms = 1000.0 * elapsed / args.steps
     frames = args.batch * args.seq * world
@@ -596,6 +712,7 @@ def main():
         "roofline": roof,
         "kernels": kernels,
         "cpu_baseline": None,
+        "ranks_seen": {k: v for k, v in seen.items() if k != "ranks"} | {"devices": [r["device"] for r in seen["ranks"]]},
     }
     if rank == 0:
         progress(f"headline {ms:.3f} ms/step")

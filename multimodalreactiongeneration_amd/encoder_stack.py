@@ -44,6 +44,9 @@ from .functional import _ptr, _stream, gemm, _dx_gemm, _wt_note, _gbuf, _on_side
 # time steps per chunk (the diagonal width); MRG_STACK_CHUNK overrides.  100 since the deferred weight
 # gradients run beside the backward recurrences (longer recurrences leave them more room): A/B on one
 # box 50 / 60 / 75 / 100 / 150 / 300 -> 21.80 / 21.68 / 21.53 / 21.29 / 21.55 / 23.05 ms/step (r03)
+# one side-stream fork per weight-gradient product instead of one per layer (a capture regression case:
+# tests/test_gpu_capture.py)
+SPLIT_FORKS = os.environ.get("MRG_STACK_SPLIT_FORKS", "0") == "1"
 CHUNK = int(os.environ.get("MRG_STACK_CHUNK", "100"))
 # problems per recurrence launch (lstm.hip: <= 12); 0 = as many as the MFMA form's grid keeps resident
 # (8 workgroups of 16 rows per problem, one per CU: 8 problems at B = 64 on 256 CUs; a wider launch
@@ -464,21 +467,31 @@ class _EncoderStackFn(Function):
                  b_div=kw.get("x_div", 0), splits=Fn.wgrad_splits(Nout, Nin, n), device=dev,
                  asum_out=_ptr(kw.get("gb")), asum_out2=_ptr(kw.get("gb2")))
 
+        def ln_reduce(ws, gg, gb):
+            scratch = Fn._ws(2 * H * 4, dev).view(2, H) if (gg is None or gb is None) else None
+            _lib.check(lib.mrg_residual_layernorm_param_reduce(
+                gr["nblk"] * 32, H, _ptr(ws), _ptr(gg if gg is not None else scratch[0]),
+                _ptr(gb if gb is not None else scratch[1]), 1, _stream()), "layernorm param reduce")
+
+        parts = [lambda: wg(_ptr(dG), 4 * H, _ptr(st["x"]), H, rows, 4 * H, H, gw_ih, gb=first,
+                            gb2=gbh if gbi is not None else None)]
+        if gw_hh is not None and T > 1:   # sum_t dG_t^T y_{t-1}: time-major rows shifted by one step
+            parts.append(lambda: wg(_p(dG, B * 4 * H), 4 * H, _ptr(st["y"]), H, (T - 1) * B, 4 * H, H, gw_hh))
+        parts.append(lambda: wg(_ptr(g2), H, _ptr(st["u"]), H, rows, H, H, gw_ff, gb=gb_ff))
+        for ws, gg, gb in lns:
+            if gg is not None or gb is not None:
+                parts.append(lambda ws=ws, gg=gg, gb=gb: ln_reduce(ws, gg, gb))
+        if l == 0:   # the embedding: dW_emb = sum dx0^T feat (features read time-major through a row map)
+            parts.append(lambda: wg(_ptr(dx0), H, _ptr(ch.feat), T * ch.F, rows, H, ch.F, emb[0], x_hi=ch.F,
+                                    x_div=B, gb=emb[1]))
+        if SPLIT_FORKS:   # one fork per product (the round-3 pattern, kept as a capture regression case)
+            for f in parts:
+                _on_side(dev, rows, keep, f)
+            return
+
         def issue():
-            wg(_ptr(dG), 4 * H, _ptr(st["x"]), H, rows, 4 * H, H, gw_ih, gb=first,
-               gb2=gbh if gbi is not None else None)
-            if gw_hh is not None and T > 1:   # sum_t dG_t^T y_{t-1}: time-major rows shifted by one step
-                wg(_p(dG, B * 4 * H), 4 * H, _ptr(st["y"]), H, (T - 1) * B, 4 * H, H, gw_hh)
-            wg(_ptr(g2), H, _ptr(st["u"]), H, rows, H, H, gw_ff, gb=gb_ff)
-            for ws, gg, gb in lns:
-                if gg is None and gb is None:
-                    continue
-                scratch = Fn._ws(2 * H * 4, dev).view(2, H) if (gg is None or gb is None) else None
-                _lib.check(lib.mrg_residual_layernorm_param_reduce(
-                    gr["nblk"] * 32, H, _ptr(ws), _ptr(gg if gg is not None else scratch[0]),
-                    _ptr(gb if gb is not None else scratch[1]), 1, _stream()), "layernorm param reduce")
-            if l == 0:   # the embedding: dW_emb = sum dx0^T feat (features read time-major through a row map)
-                wg(_ptr(dx0), H, _ptr(ch.feat), T * ch.F, rows, H, ch.F, emb[0], x_hi=ch.F, x_div=B, gb=emb[1])
+            for f in parts:
+                f()
         _on_side(dev, rows, keep, issue)
 
     @staticmethod

@@ -131,13 +131,17 @@ def _ws(nbytes: int, device) -> torch.Tensor:
     return t
 
 
+# MRG_SIDE_HOLD=0 turns the hold off (diagnostic only: tests/test_gpu_capture.py)
+_HOLD_SIDE_SCRATCH = [os.environ.get("MRG_SIDE_HOLD", "1") == "1"]
+
+
 def _hold_if_side(t: torch.Tensor):
     """A scratch tensor allocated on the weight-gradient side stream stays referenced until the
     backward's join (see _ensure_join).  Freed earlier, its block could go to an allocation on the
     main stream while the side-stream kernel that uses it has not run yet: inside a HIP-graph capture
     the private pool does not keep the two streams' blocks apart (measured: the encoder stack's
     replayed gradients were corrupted by split-K slabs reused as main-stream temporaries)."""
-    if not _SIDE:
+    if not (_SIDE and _HOLD_SIDE_SCRATCH[0]):
         return
     dev = t.device.index or 0
     s = _SIDE.get(dev)

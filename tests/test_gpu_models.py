@@ -535,3 +535,139 @@ def test_fused_integrator_matches_module_path(ratio, B, T):
     assert abs(l1.item() - l0.item()) <= 1e-5 * abs(l0.item())
     for k in g0:
         assert rel_err(g1[k], g0[k]) < 1e-5, k
+
+
+# ReLU FeedForward input layers (Linear -> ReLU -> Linear, mixer_block.py FeedForward): a pre-activation
+# within ~1e-7 of 0 can take the other side of the kink under any fp32 summation order, and one row's
+# flip moves a 19,200-row gradient sum by ~1/sqrt(19200) of its scale.  The fp32 CPU oracle itself is
+# 3.8e-4 (weight) / 2.8e-4 (bias) from the float64 answer on block 2's layer at this batch
+# (tests/golden/make_b64_fixture.py), so these two tensors get a kink allowance; every other gradient
+# keeps the north_star's 1e-4.
+RELU_KINK_TOL = 2e-3
+
+
+def _b64_tol(name):
+    return RELU_KINK_TOL if ".feedforward.feed_forward.module.input." in name else TOL
+
+
+def test_benchmark_schedule_b64_vs_oracle():
+    """The benchmarked step exactly as bench.py runs it (B=64, T=300, r=1, bench weights and batch):
+    encoder wavefront with the MFMA recurrences, deferred weight gradients beside the backward
+    recurrences on the side stream, fused integrators, fwd + loss + bwd + AdamW captured as ONE HIP
+    graph and replayed once, vs the oracle's float64 answer for the same inputs
+    (tests/golden/metaformer_b64_f64.npz): loss, every parameter gradient (max|g|, L2 norm and 257
+    sampled entries incl. the argmax) and the post-AdamW parameters at the sampled entries.
+    Reference: lstmformer.py:313-333 (training_step, lossfun, configure_optimizers)."""
+    from multimodalreactiongeneration_amd import configs as C
+    from multimodalreactiongeneration_amd import functional as Fn
+    from multimodalreactiongeneration_amd.graphs import capture
+    from multimodalreactiongeneration_amd.model import Metaformer
+    from multimodalreactiongeneration_amd.synthetic import make_batch
+    d = load("metaformer_b64_f64")
+    mc, oc, me = C.lstmformer_config(ratio=1)
+    torch.manual_seed(0)
+    m = Metaformer(mc, oc, me)
+    assert abs(sum(v.double().sum().item() for v in m.state_dict().values()) - float(d["param_sum"])) < 1e-6, \
+        "torch.manual_seed(0) init differs from the fixture's"
+    m = m.to(DEV)
+    assert Fn.set_wgrad_stream(True) and Fn.set_wgrad_defer(True)   # the defaults bench.py runs with
+    opt = m.configure_optimizers()["optimizer"]
+    batch = make_batch(B=64, T=300, ratio=1, seed=1234, device=DEV)
+    one = torch.ones((), device=DEV)
+    loss_buf = torch.zeros((), device=DEV)
+
+    def step():
+        opt.zero_grad()
+        loss = m.training_step(list(batch))["loss"]
+        loss.backward(one)
+        opt.step()
+        loss_buf.copy_(loss.detach())
+    replay = capture(step, 2, preserve=opt.state_tensors())
+    replay()
+    torch.cuda.synchronize()
+    Fn.check_errors()
+    assert abs(loss_buf.item() - float(d["loss"])) / abs(float(d["loss"])) < TOL
+    worst = []
+    for k, p in m.named_parameters():
+        g = p.grad.detach().reshape(-1).double().cpu()
+        idx = torch.from_numpy(d[f"idx/{k}"])
+        gmax, _, g2 = d[f"stat/{k}"]
+        tol = _b64_tol(k)
+        scale = max(gmax, 1e-30)
+        e_pt = (g[idx] - torch.from_numpy(d[f"g/{k}"])).abs().max().item() / scale
+        e_max = abs(g.abs().max().item() - gmax) / scale
+        e_l2 = abs(g.norm().item() - np.sqrt(g2)) / max(np.sqrt(g2), 1e-30)
+        worst.append((max(e_pt, e_max, e_l2), k))
+        assert e_pt < tol and e_max < tol and e_l2 < tol, (k, e_pt, e_max, e_l2)
+        gref = torch.from_numpy(d[f"g/{k}"])
+        sel = gref.abs() > max(1e-5 * gmax, 1e-6)
+        if sel.any():
+            a = p.detach().reshape(-1).double().cpu()[idx][sel]
+            assert rel_err(a, torch.from_numpy(d[f"after/{k}"])[sel]) < tol, k
+    worst.sort()
+    print("worst gradient errors vs float64:", [(f"{e:.2e}", k) for e, k in worst[-5:]])
+
+
+def test_encoder_stack_mfma_matches_per_layer_valu():
+    """The encoder wavefront with its MFMA recurrences (the benchmarked form: 8 problems x 4 batch
+    tiles x 3 chunks at B = 64) vs the per-layer schedule on the VALU recurrence: same loss and
+    gradients within fp32 reordering."""
+    from multimodalreactiongeneration_amd import _lib
+    from multimodalreactiongeneration_amd import configs as C
+    from multimodalreactiongeneration_amd.model import Metaformer
+    from multimodalreactiongeneration_amd.synthetic import make_batch, clone_batch
+    lib = _lib.load()
+    mc, oc, me = C.lstmformer_config(ratio=1)
+    torch.manual_seed(0)
+    m = Metaformer(mc, oc, me).to(DEV)
+    B, T = 64, 300
+    lengths = [T] * B
+    lengths[-1] = T - 5
+    batch = make_batch(B=B, T=T, lead=3, seed=11, lengths=lengths, device=DEV)
+    out = []
+    prev = lib.mrg_lstm_set_mx(0, 0)
+    try:
+        for use, mx in ((False, 0), (True, 2)):
+            lib.mrg_lstm_set_mx(mx, 0)
+            m.metaformer.use_encoder_stack = use
+            for p in m.parameters():
+                p.grad = None
+            loss = m.training_step(clone_batch(batch, DEV))["loss"]
+            loss.backward()
+            torch.cuda.synchronize()
+            out.append((loss.detach().clone(), {k: p.grad.detach().clone() for k, p in m.named_parameters()}))
+    finally:
+        lib.mrg_lstm_set_mx(prev, 0)
+        m.metaformer.use_encoder_stack = type(m.metaformer).use_encoder_stack
+    (l0, g0), (l1, g1) = out
+    assert abs(l1.item() - l0.item()) <= 1e-5 * abs(l0.item())
+    for k in g0:
+        assert rel_err(g1[k], g0[k]) < _b64_tol(k), k
+
+
+def test_simple_lstm_configs0_shape_vs_oracle():
+    """BASELINE configs[0]'s shape (simple_lstm, T=100, B=4) on the GPU vs the CPU oracle: loss, every
+    gradient and the AdamW step at 1e-4 (simple_lstm.py:146-269)."""
+    from multimodalreactiongeneration_amd import configs as C
+    from multimodalreactiongeneration_amd.model import SimpleLSTM
+    from multimodalreactiongeneration_amd.synthetic import make_simple_batch
+    from oracle import mrg_oracle as O
+    cfg, oc, me = C.simple_lstm_config()
+    torch.manual_seed(0)
+    m = SimpleLSTM(cfg, oc, me)
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.to(DEV)
+    a, mo, t = make_simple_batch(B=4, T=100, seed=1234)
+    opt = m.configure_optimizers()["optimizer"]
+    loss = m.training_step((a.to(DEV), mo.to(DEV), t.to(DEV)))["loss"]
+    loss.backward()
+    opt.step()
+    torch.cuda.synchronize()
+    ref_loss, _, grads, after = O.run_train_step(O.simple_lstm_training_loss, sd, oc, cfg, a, mo, t)
+    assert abs(loss.item() - ref_loss.item()) / abs(ref_loss.item()) < TOL
+    for k, p in m.named_parameters():
+        assert rel_err(p.grad, grads[k]) < TOL, k
+        gref = grads[k]
+        sel = gref.abs() > torch.clamp(1e-5 * gref.abs().max(), min=1e-6)
+        if sel.any():
+            assert rel_err(p.detach().cpu()[sel], after[k][sel]) < TOL, k

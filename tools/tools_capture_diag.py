@@ -1,0 +1,93 @@
+"""Root cause of round 3's wrong replayed gradients with several side-stream forks.
+
+    python tools/tools_capture_diag.py          (GPU box)
+
+1. Allocator probe: inside one capture, a block allocated on the side stream and freed there — is it
+   handed to the next same-size allocation on the MAIN stream (no graph edge between the two users)?
+   Also for a main-stream block used on the side stream with record_stream.
+2. The lstmformer step (B=64, T=300, deferred weight gradients), eager vs graph replay, bitwise, for
+   (one fork per layer | one fork per product) x (side-stream scratch held to the join | not held).
+"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def allocator_probe():
+    dev = torch.device("cuda:0")
+    side = torch.cuda.Stream(device=dev)
+    cap = torch.cuda.Stream(device=dev)
+    g = torch.cuda.CUDAGraph()
+    n = 1 << 20
+    out = {}
+    with torch.cuda.stream(cap):
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, stream=cap):
+            cur = torch.cuda.current_stream()
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                a = torch.empty(n, device=dev)
+                a.fill_(1.0)
+                pa = a.data_ptr()
+                del a
+            b = torch.empty(n, device=dev)         # main stream, same size, no edge to the side fill
+            out["side_block_to_main"] = b.data_ptr() == pa
+            c = torch.empty(n, device=dev)
+            c.fill_(2.0)
+            pc = c.data_ptr()
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                c.record_stream(side)
+                c.add_(1.0)
+            del c
+            d = torch.empty(n, device=dev)
+            out["recorded_main_block_reused"] = d.data_ptr() == pc
+            with torch.cuda.stream(side):
+                e = torch.empty(n, device=dev)
+                out["freed_main_block_to_side"] = e.data_ptr() in (pc, pa)
+            cur.wait_stream(side)
+    return out
+
+
+def step_combo(split, hold):
+    from multimodalreactiongeneration_amd import configs as C
+    from multimodalreactiongeneration_amd import encoder_stack as ES
+    from multimodalreactiongeneration_amd import functional as Fn
+    from multimodalreactiongeneration_amd.graphs import capture
+    from multimodalreactiongeneration_amd.model import Metaformer
+    from multimodalreactiongeneration_amd.synthetic import make_batch
+    ES.SPLIT_FORKS = split
+    Fn._HOLD_SIDE_SCRATCH[0] = hold
+    mc, oc, me = C.lstmformer_config(ratio=1)
+    torch.manual_seed(0)
+    m = Metaformer(mc, oc, me).to("cuda:0")
+    opt = m.configure_optimizers()["optimizer"]
+    batch = make_batch(B=64, T=300, ratio=1, seed=5, device="cuda:0")
+
+    def step():
+        opt.zero_grad()
+        m.training_step(list(batch))["loss"].backward()
+    step()
+    torch.cuda.synchronize()
+    ref = {k: p.grad.clone() for k, p in m.named_parameters()}
+    replay = capture(step, 1)
+    res = []
+    for _ in range(2):
+        opt.flat_grad.fill_(-1.0)
+        replay()
+        torch.cuda.synchronize()
+        bad = [k for k, p in m.named_parameters() if not torch.equal(p.grad, ref[k])]
+        res.append(len(bad))
+    print(f"split_forks={int(split)} hold_side_scratch={int(hold)}: params differing eager/replay per replay {res}"
+          + (f" e.g. {bad[:3]}" if bad else ""), flush=True)
+    del m, opt, replay
+    torch.cuda.synchronize()
+
+
+if __name__ == "__main__":
+    print("allocator probe (inside one capture):", allocator_probe(), flush=True)
+    for split, hold in ((False, True), (True, True), (False, False), (True, False)):
+        step_combo(split, hold)
