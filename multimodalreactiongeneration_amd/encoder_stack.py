@@ -258,7 +258,9 @@ class _EncoderStackFn(Function):
     @staticmethod
     @Fn._keeps_precision
     def forward(ctx, spec, *tensors):
-        nls, tc, eps = spec
+        nls, tc, eps, sinks = spec
+        ctx.sinks = sinks
+        ctx.set_materialize_grads(False)   # a source whose gradient comes through its KVSink gets None
         lib = _lib.load()
         chains, k = [], 0
         for L in nls:
@@ -357,6 +359,11 @@ class _EncoderStackFn(Function):
                 st.update(ctx.params[m][l])
                 sts.append(st)
             states.append(sts)
+        douts = list(douts)
+        for m, sink in enumerate(ctx.sinks):   # the fused integrators' summed key / value gradients
+            g = sink.drain()
+            if g is not None:
+                douts[m] = g if douts[m] is None else douts[m] + g
         grads, carry = [], {}
         wsb = lib.mrg_residual_layernorm_bwd_workspace_bytes
         for m, ch in enumerate(chains):
@@ -514,4 +521,9 @@ def encoder_stack(chains: Sequence[Sequence], eps: float, chunk: int = 0) -> Lis
         for lay in layers:
             flat += list(lay)
         nls.append(len(layers))
-    return list(_EncoderStackFn.apply((tuple(nls), int(chunk or CHUNK), float(eps)), *flat))
+    from .integrate import KVSink
+    sinks = [KVSink() for _ in chains]
+    outs = list(_EncoderStackFn.apply((tuple(nls), int(chunk or CHUNK), float(eps), sinks), *flat))
+    for o, sink in zip(outs, sinks):
+        o._mrg_kv_sink = sink   # consumers (integrate._IntegrateFn) sum their dKV into it; backward drains
+    return outs

@@ -69,25 +69,25 @@ def _bgemm(M, N, K, items, lda, ldc, *, epi=0, ldaux=0, transposed=False, beta=0
     _lib.check(rc, "batched gemm (integrator)")
 
 
-class _KVSink:
+class KVSink:
     """The input gradient of one key / value source shared by several integrators (block 0's encoder
-    outputs, attended by every block, multi_modal_metaformer.py:440-462): each consumer's backward
-    adds dKV_i W_kv_i into ONE buffer in its GEMM epilogue (beta = 1 after the first), and the first
-    consumer of the forward, whose backward runs last (every later block sits downstream of it on the
-    main modality's chain), hands the buffer to autograd; the others return no gradient for it.  So
-    the sum is never formed by autograd's separate adds."""
-    __slots__ = ("consumers", "written", "buf")
+    outputs, attended by every block, multi_modal_metaformer.py:440-462), summed in place: each
+    consumer's backward adds its dKV_i W_kv_i into ONE buffer in its GEMM epilogue (beta = 1 after the
+    first) and returns no gradient for the source; the source's PRODUCER drains the buffer at the start
+    of its own backward (encoder_stack._EncoderStackFn), which autograd runs only after every consumer
+    that received a gradient has run its backward.  So the sum is never formed by autograd's separate
+    adds, and it is right in any consumer order, for several forwards over one source, for a source
+    passed twice to one op and when some consumers' backward never runs.  A source whose producer does
+    not drain (no ``_mrg_kv_sink`` attribute) gets per-consumer gradients that autograd sums."""
+    __slots__ = ("written", "buf")
 
     def __init__(self):
-        self.consumers, self.written, self.buf = 0, 0, None
+        self.written, self.buf = 0, None
 
-
-def _sink_of(kv):
-    sink = getattr(kv, "_mrg_kv_sink", None)
-    if sink is None:
-        sink = _KVSink()
-        kv._mrg_kv_sink = sink
-    return sink
+    def drain(self):
+        buf = self.buf if self.written else None
+        self.written, self.buf = 0, None
+        return buf
 
 
 class _IntegrateFn(Function):
@@ -157,12 +157,7 @@ class _IntegrateFn(Function):
         ctx.params = (P, cat_w, cat_b)
         ctx.spec = (n, heads, causal, scale)
         ctx.kv_need = [ctx.needs_input_grad[2 + i] for i in range(n)]
-        ctx.sinks = []
-        for i in range(n):
-            sink = _sink_of(kvs[i]) if ctx.kv_need[i] else None
-            if sink is not None:
-                sink.consumers += 1
-            ctx.sinks.append((sink, sink.consumers if sink is not None else 0))
+        ctx.sinks = [getattr(kvs[i], "_mrg_kv_sink", None) if ctx.kv_need[i] else None for i in range(n)]
         ctx.q_need = ctx.needs_input_grad[1]
         return out
 
@@ -218,24 +213,22 @@ class _IntegrateFn(Function):
                          beta=0.0 if i == 0 else 1.0, device=dev)
         dkv = []
         for i in range(n):
-            sink, order = ctx.sinks[i]
-            if sink is None:
+            if not ctx.kv_need[i]:
                 dkv.append(None)
                 continue
             Tk = kv2[i].shape[1]
-            if sink.buf is None:
+            sink = ctx.sinks[i]
+            if sink is None:   # no draining producer: this consumer's own part, summed by autograd
+                g = torch.empty(B, Tk, E, **f32)
+                _dx_gemm(B * Tk, E, 2 * E, _ptr(dKV[i]), 2 * E, P[i][0][E:], _ptr(g), E, device=dev)
+                dkv.append(g)
+                continue
+            if sink.written == 0:
                 sink.buf = torch.empty(B, Tk, E, **f32)
             _dx_gemm(B * Tk, E, 2 * E, _ptr(dKV[i]), 2 * E, P[i][0][E:], _ptr(sink.buf), E,
                      beta=0.0 if sink.written == 0 else 1.0, device=dev)
             sink.written += 1
-            if order == 1:   # the first consumer: every other one has added its part by now
-                if sink.written != sink.consumers:
-                    raise RuntimeError("fused integrator: a shared key/value source's consumers ran their "
-                                       f"backward out of order ({sink.written} of {sink.consumers} done)")
-                dkv.append(sink.buf)
-                sink.buf, sink.written = None, 0
-            else:
-                dkv.append(None)
+            dkv.append(None)   # the producer drains the sum (KVSink)
         _IntegrateFn._param_grads(lib, ctx, dev, do2, cat, G2, U, G1, O, dQ, q2, dKV, kv2, ws1, ws2, N, E, n)
         return (None, dq, *dkv) + (None,) * (len(ctx.needs_input_grad) - 2 - n)
 

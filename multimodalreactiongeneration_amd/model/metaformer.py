@@ -335,6 +335,8 @@ class MultiModalMetaformer(nn.Module):
         if not (stack_eligible(H, feats[0].shape[0]) and all(f.dim() == 3 and f.is_cuda and f.shape[1] >= 8
                                                              and f.shape[0] == feats[0].shape[0] for f in feats)):
             return None
+        if any(f.requires_grad for f in feats):   # the stack returns no feature gradient (features are data)
+            return None
         embs = list(self.feature_embedding)
         if any(e.bias is None for e in embs):
             return None
