@@ -44,6 +44,10 @@ from .functional import _ptr, _stream, gemm, _dx_gemm, _wt_note, _gbuf, _on_side
 # time steps per chunk (the diagonal width); MRG_STACK_CHUNK overrides.  100 since the deferred weight
 # gradients run beside the backward recurrences (longer recurrences leave them more room): A/B on one
 # box 50 / 60 / 75 / 100 / 150 / 300 -> 21.80 / 21.68 / 21.53 / 21.29 / 21.55 / 23.05 ms/step (r03)
+# weight gradients per (layer, chunk) as each chunk's backward completes (1), or per layer once its
+# chunk 0 is done (0): the per-chunk form starts the products diagonals earlier, so fewer of them are
+# left for the end of the backward, where no recurrence is left to hide them
+CHUNK_WGRAD = os.environ.get("MRG_STACK_CHUNK_WGRAD", "1") == "1"
 # one side-stream fork per weight-gradient product instead of one per layer (a capture regression case:
 # tests/test_gpu_capture.py)
 SPLIT_FORKS = os.environ.get("MRG_STACK_SPLIT_FORKS", "0") == "1"
@@ -368,7 +372,7 @@ class _EncoderStackFn(Function):
         wsb = lib.mrg_residual_layernorm_bwd_workspace_bytes
         for m, ch in enumerate(chains):
             T, rows = ch.T, ch.T * B
-            nblk = sum((c1 - c0) * B // 32 + ((c1 - c0) * B % 32 > 0) for c0, c1 in _chunks(T, tc))
+            nblk = sum(_ln_blocks(lib, (c1 - c0) * B, H) for c0, c1 in _chunks(T, tc))
             gl = []
             for l in range(ch.L):
                 gl.append(dict(dG=torch.empty(T, B, 4 * H, **f32), g1=torch.empty(T, B, H, **f32),
@@ -384,7 +388,7 @@ class _EncoderStackFn(Function):
         douts = [d.contiguous() for d in douts]
 
         def block_off(T, c):
-            return sum((c1 - c0) * B // 32 + ((c1 - c0) * B % 32 > 0) for c0, c1 in _chunks(T, tc)[:c])
+            return sum(_ln_blocks(lib, (c1 - c0) * B, H) for c0, c1 in _chunks(T, tc)[:c])
 
         diags = _diagonals(chains, tc)
         # backward: diagonals in reverse, within one the chunk index of every chain's top layer first
@@ -446,16 +450,22 @@ class _EncoderStackFn(Function):
                                   _p(gr["g1"], r0 * H)))
                 _bgemm(lib, tlen * B, H, 4 * H, items, 4 * H, H, epi=3, ldaux=H, transposed=True, dev=dev)
             for m, l, c, t0, t1 in probs:
-                if c == 0:
-                    _EncoderStackFn._weight_grads(lib, chains[m], states[m][l], grads[m][l], l, B, H, dev)
+                if CHUNK_WGRAD:   # this chunk's share now: the products start diagonals earlier
+                    _EncoderStackFn._weight_grads(lib, chains[m], states[m][l], grads[m][l], l, B, H, dev,
+                                                  t0, t1, block_off(chains[m].T, c))
+                elif c == 0:
+                    _EncoderStackFn._weight_grads(lib, chains[m], states[m][l], grads[m][l], l, B, H, dev,
+                                                  0, chains[m].T, 0)
         return (None,) + tuple(_EncoderStackFn._input_grads(chains, ctx.needs_input_grad))
 
     @staticmethod
-    def _weight_grads(lib, ch, st, gr, l, B, H, dev):
-        """Every parameter gradient of layer l over the whole sequence (its last chunk is done), issued
-        as ONE fork onto the weight-gradient side stream (functional._side)."""
+    def _weight_grads(lib, ch, st, gr, l, B, H, dev, t0, t1, bo):
+        """Layer l's parameter gradients over time steps [t0, t1) (one chunk, or the whole sequence once
+        its last chunk is done), accumulated into the gradient buffers and issued as ONE fork onto the
+        weight-gradient side stream (functional._side); bo = the chunk's first LayerNorm partial block.
+        Rows are time-major, so a chunk is one contiguous row range."""
         T = ch.T
-        rows = T * B
+        r0, rows = t0 * B, (t1 - t0) * B
         dG, g2, g1, dx0 = gr["dG"], gr["g2"], gr["g1"], gr["dv"]
         gbi, gbh = _gbuf(st["b_ih"]), _gbuf(st["b_hh"])
         first = gbi if gbi is not None else gbh
@@ -463,6 +473,7 @@ class _EncoderStackFn(Function):
         lns = [(gr["ws1"], _gbuf(st["g1"]), _gbuf(st["be1"])), (gr["ws2"], _gbuf(st["g2"]), _gbuf(st["be2"]))]
         emb = (_gbuf(ch.emb_w), _gbuf(ch.emb_b)) if l == 0 else (None, None)
         keep = (dG, g2, g1, dx0, st["x"], st["y"], st["u"], gr["ws1"], gr["ws2"], ch.feat)
+        th = max(t0, 1)   # dW_hh pairs dG_t with y_{t-1}: t >= 1
 
         def wg(dY, ldy, X, ldx, n, Nout, Nin, gw, **kw):
             if gw is None:
@@ -475,22 +486,25 @@ class _EncoderStackFn(Function):
                  asum_out=_ptr(kw.get("gb")), asum_out2=_ptr(kw.get("gb2")))
 
         def ln_reduce(ws, gg, gb):
+            # the chunk's partial blocks start at block bo; rows = the chunk's rows (the reduce derives
+            # the block count from them as the LayerNorm backward did)
             scratch = Fn._ws(2 * H * 4, dev).view(2, H) if (gg is None or gb is None) else None
             _lib.check(lib.mrg_residual_layernorm_param_reduce(
-                gr["nblk"] * 32, H, _ptr(ws), _ptr(gg if gg is not None else scratch[0]),
+                rows, H, _p(ws, bo * 2 * H), _ptr(gg if gg is not None else scratch[0]),
                 _ptr(gb if gb is not None else scratch[1]), 1, _stream()), "layernorm param reduce")
 
-        parts = [lambda: wg(_ptr(dG), 4 * H, _ptr(st["x"]), H, rows, 4 * H, H, gw_ih, gb=first,
+        parts = [lambda: wg(_p(dG, r0 * 4 * H), 4 * H, _p(st["x"], r0 * H), H, rows, 4 * H, H, gw_ih, gb=first,
                             gb2=gbh if gbi is not None else None)]
-        if gw_hh is not None and T > 1:   # sum_t dG_t^T y_{t-1}: time-major rows shifted by one step
-            parts.append(lambda: wg(_p(dG, B * 4 * H), 4 * H, _ptr(st["y"]), H, (T - 1) * B, 4 * H, H, gw_hh))
-        parts.append(lambda: wg(_ptr(g2), H, _ptr(st["u"]), H, rows, H, H, gw_ff, gb=gb_ff))
+        if gw_hh is not None and t1 > th:   # sum_t dG_t^T y_{t-1}: time-major rows shifted by one step
+            parts.append(lambda: wg(_p(dG, th * B * 4 * H), 4 * H, _p(st["y"], (th - 1) * B * H), H, (t1 - th) * B,
+                                    4 * H, H, gw_hh))
+        parts.append(lambda: wg(_p(g2, r0 * H), H, _p(st["u"], r0 * H), H, rows, H, H, gw_ff, gb=gb_ff))
         for ws, gg, gb in lns:
             if gg is not None or gb is not None:
                 parts.append(lambda ws=ws, gg=gg, gb=gb: ln_reduce(ws, gg, gb))
         if l == 0:   # the embedding: dW_emb = sum dx0^T feat (features read time-major through a row map)
-            parts.append(lambda: wg(_ptr(dx0), H, _ptr(ch.feat), T * ch.F, rows, H, ch.F, emb[0], x_hi=ch.F,
-                                    x_div=B, gb=emb[1]))
+            parts.append(lambda: wg(_p(dx0, r0 * H), H, _p(ch.feat, t0 * ch.F), T * ch.F, rows, H, ch.F, emb[0],
+                                    x_hi=ch.F, x_div=B, gb=emb[1]))
         if SPLIT_FORKS:   # one fork per product (the round-3 pattern, kept as a capture regression case)
             for f in parts:
                 _on_side(dev, rows, keep, f)
@@ -505,6 +519,12 @@ class _EncoderStackFn(Function):
     def _input_grads(chains, need):
         # the features are data (no gradient), parameters get theirs in place through _gbuf
         return [None] * (len(need) - 1)
+
+
+def _ln_blocks(lib, rows, H) -> int:
+    """LayerNorm-backward partial blocks of `rows` rows (from the C ABI's workspace size, so the row
+    count per block is never restated here)."""
+    return int(lib.mrg_residual_layernorm_bwd_workspace_bytes(rows, H)) // (2 * H * 4)
 
 
 def stack_eligible(H, B) -> bool:
