@@ -1,0 +1,75 @@
+/*
+ * mrg_tuning.h — tuning, measurement and test hooks of libmrg.so (not part of the drop-in
+ * boundary in mrg.h): knobs the measured A/Bs in DESIGN.md used, the kernel-bound probes
+ * bench.py times the families with, fault injection / CU-occupying stand-ins for the tests, and
+ * the structural-variant and pre-split-plane GEMM entry points that measured slower in the step.
+ * Same conventions as mrg.h (0 = success, mrg_last_error()).
+ */
+#ifndef MRG_TUNING_H_
+#define MRG_TUNING_H_
+
+#include "mrg.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* LDS-DMA pipelined x6 kernel for k-contiguous products (transA 0, transB 1, K % 32 == 0, unsplit,
+ * >= 2048 rows, >= 256 columns): ring depth 2..4 (0 = off; default 2, MRG_GEMM_GLDS) and column
+ * tile (64 forces 64-wide tiles, 128 = by shape).                                               */
+int mrg_gemm_set_glds(int depth, int bn);
+/* Weight-gradient products (transA 1, transB 0) on the LDS-DMA kernel (1, default) or the
+ * register-staged one (0); returns the previous setting.                                        */
+int mrg_gemm_set_glds_wg(int on);
+/* Three bf16 planes (the x6 split: v ~ p0 + p1 + p2) of n row-major fp32 weights, once per optimizer
+ * step: dst_i [3][R'][C'] with (R', C') = (rows_i, cols_i), or (cols_i, rows_i) when transpose_i.   */
+int mrg_split_planes_batched(int n, const float* const* src, void* const* dst, const int* rows, const int* cols,
+                             const int* transpose, hipStream_t stream);
+/* C = epi(alpha A B^T + beta C + bias), B as three bf16 planes (row n of plane p at
+ * Bplanes + p * bplane + n * ldb, bf16 elements), A [M][K] through the RowMap; K % 32 == 0.  The
+ * forward products x W^T and the input-gradient products dY W (B = planes of W^T) of the nn.Linear /
+ * LSTM / MultiheadAttention layers (mixer_block.py:63-74,237-252, for_sequential.py:42-51).      */
+int mrg_gemm_x6_planes(int M, int N, int K, float alpha, const float* A, long lda, long lda_hi, int a_rdiv,
+                       const void* Bplanes, long ldb, long bplane, float beta, float* C, long ldc,
+                       const float* bias, int epilogue, const float* aux, long ldaux, hipStream_t stream);
+/* Tuning only: force the tile shape (0: 128x128, 1: 128x64, 2: 64x64), -1 = heuristic. */
+int mrg_gemm_force_tile(int tile);
+/* Tuning only: structural variants of the x6 kernel (0 product, 1 split + one MFMA, 2 plane-0 +
+ * six MFMAs, 3 plane-0 + one MFMA) on C = A B^T, A [M][K], B [N][K]; var != 0 gives no valid C. */
+int mrg_gemm_x6_variant(int var, int M, int N, int K, const float* A, const float* B, float* C,
+                        hipStream_t stream);
+/* Fault injection (tests only): mode 1 makes the NEXT mrg_lstm_fwd launch drop member 0's first
+ * hand-off, so the recurrence times out and reports through *err; 0 disarms.  Process-wide.  */
+int mrg_lstm_debug_inject(int mode);
+/* Tests only: keep `blocks` workgroups of `threads` lanes and `lds` bytes of LDS resident for `usec`
+ * microseconds on `stream` (a stand-in for a CU-occupying kernel, e.g. an RCCL collective, beside a
+ * persistent recurrence, which must then wait for CUs without timing out its hand-offs).        */
+int mrg_debug_busy(int blocks, int threads, int lds, double usec, hipStream_t stream);
+/* Measurement (bench.py): while on, every kernel launched for a tagged library call (tag >= 0) is
+ * timed by start / stop events bound to that kernel (hipExtLaunchKernelGGL): its own execution,
+ * as rocprofv3 reports it.  stop waits, writes (ms, tag) per launch and returns the count. */
+int mrg_probe_start(int cap);
+int mrg_probe_tag(int tag);
+int mrg_probe_stop(float* ms, int* tags, int cap);
+
+/* Tuning knob: number of workgroups that share one batch row group at H = 256
+ * (8 or 16; default 8).  Process-wide; set before capture, not during. */
+int mrg_lstm_config(int group256);
+/* Diagnostics only: record per-step phase clocks (s_memtime) of block 0 of the next
+ * LSTM launches into buf ([T][8] u64); null disables.  Never in timed runs. */
+int mrg_lstm_debug_stamps(void* buf);
+/* Hand-off granule stores at workgroup scope (1, default; the line stays in the XCD's L2 where the
+ * group's agent-scope polls read it) or agent scope (0).  Env MRG_LSTM_LOCAL=0 starts with 0. */
+int mrg_lstm_set_local_handoff(int on);
+
+/* Timing experiments only: mrg_ssd_gate_cell_fwd (mode 1) with parts removed (dbg 1: no input
+ * prologue, 2: no gate GEMM, 3: neither); H = 256.  Outputs are not meaningful for dbg != 0. */
+int mrg_ssd_gate_cell_fwd_dbg(int dbg, int B, int H, int mode, const float* xin, const float* hp,
+                              const float* rp, const float* gamma, const float* beta, float eps, float* xout,
+                              float* mean, float* rstd, const float* w_ih, const float* b_ih,
+                              const float* b_hh, float* gates, float* c, float* h, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MRG_TUNING_H_ */

@@ -11,10 +11,30 @@ from tests.model_shapes import keys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _header_functions():
-    src = open(os.path.join(ROOT, "include", "mrg.h")).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(mrg_[a-z0-9_]+)\s*\(", src)))
+HEADERS = ("mrg.h", "mrg_tuning.h")   # the drop-in boundary; tuning / measurement / test hooks
+
+
+def _header_text(name="mrg.h"):
+    return open(os.path.join(ROOT, "include", name)).read()
+
+
+def _header_functions(names=HEADERS):
+    out = set()
+    for name in names:
+        src = re.sub(r"/\*.*?\*/", "", _header_text(name), flags=re.S)
+        out.update(re.findall(r"\b(mrg_[a-z0-9_]+)\s*\(", src))
+    return sorted(out)
+
+
+def test_boundary_header_holds_no_tuning_hooks():
+    """include/mrg.h is the drop-in boundary only: the tuning knobs, probes, fault injection and the
+    measured-slower GEMM variants live in include/mrg_tuning.h."""
+    boundary = set(_header_functions(("mrg.h",)))
+    tuning = set(_header_functions(("mrg_tuning.h",)))
+    assert not boundary & tuning
+    for name in ("mrg_gemm_x6_variant", "mrg_gemm_force_tile", "mrg_ssd_gate_cell_fwd_dbg", "mrg_split_planes_batched",
+                 "mrg_gemm_x6_planes", "mrg_lstm_debug_inject", "mrg_lstm_debug_stamps", "mrg_probe_start"):
+        assert name in tuning and name not in boundary, name
 
 
 def test_library_exports_every_header_symbol():
@@ -173,7 +193,7 @@ def test_checkpoint_round_trip_through_load_model(tmp_path, model_type):
 def test_ctypes_signatures_match_header_arity():
     """Every binding in _lib.SIGNATURES declares as many arguments as include/mrg.h gives the entry."""
     from multimodalreactiongeneration_amd import _lib
-    h = open(os.path.join(ROOT, "include", "mrg.h")).read()
+    h = "\n".join(_header_text(n) for n in HEADERS)
     for name, (_res, args) in _lib.SIGNATURES.items():
         m = re.search(r"^(?:const\s+)?\w+\s*\**\s*" + name + r"\s*\(([^;]*?)\);", h, re.S | re.M)
         assert m, name

@@ -377,6 +377,27 @@ def test_residual_layernorm_vs_torch(E):
     assert rel_err(gd.grad, gr.grad) < TOL and rel_err(btd.grad, btr.grad) < TOL
 
 
+@pytest.mark.parametrize("rows,E", [(5000, 256), (19200, 256), (19200, 1000), (70, 256)])
+def test_layernorm_param_reduce_row_groups(rows, E):
+    """dgamma / dbeta through the 2-D ticketed parameter reduce: ragged row groups (5000 rows: 157
+    partial blocks in 9 groups), the benchmark's 19,200 rows (16 groups), E = 1000 (16 column blocks,
+    partial last) and a single group; twice in a row (the tickets return to 0), vs torch float64."""
+    from multimodalreactiongeneration_amd import functional as Fn
+    g = torch.Generator().manual_seed(rows + E)
+    a, b = torch.randn(rows, E, generator=g), torch.randn(rows, E, generator=g)
+    gam, bet = 1 + 0.1 * torch.randn(E, generator=g), 0.1 * torch.randn(E, generator=g)
+    dy = torch.randn(rows, E, generator=g)
+    gr, btr = gam.double().requires_grad_(True), bet.double().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(a.double() + b.double(), (E,), gr, btr, 1e-5)
+    yr.backward(dy.double())
+    for _ in range(2):
+        gd, btd = _param(gam), _param(bet)
+        y = Fn.residual_layernorm(a.to(DEV), b.to(DEV), gd, btd)
+        y.backward(dy.to(DEV))
+        torch.cuda.synchronize()
+        assert rel_err(gd.grad, gr.grad) < TOL and rel_err(btd.grad, btr.grad) < TOL
+
+
 @pytest.mark.parametrize("loss_type", ["huber", "mse", "mae", "smoothl1"])
 def test_masked_loss_vs_oracle(loss_type):
     from multimodalreactiongeneration_amd import functional as Fn
