@@ -47,20 +47,27 @@ struct AttnArgs {
   int causal;
   float scale;
   int qvec, ovec, dkvvec;  // rows of q / o / dk and dv 16-B aligned: float4 loads and stores
+  // query chunk (mrg_attention_*_chunk): the Tq queries are rows [q_off, q_off + Tq) of a sequence of
+  // Tqf queries (the causal rule uses global indices and Tk / Tqf); qpad rows have stride qp_bs;
+  // kv_acc: the dK / dV pass adds into dk / dv (a chunk's share) instead of storing
+  int q_off, Tqf;
+  long qp_bs;
+  int kv_acc;
 };
 
 // exclusive upper bound of the keys query i may see (causal rule only; Tk when not causal)
 __device__ __forceinline__ int key_bound(const AttnArgs& a, int i) {
   if (!a.causal) return a.Tk;
-  i = min(i, a.Tq - 1);
-  int lim = (a.Tk >= a.Tq) ? (i + 1) * (a.Tk / a.Tq) : i / (a.Tq / a.Tk) + 1;
+  i = min(i, a.Tq - 1) + a.q_off;
+  int lim = (a.Tk >= a.Tqf) ? (i + 1) * (a.Tk / a.Tqf) : i / (a.Tqf / a.Tk) + 1;
   return min(lim, a.Tk);
 }
 
 // first query that may see key j (causal rule only)
 __device__ __forceinline__ int query_start(const AttnArgs& a, int j) {
   if (!a.causal) return 0;
-  return (a.Tk >= a.Tq) ? j / (a.Tk / a.Tq) : j * (a.Tq / a.Tk);
+  const int g = (a.Tk >= a.Tqf) ? j / (a.Tk / a.Tqf) : j * (a.Tqf / a.Tk);
+  return max(g - a.q_off, 0);   // chunk-local
 }
 
 static constexpr int TT = 64;  // keys (forward, dQ) or queries (dK/dV) per LDS tile
@@ -196,6 +203,30 @@ __device__ __forceinline__ void store_row(float* p, int lg, bool vec, const f32x
     }
 }
 
+// as store_row, adding to what p holds
+template <int D>
+__device__ __forceinline__ void add_row(float* p, int lg, bool vec, const f32x4 (&v)[AttnCfg<D>::DT], float mul) {
+  using C = AttnCfg<D>;
+  if constexpr (C::VEC && C::DT == 4) {
+    if (vec) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float4* q = reinterpret_cast<float4*>(p + 4 * (4 * lg + r));
+        const float4 o = *q;
+        *q = make_float4(o.x + v[0][r] * mul, o.y + v[1][r] * mul, o.z + v[2][r] * mul, o.w + v[3][r] * mul);
+      }
+      return;
+    }
+  }
+#pragma unroll
+  for (int dt = 0; dt < C::DT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int d = dout<D>(lg, dt, r);
+      if (d < D) p[d] += v[dt][r] * mul;
+    }
+}
+
 // S^T tile (16 keys x 16 queries) = K rows [kr..kr+15] . Q^T, two accumulation chains
 template <int D>
 __device__ __forceinline__ f32x4 qk16(const float* Ks, int rowbase, const float (&qreg)[AttnCfg<D>::KS], int lq,
@@ -225,7 +256,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   const int qi = q0 + wave * 16 + lq;
   const int hoff = h * D;
   const bool pad = a.qpad && a.kpad;
-  const bool qp = pad && qi < a.Tq && a.qpad[(long)b * a.Tq + qi];
+  const bool qp = pad && qi < a.Tq && a.qpad[(long)b * a.qp_bs + qi];
   const int kmax = key_bound(a, qi);                    // this lane's query
   const int wmin = key_bound(a, q0 + wave * 16);        // smallest bound in the wave (monotone in i)
   const int wlim = key_bound(a, q0 + wave * 16 + 15);   // largest: sub-tiles from here on are masked
@@ -352,7 +383,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
   const int hoff = h * D;
   const bool qv = qi < a.Tq;
   const bool pad = a.qpad && a.kpad;
-  const bool qp = pad && qv && a.qpad[(long)b * a.Tq + qi];
+  const bool qp = pad && qv && a.qpad[(long)b * a.qp_bs + qi];
   const int kmax = key_bound(a, qi);
   const int wlim = key_bound(a, q0 + wave * 16 + 15);
   float qreg[C::KS], dreg[C::KS];
@@ -495,7 +526,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
   const int qs = (query_start(a, kb0) / 16) * 16;
   const float* qb_ = a.q + (long)b * a.q_bs + hoff;
   const float* db_ = a.dout + (long)b * a.do_bs + hoff;
-  const unsigned char* qpb = pad ? a.qpad + (long)b * a.Tq : nullptr;
+  const unsigned char* qpb = pad ? a.qpad + (long)b * a.qp_bs : nullptr;
   TileRegs<D> tq, td;
   unsigned char qpn = 0;  // padding flag of query qt0 + lane
   if (qs < a.Tq) {
@@ -582,8 +613,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
     }
   }
   if (kv) {
-    store_row<D>(a.dk + (long)b * a.dk_bs + (long)kj * a.dk_ts + hoff, lg, a.dkvvec, dkT, a.scale);
-    store_row<D>(a.dv + (long)b * a.dv_bs + (long)kj * a.dv_ts + hoff, lg, a.dkvvec, dvT, 1.0f);
+    if (a.kv_acc) {   // a query chunk's share: add (the chunks run in a fixed order: deterministic)
+      add_row<D>(a.dk + (long)b * a.dk_bs + (long)kj * a.dk_ts + hoff, lg, a.dkvvec, dkT, a.scale);
+      add_row<D>(a.dv + (long)b * a.dv_bs + (long)kj * a.dv_ts + hoff, lg, a.dkvvec, dvT, 1.0f);
+    } else {
+      store_row<D>(a.dk + (long)b * a.dk_bs + (long)kj * a.dk_ts + hoff, lg, a.dkvvec, dkT, a.scale);
+      store_row<D>(a.dv + (long)b * a.dv_bs + (long)kj * a.dv_ts + hoff, lg, a.dkvvec, dvT, 1.0f);
+    }
   }
 }
 
@@ -601,6 +637,7 @@ static AttnArgs attn_base(int B, int Hh, int Tq, int Tk, const float* q, long q_
   a.v = v; a.v_bs = v_bs; a.v_ts = v_ts; a.o = const_cast<float*>(o); a.o_bs = o_bs; a.o_ts = o_ts;
   a.lse = const_cast<float*>(lse); a.qpad = qpad; a.kpad = kpad; a.B = B; a.Hh = Hh; a.Tq = Tq; a.Tk = Tk;
   a.causal = causal; a.scale = scale;
+  a.q_off = 0; a.Tqf = Tq; a.qp_bs = Tq; a.kv_acc = 0;
   return a;
 }
 
@@ -669,6 +706,71 @@ MRG_API int mrg_attention_bwd(int B, int Hh, int Tq, int Tk, int D,
   MRG_ATTN_DISPATCH(attn_bwd_dq_kernel, gq, a);  // also writes delta = rowsum(dO * O) to the workspace
   if (check_launch("attn_bwd_dq_kernel")) return 1;
   dim3 gk(Hh, B, (Tk + 63) / 64);
+  MRG_ATTN_DISPATCH(attn_bwd_dkv_kernel, gk, a);
+  return check_launch("attn_bwd_dkv_kernel");
+}
+
+// Query-chunk forms (the block-level (block, time-chunk) wavefront, metaformer_stack.py): the Tq
+// query rows handed in (q, o, dout, dq: pointers to the chunk's first row; lse and the workspace:
+// chunk-sized [B, heads, Tq]) are rows [q_off, q_off + Tq) of a Tq_full-query sequence; qpad is the
+// whole sequence's [B, Tq_full] flags.  bwd with kv_accumulate = 1 ADDS the chunk's share into
+// dk / dv (only the key blocks some query of the chunk sees are touched).
+MRG_API int mrg_attention_fwd_chunk(int B, int Hh, int Tq, int Tk, int D, int q_off, int Tq_full,
+                                    const float* q, long q_bs, long q_ts, const float* k, long k_bs, long k_ts,
+                                    const float* v, long v_bs, long v_ts, float* o, long o_bs, long o_ts,
+                                    float* lse, const unsigned char* qpad, const unsigned char* kpad,
+                                    int causal, float scale, hipStream_t stream) {
+  if (int e = attn_check(D, Tq_full, Tk, causal)) return e;
+  MRG_REQUIRE(q_off >= 0 && Tq >= 0 && q_off + Tq <= Tq_full, "attention fwd chunk: rows [%d, %d) outside %d",
+              q_off, q_off + Tq, Tq_full);
+  if (B == 0 || Tq == 0) return 0;
+  MRG_REQUIRE(rows16(k, k_bs, k_ts) && rows16(v, v_bs, v_ts),
+              "attention fwd: K/V rows must be 16-B aligned (strides multiple of 4 floats)");
+  AttnArgs a = attn_base(B, Hh, Tq, Tk, q, q_bs, q_ts, k, k_bs, k_ts, v, v_bs, v_ts, o, o_bs, o_ts, lse,
+                         qpad ? qpad + q_off : nullptr, kpad, causal, scale);
+  a.q_off = q_off; a.Tqf = Tq_full; a.qp_bs = Tq_full;
+  a.qvec = rows16(q, q_bs, q_ts) && (D % 4) == 0;
+  a.ovec = rows16(o, o_bs, o_ts) && (D % 4) == 0;
+  dim3 grid(Hh, B, (Tq + 63) / 64);
+  MRG_ATTN_DISPATCH(attn_fwd_kernel, grid, a);
+  return check_launch("attn_fwd_kernel");
+}
+
+MRG_API int mrg_attention_bwd_chunk(int B, int Hh, int Tq, int Tk, int D, int q_off, int Tq_full,
+                                    const float* q, long q_bs, long q_ts, const float* k, long k_bs, long k_ts,
+                                    const float* v, long v_bs, long v_ts, const float* o, long o_bs, long o_ts,
+                                    const float* lse, const unsigned char* qpad, const unsigned char* kpad,
+                                    int causal, float scale, const float* dout, long do_bs, long do_ts,
+                                    float* dq, long dq_bs, long dq_ts, float* dk, long dk_bs, long dk_ts,
+                                    float* dv, long dv_bs, long dv_ts, int kv_accumulate, float* workspace,
+                                    hipStream_t stream) {
+  if (int e = attn_check(D, Tq_full, Tk, causal)) return e;
+  MRG_REQUIRE(q_off >= 0 && Tq >= 0 && q_off + Tq <= Tq_full, "attention bwd chunk: rows [%d, %d) outside %d",
+              q_off, q_off + Tq, Tq_full);
+  if (B == 0 || Tq == 0 || Tk == 0) return 0;
+  MRG_REQUIRE(rows16(q, q_bs, q_ts) && rows16(k, k_bs, k_ts) && rows16(v, v_bs, v_ts) &&
+              rows16(dout, do_bs, do_ts), "attention bwd: Q/K/V/dO rows must be 16-B aligned");
+  MRG_REQUIRE(workspace != nullptr, "attention bwd: workspace (B*heads*Tq floats) required");
+  AttnArgs a = attn_base(B, Hh, Tq, Tk, q, q_bs, q_ts, k, k_bs, k_ts, v, v_bs, v_ts, o, o_bs, o_ts, lse,
+                         qpad ? qpad + q_off : nullptr, kpad, causal, scale);
+  a.q_off = q_off; a.Tqf = Tq_full; a.qp_bs = Tq_full; a.kv_acc = kv_accumulate ? 1 : 0;
+  a.dout = dout; a.do_bs = do_bs; a.do_ts = do_ts; a.dlt = workspace;
+  a.dq = dq; a.dq_bs = dq_bs; a.dq_ts = dq_ts; a.dk = dk; a.dk_bs = dk_bs; a.dk_ts = dk_ts;
+  a.dv = dv; a.dv_bs = dv_bs; a.dv_ts = dv_ts;
+  a.qvec = 1;
+  a.ovec = rows16(o, o_bs, o_ts);
+  a.dkvvec = rows16(dk, dk_bs, dk_ts) && rows16(dv, dv_bs, dv_ts);
+  dim3 gq(Hh, B, (Tq + 63) / 64);
+  MRG_ATTN_DISPATCH(attn_bwd_dq_kernel, gq, a);
+  if (check_launch("attn_bwd_dq_kernel")) return 1;
+  // accumulating: only the key blocks the chunk's last query can see (the rest get nothing)
+  int tk = Tk;
+  if (a.kv_acc && causal) {
+    const int gl = q_off + Tq - 1;
+    tk = (Tk >= Tq_full) ? (gl + 1) * (Tk / Tq_full) : gl / (Tq_full / Tk) + 1;
+    tk = tk < Tk ? tk : Tk;
+  }
+  dim3 gk(Hh, B, (tk + 63) / 64);
   MRG_ATTN_DISPATCH(attn_bwd_dkv_kernel, gk, a);
   return check_launch("attn_bwd_dkv_kernel");
 }

@@ -1107,3 +1107,55 @@ def test_fill_zero_any_alignment_and_size():
             assert bool((host[:off] == 0xAB).all()) and bool((host[off + n:] == 0xAB).all()), (off, n)
     z = Fn.zeros(3, 5, dtype=torch.int64, device=DEV)
     assert z.dtype == torch.int64 and int(z.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("Tq,Tk,causal,cuts", [(300, 300, True, (0, 100, 200, 300)), (150, 300, True, (0, 37, 64, 150)),
+                                                (300, 150, True, (0, 150, 300)), (100, 100, False, (0, 50, 100))])
+def test_attention_query_chunks_match_whole(Tq, Tk, causal, cuts):
+    """mrg_attention_{fwd,bwd}_chunk over query chunks (the block wavefront's form) vs one whole call:
+    outputs, log-sum-exp and dQ bitwise (every query's arithmetic is the same), dK / dV accumulated
+    chunk by chunk within fp32 reordering; ragged padding flags included."""
+    from multimodalreactiongeneration_amd import _lib
+    from multimodalreactiongeneration_amd.functional import _ptr, _stream
+    lib = _lib.load()
+    B, Hh, D = 3, 4, 64
+    E = Hh * D
+    g = torch.Generator().manual_seed(Tq + 3 * Tk)
+    q, k, v, do = (torch.randn(B, T, E, generator=g).to(DEV) for T in (Tq, Tk, Tk, Tq))
+    qpad = torch.zeros(B, Tq, dtype=torch.uint8)
+    kpad = torch.zeros(B, Tk, dtype=torch.uint8)
+    qpad[1, Tq * 2 // 3:] = 1
+    kpad[1, Tk * 2 // 3:] = 1
+    qpad, kpad = qpad.to(DEV), kpad.to(DEV)
+    sc = 1.0 / math.sqrt(D)
+    f = dict(device=DEV, dtype=torch.float32)
+
+    def bwd_args(qq, oo, lse, dd, dq, dk, dv):
+        return (_ptr(qq), Tq * E, E, _ptr(k), Tk * E, E, _ptr(v), Tk * E, E, _ptr(oo), Tq * E, E, _ptr(lse),
+                _ptr(qpad), _ptr(kpad), int(causal), sc, _ptr(dd), Tq * E, E, _ptr(dq), Tq * E, E, _ptr(dk), Tk * E, E,
+                _ptr(dv), Tk * E, E)
+    o, lse = torch.empty(B, Tq, E, **f), torch.empty(B, Hh, Tq, **f)
+    assert lib.mrg_attention_fwd(B, Hh, Tq, Tk, D, _ptr(q), Tq * E, E, _ptr(k), Tk * E, E, _ptr(v), Tk * E, E, _ptr(o),
+                                 Tq * E, E, _ptr(lse), _ptr(qpad), _ptr(kpad), int(causal), sc, _stream()) == 0
+    dq, dk, dv = torch.empty(B, Tq, E, **f), torch.empty(B, Tk, E, **f), torch.empty(B, Tk, E, **f)
+    ws = torch.empty(B * Hh * Tq, **f)
+    assert lib.mrg_attention_bwd(B, Hh, Tq, Tk, D, *bwd_args(q, o, lse, do, dq, dk, dv), _ptr(ws), _stream()) == 0
+    oc, dqc = torch.full_like(o, 7.0), torch.full_like(dq, 7.0)
+    dkc, dvc = torch.zeros_like(dk), torch.zeros_like(dv)
+    for q0, q1 in zip(cuts[:-1], cuts[1:]):
+        n = q1 - q0
+        lc = torch.empty(B, Hh, n, **f)
+        assert lib.mrg_attention_fwd_chunk(B, Hh, n, Tk, D, q0, Tq, _ptr(q, q0 * E), Tq * E, E, _ptr(k), Tk * E, E,
+                                           _ptr(v), Tk * E, E, _ptr(oc, q0 * E), Tq * E, E, _ptr(lc), _ptr(qpad),
+                                           _ptr(kpad), int(causal), sc, _stream()) == 0
+        wsc = torch.empty(B * Hh * n, **f)
+        assert lib.mrg_attention_bwd_chunk(
+            B, Hh, n, Tk, D, q0, Tq, _ptr(q, q0 * E), Tq * E, E, _ptr(k), Tk * E, E, _ptr(v), Tk * E, E,
+            _ptr(oc, q0 * E), Tq * E, E, _ptr(lc), _ptr(qpad), _ptr(kpad), int(causal), sc, _ptr(do, q0 * E),
+            Tq * E, E, _ptr(dqc, q0 * E), Tq * E, E, _ptr(dkc), Tk * E, E, _ptr(dvc), Tk * E, E, 1, _ptr(wsc),
+            _stream()) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(lc, lse[:, :, q0:q1])
+    torch.cuda.synchronize()
+    assert torch.equal(oc, o) and torch.equal(dqc, dq)
+    assert rel_err(dkc, dk) < 1e-5 and rel_err(dvc, dv) < 1e-5

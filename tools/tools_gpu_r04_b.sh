@@ -6,7 +6,7 @@ mkdir -p $O
 timeout -k 10 300 python -u _bisect/diag_replay.py _bisect/a > $O/bisect_a.log 2>&1; echo "bisect rc=$?"
 timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
   tests/test_gpu_capture.py tests/test_gpu_models.py tests/test_gpu_ops.py \
-  -k "layernorm or encoder_stack or b64 or kv_sink or feature_input or fused_integrator or wgrad_side or benchmark_width" -s > $O/tests.log 2>&1
+  -k "query_chunks or layernorm or encoder_stack or b64 or kv_sink or feature_input or fused_integrator or wgrad_side or benchmark_width" -s > $O/tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 for i in 1 2; do
   for v in 0 1; do
