@@ -326,6 +326,10 @@ int mrg_zero_padding(long n, const float* x, float value, float* y, hipStream_t 
  * rings, loss-gradient lead frames) without a torch fill kernel.  Replaces the `zero_grad` /
  * `torch.zeros` of the reference's step (lstmformer.py:313-322 loss, Lightning's optimizer zero_grad). */
 int mrg_fill_zero(void* p, long bytes, hipStream_t stream);
+/* dst [n1][n0][E] = src [n0][n1][E] (beta = 1: dst +=): the batch-major [B, T, E] <-> time-major
+ * [T, B, E] activations and gradients at the metaformer blocks' wavefront boundaries
+ * (multi_modal_metaformer.py:501-502 feeds block outputs forward batch-major).  E % 4 == 0.     */
+int mrg_swap01(int n0, int n1, int E, const float* src, float* dst, float beta, hipStream_t stream);
 
 /* ---------------------------------------------------------------- loss
  * Masked regression loss of training_step (lstmformer.py:372-380,

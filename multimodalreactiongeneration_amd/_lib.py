@@ -113,6 +113,7 @@ SIGNATURES = {
     "mrg_debug_busy": (c_int, [c_int, c_int, c_int, ctypes.c_double, P]),
     "mrg_padding_flags": (c_int, [c_int, c_int, P, c_long, c_long, c_float, P, P]),
     "mrg_zero_padding": (c_int, [c_long, P, c_float, P, P]),
+    "mrg_swap01": (c_int, [c_int, c_int, c_int, P, P, c_float, P]),
     "mrg_fill_zero": (c_int, [P, c_long, P]),
     "mrg_probe_start": (c_int, [c_int]),
     "mrg_probe_tag": (c_int, [c_int]),

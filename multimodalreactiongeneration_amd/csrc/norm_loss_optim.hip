@@ -909,7 +909,42 @@ __global__ __launch_bounds__(256) void fill_zero_kernel(unsigned char* p, long h
   if (t < bytes - tail0) p[tail0 + t] = 0;
 }
 
+// dst[j][i][:] = src[i][j][:] for an [n0][n1][E] tensor (E % 4 == 0, 16-B aligned): float4 rows,
+// one thread per 16 B, rows in destination order (coalesced stores, 1-KB row reads)
+__global__ __launch_bounds__(256) void swap01_kernel(const float* __restrict__ src, float* __restrict__ dst, int n0,
+                                                     int n1, int E4, float beta) {
+  const long total = (long)n0 * n1 * E4;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
+    const long row = e / E4;
+    const int c = (int)(e - row * E4);
+    const int j = (int)(row / n0), i = (int)(row - (long)j * n0);   // dst row (j, i)
+    const float4 v = reinterpret_cast<const float4*>(src)[((long)i * n1 + j) * E4 + c];
+    float4* d = reinterpret_cast<float4*>(dst) + e;
+    if (beta != 0.0f) {
+      const float4 o = *d;
+      *d = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+    } else {
+      *d = v;
+    }
+  }
+}
+
 }  // namespace mrg
+
+// [n0][n1][E] -> [n1][n0][E] (batch-major <-> time-major activations at the block wavefront's
+// boundaries); beta = 1 adds into dst (a gradient arriving from two consumers).
+MRG_API int mrg_swap01(int n0, int n1, int E, const float* src, float* dst, float beta, hipStream_t stream) {
+  MRG_REQUIRE(n0 >= 0 && n1 >= 0 && E > 0 && E % 4 == 0 && ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) &&
+                  (beta == 0.0f || beta == 1.0f),
+              "mrg_swap01: E %% 4 == 0, 16-B aligned buffers, beta 0 or 1 required");
+  const long total = (long)n0 * n1 * (E / 4);
+  if (total == 0) return 0;
+  long blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  klaunch(mrg::swap01_kernel, (unsigned)blocks, 256, 0, stream, src, dst, n0, n1, E / 4, beta);
+  return check_launch("swap01_kernel");
+}
 
 MRG_API int mrg_fill_zero(void* p, long bytes, hipStream_t stream) {
   MRG_REQUIRE(bytes >= 0 && (bytes == 0 || p), "mrg_fill_zero: bad arguments");
