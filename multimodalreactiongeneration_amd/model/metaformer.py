@@ -90,8 +90,17 @@ class IntegrateModalBlock(nn.Module):
     def _fused(self, main_modal, other_modals, attn_mask, hxs):
         """integrate.integrate(...) when the block is inside its form (single-block MHA layerds with
         residual LN, one-Linear residual-LN FeedForward, block-causal or no mask, no state), else None."""
-        from .masks import BlockCausalMask
         from ..integrate import integrate
+        args = self.fused_args(main_modal, other_modals, attn_mask, hxs)
+        if args is None:
+            return None
+        params, cw, cb, heads, causal, eps, qpads, kpads = args
+        return integrate(main_modal, list(other_modals), qpads, kpads, params, cw, cb, heads, causal, eps)
+
+    def fused_args(self, main_modal, other_modals, attn_mask, hxs):
+        """(per-integrator parameter tuples, cat_w, cat_b, heads, causal, eps, qpads, kpads) of the fused
+        form (integrate.py, block_stack.py), or None when the block is outside it."""
+        from .masks import BlockCausalMask
         if not (self.use_fused and isinstance(main_modal, torch.Tensor) and main_modal.is_cuda
                 and main_modal.dim() == 3 and main_modal.shape[1] > 1 and all(h is None for h in hxs)):
             return None
@@ -137,8 +146,7 @@ class IntegrateModalBlock(nn.Module):
             return None
         qpads = [m.main_pad if causal else None for m in masks]
         kpads = [m.other_pad if causal else None for m in masks]
-        return integrate(main_modal, list(other_modals), qpads, kpads, params, cw, self.cat_linear.bias,
-                         heads.pop(), causal, eps.pop())
+        return params, cw, self.cat_linear.bias, heads.pop(), causal, eps.pop(), qpads, kpads
 
     def forward(self, main_modal, other_modals, attn_mask=None, hxs=None):
         other_modals, attn_mask, hxs = self.check_form_input(other_modals, attn_mask, hxs)
@@ -342,6 +350,54 @@ class MultiModalMetaformer(nn.Module):
             return None
         return encoder_stack([(f, e.weight, e.bias, l) for f, e, l in zip(feats, embs, layers)], eps)
 
+    # ---- MI355X schedule: blocks 1.. as one (block, time-chunk) wavefront (block_stack.py); on by
+    # default, MRG_BLOCK_STACK=0 (or MRG_BLOCK_CHUNK=0) keeps the block-by-block schedule
+    use_block_stack = os.environ.get("MRG_BLOCK_STACK", "1") == "1"
+
+    def _stack_blocks(self, x, other_modals, attn_mask):
+        """The output of blocks 1.. through block_stack.block_stack, or None when a block is outside its
+        form (LSTM block as in the encoder stack, fused-integrator form, Linear-ReLU-Linear residual-LN
+        FeedForward, one LayerNorm eps) or the input is not a CUDA fp32 [B, T, E] tensor."""
+        from ..block_stack import block_stack, CHUNK
+        blocks = list(self.metaformer_blocks)[1:]
+        if not (self.use_block_stack and CHUNK > 0 and blocks and isinstance(x, torch.Tensor) and x.is_cuda
+                and x.dim() == 3 and x.shape[1] >= 2 and Fn._ARITH[0] is None and x.shape[2] % 4 == 0):
+            return None
+        if any(b.encode_other_modal for b in blocks):
+            return None
+        flat, eps_all, fa0 = [], set(), None
+        for b in blocks:
+            got = self._stack_layers(b)
+            if got is None or len(got[0]) != 1 or len(got[0][0]) != 1:
+                return None
+            layer, eps = got[0][0][0], got[1]
+            om, am, hx = b.integrator.check_form_input(other_modals, attn_mask, None)
+            fa = b.integrator.fused_args(x, om, am, hx)
+            if fa is None:
+                return None
+            params, cw, cb, heads, causal, ieps, qpads, kpads = fa
+            ff = getattr(b.feedforward, "feed_forward", None)
+            if not (isinstance(ff, ResidualConnection) and ff.layer_norm is not None):
+                return None
+            mods = list(ff.module.children())
+            if not (len(mods) == 3 and isinstance(mods[0], nn.Linear) and isinstance(mods[1], nn.ReLU)
+                    and isinstance(mods[2], nn.Linear) and mods[0].bias is not None and mods[2].bias is not None):
+                return None
+            if fa0 is None:
+                fa0 = (heads, causal, qpads, kpads, om)
+            elif (heads, causal) != fa0[:2] or any(a is not b2 for a, b2 in zip(qpads + kpads, fa0[2] + fa0[3])):
+                return None
+            eps_all.update((eps, ieps, ff.layer_norm.eps))
+            flat.append([*layer, *[t for p in params for t in p], cw, cb, mods[0].weight, mods[0].bias,
+                         mods[2].weight, mods[2].bias, ff.layer_norm.weight, ff.layer_norm.bias])
+        heads, causal, qpads, kpads, om = fa0
+        if len(eps_all) != 1 or any(q is not qpads[0] for q in qpads):
+            return None
+        if x.shape[2] // heads not in (8, 16, 32, 64):
+            return None
+        sinks = [getattr(kv, "_mrg_kv_sink", None) for kv in om]
+        return block_stack(x, list(om), qpads[0], kpads, flat, heads, causal, eps_all.pop(), sinks)
+
     def _fast_eligible(self) -> bool:
         if self.interlayer_residual:
             return False
@@ -373,6 +429,13 @@ class MultiModalMetaformer(nn.Module):
         if fast:
             record = []
             for bi, block in enumerate(self.metaformer_blocks):
+                if bi == 1:
+                    out = self._stack_blocks(main_modal, other_modals, integrate_attn_mask)
+                    if out is not None:
+                        main_modal = out
+                        record += [{"emb": [None] * b.emb_num_modal, "crm": [None] * (self.modal_num - 1)}
+                                   for b in list(self.metaformer_blocks)[1:]]
+                        break
                 mods = [main_modal] + (list(other_modals) if block.encode_other_modal else [])
                 enc = stacked if (bi == 0 and stacked is not None) else self._fast_first_embedding(block, mods)
                 main_modal = enc[0]
