@@ -38,8 +38,9 @@ int mrg_gemm_force_tile(int tile);
  * six MFMAs, 3 plane-0 + one MFMA) on C = A B^T, A [M][K], B [N][K]; var != 0 gives no valid C. */
 int mrg_gemm_x6_variant(int var, int M, int N, int K, const float* A, const float* B, float* C,
                         hipStream_t stream);
-/* Fault injection (tests only): mode 1 makes the NEXT mrg_lstm_fwd launch drop member 0's first
- * hand-off, so the recurrence times out and reports through *err; 0 disarms.  Process-wide.  */
+/* Fault injection (tests only): mode 1 makes the NEXT mrg_lstm_fwd launch (mode 2: the next
+ * mrg_lstm_bwd launch) drop member 0's first hand-off, VALU or MFMA form, so the recurrence times
+ * out and reports through *err; 0 disarms.  Process-wide.  */
 int mrg_lstm_debug_inject(int mode);
 /* Tests only: keep `blocks` workgroups of `threads` lanes and `lds` bytes of LDS resident for `usec`
  * microseconds on `stream` (a stand-in for a CU-occupying kernel, e.g. an RCCL collective, beside a

@@ -370,7 +370,7 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
         for (int o = 0; o < OT; ++o) acc[o] = group_sum<RC>(acc[o]);
         // every lane of the RC group holds the sums: lanes rc < OT each publish granule o = rc, so
         // a wave's puts are contiguous 8-B granules in ONE store instruction (full 128-B lines)
-        if (rc < OT && b0 + b < B) {
+        if (rc < OT && b0 + b < B && !(args.inject == 2 && j == 0 && tt == 0)) {
           const int h0 = ogr * OT;
           const int dest = h0 / U, du = h0 % U;
           float v = acc[0];
@@ -441,7 +441,7 @@ template <int H, int G>
 static int launch_fwd(const LstmFwdArgs& a, int force_bs, int cus, hipStream_t s) {
   constexpr int NT = LstmNT<H, G>::value;
   const long groups1 = a.B;
-  if (H == 256 && G == 8 && g_mx && force_bs <= 0 && !a.inject && (!a.stamps || g_mx == 2)) {
+  if (H == 256 && G == 8 && g_mx && force_bs <= 0 && (!a.stamps || g_mx == 2)) {
     const int bs = valu_bs(lstm_fwd_kernel<H, G, 1>, lstm_fwd_kernel<H, G, 2>, lstm_fwd_kernel<H, G, 4>,
                            lstm_fwd_kernel<H, G, 8>, lstm_fwd_kernel<H, G, 16>, NT, a.nprob, a.B, G, cus);
     if (g_mx == 2 || bs == 0 || bs >= g_mx_min_bs) {
@@ -532,7 +532,7 @@ MRG_API int mrg_lstm_set_local_handoff(int on) {
 
 // Tests only: arm a fault for the next forward launch (see mrg.h).
 MRG_API int mrg_lstm_debug_inject(int mode) {
-  MRG_REQUIRE(mode == 0 || mode == 1, "mrg_lstm_debug_inject: mode must be 0 or 1");
+  MRG_REQUIRE(mode >= 0 && mode <= 2, "mrg_lstm_debug_inject: mode must be 0, 1 (next fwd) or 2 (next bwd)");
   g_inject = mode;
   return 0;
 }
@@ -597,8 +597,8 @@ MRG_API int mrg_lstm_fwd(int nprob, int B, int T, int H,
   LstmFwdArgs a;
   memset(&a, 0, sizeof(a));
   a.nprob = nprob; a.B = B; a.T = T; a.err = err; a.stamps = g_stamps;
-  a.inject = g_inject;
-  g_inject = 0;  // one launch only
+  a.inject = g_inject == 1 ? 1 : 0;
+  if (g_inject == 1) g_inject = 0;  // one launch only
   a.local = g_local;
   for (int i = 0; i < nprob; ++i) {
     LstmFwdProblem& p = a.p[i];
@@ -639,6 +639,8 @@ MRG_API int mrg_lstm_bwd(int nprob, int B, int T, int H,
   memset(&a, 0, sizeof(a));
   a.nprob = nprob; a.B = B; a.T = T; a.err = err; a.stamps = g_stamps;
   a.local = g_local;
+  a.inject = g_inject == 2 ? 2 : 0;
+  if (g_inject == 2) g_inject = 0;  // one launch only
   for (int i = 0; i < nprob; ++i) {
     LstmBwdProblem& p = a.p[i];
     p.w_hh = w_hh[i]; p.gates = gates[i]; p.cs = cs[i]; p.c0 = c0 ? c0[i] : nullptr;

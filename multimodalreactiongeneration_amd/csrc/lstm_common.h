@@ -55,6 +55,7 @@ struct LstmFwdArgs {
 struct LstmBwdArgs {
   LstmBwdProblem p[MAXP];
   int nprob, B, T;
+  int inject;  // fault injection (mrg_lstm_debug_inject mode 2): member 0 drops its first hand-off
   int local;
   int* err;
   unsigned long long* stamps;

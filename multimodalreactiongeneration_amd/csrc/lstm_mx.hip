@@ -149,7 +149,7 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_fwd_mx_kernel(LstmFwdArgs args)
     }
     {  // publish h of units (cu, cu + 1) from the even lane of each pair (lanes l, l ^ 1 hold cu, cu ^ 1)
       const float hn = dpp_f<0xB1>(h);
-      if (cvalid && (cu & 1) == 0)
+      if (cvalid && (cu & 1) == 0 && !(args.inject == 1 && j == 0 && tt == 0))
         put_pair(xb + ((long)par * B + bg) * HP + (hcol >> 1), (unsigned)(tt + 1) & 3u, h, hn, local);
     }
     if (cvalid) {
@@ -317,7 +317,7 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_bwd_mx_kernel(LstmBwdArgs args)
         for (int i = 0; i < 4; ++i) {
           const int b = 4 * (lane >> 4) + i;
           const float vn = dpp_f<0xB1>(acc[ct][i]);
-          if (b0 + b < B && (ar & 1) == 0)
+          if (b0 + b < B && (ar & 1) == 0 && !(args.inject == 2 && j == 0 && tt == 0))
             put_pair(xb + ((long)par * B + b0 + b) * xstride_b + (long)dest * (H / 2) + (long)j * (U / 2) + (du >> 1),
                      (unsigned)(tt + 1) & 3u, acc[ct][i], vn, local);
         }

@@ -948,6 +948,46 @@ def test_lstm_handoff_timeout_skips_adamw_and_raises():
     assert not torch.equal(opt.flat, before)
 
 
+@pytest.mark.parametrize("mode,mx", [(1, 2), (2, 2), (2, 0)])
+def test_lstm_handoff_timeout_reports_and_returns(mode, mx):
+    """The hand-off timeout path of the MFMA recurrence (lstm_mx.hip pair granules, forward: mode 1) and
+    of the backward recurrences (mode 2; MFMA and VALU forms): member 0 drops its first hand-off, the
+    waiting members time out, OR the device error flag (which DDP agrees on across ranks) and the
+    launch returns; a clean launch afterwards matches a clean launch before."""
+    from multimodalreactiongeneration_amd import _lib as L
+    from multimodalreactiongeneration_amd import functional as Fn
+    lib = L.load()
+    torch.manual_seed(5)
+    H, B, T = 256, 16, 4
+    w = [torch.nn.Parameter((torch.randn(4 * H, H) * 0.05).to(DEV)) for _ in range(2)]
+    b = [torch.nn.Parameter(torch.zeros(4 * H).to(DEV)) for _ in range(2)]
+    x = torch.randn(B, T, H, device=DEV)
+    err = Fn._err_flag(DEV)
+    prev = lib.mrg_lstm_set_mx(mx, 0)
+
+    def run():
+        for p in w + b:
+            p.grad = None
+        y, _, _ = Fn.lstm_layer(x, w[0], w[1], b[0], b[1])
+        y.square().sum().backward()
+        torch.cuda.synchronize()
+        return y.detach().clone(), w[1].grad.detach().clone()
+    try:
+        y0, g0 = run()
+        assert int(err.item()) == 0
+        L.check(lib.mrg_lstm_debug_inject(mode), "inject")
+        run()
+        assert int(err.item()) != 0
+        err.zero_()
+        y1, g1 = run()
+        assert int(err.item()) == 0
+        assert torch.equal(y1, y0) and torch.equal(g1, g0)
+    finally:
+        lib.mrg_lstm_debug_inject(0)
+        lib.mrg_lstm_set_mx(prev, 0)
+        err.zero_()
+
+
 @pytest.mark.parametrize("M,N,K,epi,n", [(3840, 1024, 256, 0, 11), (3840, 256, 256, 3, 5), (3840, 256, 1024, 3, 16),
                                          (300, 256, 64, 0, 3), (100, 96, 40, 1, 2)])
 def test_batched_gemm_matches_single_products(M, N, K, epi, n, gemm_mode):
