@@ -4,7 +4,7 @@ set -o pipefail
 O=gpurun_out/r04_c
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
-  tests/test_gpu_ops.py tests/test_gpu_models.py -k "query_chunks or block_stack or b64" -s > $O/tests.log 2>&1
+  tests/test_gpu_ops.py tests/test_gpu_models.py -k "query_chunks or block_stack or b64 or timeout_reports" -s > $O/tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 for i in 1 2; do
   for v in 0 1; do
