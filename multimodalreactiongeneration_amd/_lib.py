@@ -36,6 +36,7 @@ SIGNATURES = {
     "mrg_gemm_force_tile": (c_int, [c_int]),
     "mrg_gemm_set_blocks_per_cu": (c_int, [c_int]),
     "mrg_gemm_set_glds": (c_int, [c_int, c_int]),
+    "mrg_gemm_set_wgrad_kernel": (c_int, [c_int]),
     "mrg_gemm_set_glds_wg": (c_int, [c_int]),
     "mrg_transpose_batched": (c_int, [c_int, PP, PP, PI, PI, P]),
     "mrg_split_planes_batched": (c_int, [c_int, PP, PP, PI, PI, PI, P]),

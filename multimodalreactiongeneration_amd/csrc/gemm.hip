@@ -885,6 +885,10 @@ static int g_glds_wg = [] {  // weight-gradient products on gemm_x6g_wgrad_kerne
   const char* e = getenv("MRG_GEMM_GLDS_WG");
   return e ? atoi(e) : 1;
 }();
+static int g_wsp = [] {  // weight gradients on the warp-specialized kernel (gemm_wsp.hip); MRG_GEMM_WSP
+  const char* e = getenv("MRG_GEMM_WSP");
+  return (e && atoi(e) != 0) ? 1 : 0;
+}();
 static int g_glds_bn = [] {  // 64 forces 64-wide column tiles (tuning); 128 = by shape
   const char* e = getenv("MRG_GEMM_GLDS_BN");
   return e ? atoi(e) : 128;
@@ -940,6 +944,13 @@ MRG_API int mrg_gemm_set_mode(int mode) {
 MRG_API int mrg_gemm_get_mode(void) { return g_gemm_mode; }
 
 // Weight-gradient products on the LDS-DMA kernel (1) or the register-staged one (0); returns the old value.
+// Weight-gradient kernel: 1 = warp-specialized (gemm_wsp.hip), 0 = the LDS-DMA form; returns the old one.
+MRG_API int mrg_gemm_set_wgrad_kernel(int wsp) {
+  const int prev = g_wsp;
+  g_wsp = wsp ? 1 : 0;
+  return prev;
+}
+
 MRG_API int mrg_gemm_set_glds_wg(int on) {
   const int prev = g_glds_wg;
   g_glds_wg = on ? 1 : 0;
@@ -1128,8 +1139,9 @@ static int gemm_ex(int mode, int M, int N, int K, float alpha,
                   (K % 32) == 0 && (M % 4) == 0 && (N % 4) == 0 && M >= 64 && N >= 64 && !a.cnt;
   if (wg) {
     tile = 0;
-    launch_x6g_wgrad(a, splits, 128, 128, stream, mode == 2 ? 1 : 3,
-                     g_blocks_per_cu > 0 ? g_blocks_per_cu * resident_cus() : 0);
+    const int cap = g_blocks_per_cu > 0 ? g_blocks_per_cu * resident_cus() : 0;
+    if (g_wsp && mode != 2) launch_x6s_wgrad(a, splits, stream, cap);
+    else launch_x6g_wgrad(a, splits, 128, 128, stream, mode == 2 ? 1 : 3, cap);
   } else if (launch_gemm(mode, a, tile, bk, transA, transB, va, vb, splits, stream)) {
     return 2;
   }

@@ -145,6 +145,10 @@ void launch_x6g(GemmArgs a, int ns, int bm, int bn, hipStream_t s, int planes = 
 // max_grid > 0: at most that many workgroups (a multiple of 8), walking the items
 void launch_x6g_wgrad(GemmArgs a, int splits, int bm, int bn, hipStream_t s, int planes = 3, int max_grid = 0);
 
+// warp-specialized weight-gradient form (gemm_wsp.hip): same contract as launch_x6g_wgrad (x6 only),
+// 128 x 128 tiles, bitwise the same results
+void launch_x6s_wgrad(GemmArgs a, int splits, hipStream_t s, int max_grid = 0);
+
 static constexpr int MRG_TP_MAX = 32;
 struct TransposeBatch {
   int n;

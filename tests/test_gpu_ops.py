@@ -235,6 +235,48 @@ def test_weight_grad_kernels_vs_fp64(rows, N, In, time_shift, wg):
     assert rel_err(gb, ref_b) < 2e-6
 
 
+@pytest.mark.parametrize("rows,N,In,time_shift", [(19200, 1024, 256, False), (64 * 299, 1024, 256, True),
+                                                  (19200, 256, 256, False), (19200, 256, 512, False),
+                                                  (2048, 100, 36, False), (6400, 64, 256, False)])
+def test_weight_grad_specialized_kernel_bitwise(rows, N, In, time_shift):
+    """The warp-specialized weight-gradient kernel (gemm_wsp.hip: splitter waves fill bf16 planes while
+    MFMA waves multiply) gives bitwise the LDS-DMA kernel's dW and fused bias sums (same products and
+    sums in the same order), split-K slabs, ragged tiles and the time-shifted RowMap form included,
+    and matches fp64."""
+    from multimodalreactiongeneration_amd import functional as Fn
+    from multimodalreactiongeneration_amd import _lib as L
+    lib = L.load()
+    g = torch.Generator().manual_seed(rows + 3 * N + In)
+    if time_shift:
+        B_, T_ = 64, 300
+        dy_full, x_full = torch.randn(B_, T_, N, generator=g), torch.randn(B_, T_, In, generator=g)
+        dy, x = dy_full[:, 1:].reshape(-1, N), x_full[:, :-1].reshape(-1, In)
+        dyd, xd = dy_full.to(DEV), x_full.to(DEV)
+        kw = dict(dy_hi=T_ * N, dy_div=T_ - 1, x_hi=T_ * In, x_div=T_ - 1)
+        dyp, xp = Fn._ptr(dyd, N), Fn._ptr(xd)
+    else:
+        dy, x = torch.randn(rows, N, generator=g), torch.randn(rows, In, generator=g)
+        dyd, xd = dy.to(DEV), x.to(DEV)
+        kw = {}
+        dyp, xp = Fn._ptr(dyd), Fn._ptr(xd)
+    gw0, gb0 = torch.randn(N, In, generator=g), torch.randn(N, generator=g)
+    out = []
+    prev = Fn.set_wgrad_stream(False)
+    try:
+        for wsp in (0, 1):
+            old = lib.mrg_gemm_set_wgrad_kernel(wsp)
+            gw, gb = gw0.to(DEV), gb0.to(DEV)
+            Fn._wgrad(dyp, N, xp, In, dy.shape[0], N, In, gw, DEV, gb=gb, keep=(dyd, xd), **kw)
+            torch.cuda.synchronize()
+            lib.mrg_gemm_set_wgrad_kernel(old)
+            out.append((gw.clone(), gb.clone()))
+    finally:
+        Fn.set_wgrad_stream(prev)
+    assert torch.equal(out[1][0], out[0][0]) and torch.equal(out[1][1], out[0][1])
+    assert rel_err(out[1][0], gw0.double() + dy.double().t() @ x.double()) < 2e-6
+    assert rel_err(out[1][1], gb0.double() + dy.double().sum(0)) < 2e-6
+
+
 def _bf16(t):
     return t.to(torch.bfloat16).double()
 
