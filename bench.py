@@ -38,8 +38,10 @@ PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03_pmc_summary.json")
 FAMILIES = {
     "gemm": "gemm_x6g_kernel (LDS-DMA, activation and input-gradient products) + gemm_x6_kernel (weight gradients, "
             "+ splitk_reduce4_kernel): every GEMM of the step, 2MNK FLOP per launch",
-    "lstm_fwd": "lstm_fwd_kernel<256,8,BS>: persistent recurrence, 8H^2 FLOP per (b, t) per layer",
-    "lstm_bwd": "lstm_bwd_kernel<256,8,BS>: persistent reverse recurrence, 8H^2 FLOP per (b, t) per layer",
+    "lstm_fwd": "lstm_fwd_kernel<H,G,BS> (VALU) + lstm_fwd_mx_kernel (MFMA, H=256): persistent recurrence, "
+                "8H^2 FLOP per (b, t) per layer and direction",
+    "lstm_bwd": "lstm_bwd_kernel<H,G,BS> (VALU) + lstm_bwd_mx_kernel (MFMA, H=256): persistent reverse "
+                "recurrence, 8H^2 FLOP per (b, t) per layer and direction",
     "attn_fwd": "attn_fwd_kernel<64>: block-causal flash attention, 4D FLOP per visible (q, k) pair per head",
     "attn_bwd": "attn_bwd_dq_kernel<64> + attn_bwd_dkv_kernel<64>: 10D FLOP per visible pair per head",
 }
