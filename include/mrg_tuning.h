@@ -21,9 +21,10 @@ int mrg_gemm_set_glds(int depth, int bn);
 /* Weight-gradient products (transA 1, transB 0) on the LDS-DMA kernel (1, default) or the
  * register-staged one (0); returns the previous setting.                                        */
 int mrg_gemm_set_glds_wg(int on);
-/* Weight-gradient products on the warp-specialized kernel (1: splitter waves fill bf16 planes while
- * MFMA waves multiply, gemm_wsp.hip; bitwise the LDS-DMA form's results) or the LDS-DMA kernel (0);
- * env MRG_GEMM_WSP; returns the previous setting.                                                */
+/* Warp-specialized x6 kernels (gemm_wsp.hip: splitter waves fill bf16 planes while MFMA waves
+ * multiply; bitwise the LDS-DMA forms' results), a bit mask: 1 = weight-gradient products, 2 = the
+ * k-contiguous products (forward / input gradients, batched too), 0 = the LDS-DMA kernels;
+ * env MRG_GEMM_WSP; returns the previous mask.                                                    */
 int mrg_gemm_set_wgrad_kernel(int wsp);
 /* Three bf16 planes (the x6 split: v ~ p0 + p1 + p2) of n row-major fp32 weights, once per optimizer
  * step: dst_i [3][R'][C'] with (R', C') = (rows_i, cols_i), or (cols_i, rows_i) when transpose_i.   */

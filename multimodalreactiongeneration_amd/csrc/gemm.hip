@@ -887,7 +887,7 @@ static int g_glds_wg = [] {  // weight-gradient products on gemm_x6g_wgrad_kerne
 }();
 static int g_wsp = [] {  // weight gradients on the warp-specialized kernel (gemm_wsp.hip); MRG_GEMM_WSP
   const char* e = getenv("MRG_GEMM_WSP");
-  return (e && atoi(e) != 0) ? 1 : 0;
+  return e ? (atoi(e) & 3) : 0;   // bit 0: weight gradients, bit 1: k-contiguous products
 }();
 static int g_glds_bn = [] {  // 64 forces 64-wide column tiles (tuning); 128 = by shape
   const char* e = getenv("MRG_GEMM_GLDS_BN");
@@ -947,7 +947,7 @@ MRG_API int mrg_gemm_get_mode(void) { return g_gemm_mode; }
 // Weight-gradient kernel: 1 = warp-specialized (gemm_wsp.hip), 0 = the LDS-DMA form; returns the old one.
 MRG_API int mrg_gemm_set_wgrad_kernel(int wsp) {
   const int prev = g_wsp;
-  g_wsp = wsp ? 1 : 0;
+  g_wsp = wsp & 3;
   return prev;
 }
 
@@ -1106,7 +1106,8 @@ static int gemm_ex(int mode, int M, int N, int K, float alpha,
     if (N >= 1024) bm = 128;
     else if (N == 256 && K <= 256) bn = 64;
     if (g_glds_bn == 64) bn = 64;
-    launch_x6g(a, g_glds, bm, bn, stream, mode == 2 ? 1 : 3);
+    if ((g_wsp & 2) && mode != 2) launch_x6s(a, bm, bn, stream);
+    else launch_x6g(a, g_glds, bm, bn, stream, mode == 2 ? 1 : 3);
     return check_launch("gemm_x6g_kernel");
   }
   int tile;  // 0: 128x128, 1: 128x64, 2: 64x64
@@ -1140,7 +1141,7 @@ static int gemm_ex(int mode, int M, int N, int K, float alpha,
   if (wg) {
     tile = 0;
     const int cap = g_blocks_per_cu > 0 ? g_blocks_per_cu * resident_cus() : 0;
-    if (g_wsp && mode != 2) launch_x6s_wgrad(a, splits, stream, cap);
+    if ((g_wsp & 1) && mode != 2) launch_x6s_wgrad(a, splits, stream, cap);
     else launch_x6g_wgrad(a, splits, 128, 128, stream, mode == 2 ? 1 : 3, cap);
   } else if (launch_gemm(mode, a, tile, bk, transA, transB, va, vb, splits, stream)) {
     return 2;
@@ -1250,7 +1251,8 @@ MRG_API int mrg_gemm_x6g_batched(int n, int M, int N, int K, float alpha, const 
   if (N >= 1024) bm = 128;
   else if (N == 256 && K <= 256) bn = 64;
   if (g_glds_bn == 64) bn = 64;
-  launch_x6g(a, g_glds, bm, bn, stream, mode == 2 ? 1 : 3, &gb);
+  if ((g_wsp & 2) && mode != 2) launch_x6s(a, bm, bn, stream, &gb);
+  else launch_x6g(a, g_glds, bm, bn, stream, mode == 2 ? 1 : 3, &gb);
   return check_launch("gemm_x6g_kernel (batched)");
 }
 

@@ -148,6 +148,8 @@ void launch_x6g_wgrad(GemmArgs a, int splits, int bm, int bn, hipStream_t s, int
 // warp-specialized weight-gradient form (gemm_wsp.hip): same contract as launch_x6g_wgrad (x6 only),
 // 128 x 128 tiles, bitwise the same results
 void launch_x6s_wgrad(GemmArgs a, int splits, hipStream_t s, int max_grid = 0);
+// and of the k-contiguous products (launch_x6g's contract, x6 only; bm, bn in {64, 128})
+void launch_x6s(GemmArgs a, int bm, int bn, hipStream_t s, const GemmBatch* gb = nullptr);
 
 static constexpr int MRG_TP_MAX = 32;
 struct TransposeBatch {

@@ -209,6 +209,199 @@ __global__ __launch_bounds__(WT, 1) void gemm_x6s_wgrad_kernel(GemmArgs a) {
   }
 }
 
+// ----------------------------------------------------------------------------------------------
+// The same specialization for the k-contiguous products C = A B^T (+ bias / epilogue): x W^T of
+// nn.Linear / the LSTM input projection, and dY W through the transposed weight copies
+// (mixer_block.py:63-74,237-252, for_sequential.py:42-51).  Splitter thread s owns the k-octet units
+// u = s + 256 q of the (BM + BN) x 4 octets of a k-tile, 4 consecutive threads on one 128-B row
+// piece (coalesced), loads two k-tiles ahead in registers; consumers are a 2 x 2 grid of
+// (BM / 2) x (BN / 2) wave tiles, fragments and six-MFMA order of gemm_x6g_kernel (bitwise equal).
+// One workgroup per output tile (grid = tiles x problems, problem-major like the batched form).
+namespace {
+
+template <int BM, int BN>
+struct FwdUnits {
+  static constexpr int U = (BM + BN) * 4 / 256;      // octet units per splitter thread per k-tile
+  float v[U][8];
+};
+
+template <int BM, int BN>
+__device__ __forceinline__ void fwd_load(const GemmArgs& a, FwdUnits<BM, BN>& r, int kt0, int s, int m0, int n0) {
+#pragma unroll
+  for (int q = 0; q < FwdUnits<BM, BN>::U; ++q) {
+    const int u = s + 256 * q, row = u >> 2, c = u & 3;
+    const bool isa = row < BM;
+    const int gr = isa ? m0 + row : n0 + row - BM;
+    const bool ok = isa ? gr < a.M : gr < a.N;
+    const float* p = isa ? a.A + a.amap.off(ok ? gr : 0) : a.B + a.bmap.off(ok ? gr : 0);
+    p += kt0 + 8 * c;
+    float4 x0 = make_float4(0.f, 0.f, 0.f, 0.f), x1 = x0;
+    if (ok) {
+      x0 = *reinterpret_cast<const float4*>(p);
+      x1 = *reinterpret_cast<const float4*>(p + 4);
+    }
+    r.v[q][0] = x0.x; r.v[q][1] = x0.y; r.v[q][2] = x0.z; r.v[q][3] = x0.w;
+    r.v[q][4] = x1.x; r.v[q][5] = x1.y; r.v[q][6] = x1.z; r.v[q][7] = x1.w;
+  }
+}
+
+// plane buffer: A planes 0..2 ([BM][32 k] bf16 each) then B planes 0..2 ([BN][32 k])
+template <int BM, int BN>
+__device__ __forceinline__ void fwd_store(unsigned char* buf, const FwdUnits<BM, BN>& r, int s) {
+#pragma unroll
+  for (int q = 0; q < FwdUnits<BM, BN>::U; ++q) {
+    const int u = s + 256 * q, row = u >> 2, c = u & 3;
+    const bool isa = row < BM;
+    const int x = isa ? row : row - BM;
+    unsigned char* base = buf + (isa ? 0 : 3 * BM * 64);
+    const int pl = (isa ? BM : BN) * 64;
+    u32x4w p0, p1, p2;
+    split8w(r.v[q], p0, p1, p2);
+    const int off = xo(x, c);
+    *reinterpret_cast<u32x4w*>(base + off) = p0;
+    *reinterpret_cast<u32x4w*>(base + pl + off) = p1;
+    *reinterpret_cast<u32x4w*>(base + 2 * pl + off) = p2;
+  }
+}
+
+}  // namespace
+
+template <int BM, int BN>
+__global__ __launch_bounds__(WT, 1) void gemm_x6s_kernel(GemmArgs a_in, GemmBatch gb) {
+  constexpr int FB = 3 * (BM + BN) * 64;   // one plane buffer
+  constexpr int TM = BM / 64, TN = BN / 64;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * FB > 4 * 32 * (TN * 32 + 4) * 4 ? 2 * FB
+                                                                                               : 4 * 32 * (TN * 32 + 4) * 4];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  GemmArgs a = a_in;
+  if (gb.n > 0) {
+    const int p = t / a.tiles_mn;
+    t -= p * a.tiles_mn;
+    a.A = gb.A[p]; a.B = gb.B[p]; a.C = gb.C[p]; a.bias = gb.bias[p]; a.aux = gb.aux[p];
+  }
+  const int m0 = (t / a.tiles_n) * BM, n0 = (t % a.tiles_n) * BN;
+  const int nk = a.K / 32;
+  if (wave >= 4) {
+    const int s = tid - 256;
+    FwdUnits<BM, BN> r0, r1;
+    if (nk > 0) fwd_load<BM, BN>(a, r0, 0, s, m0, n0);
+    if (nk > 1) fwd_load<BM, BN>(a, r1, 32, s, m0, n0);
+    if (nk > 0) fwd_store<BM, BN>(lds, r0, s);
+    if (nk > 2) fwd_load<BM, BN>(a, r0, 64, s, m0, n0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; kt += 2) {
+      if (kt + 1 < nk) {
+        fwd_store<BM, BN>(lds + FB, r1, s);
+        if (kt + 3 < nk) fwd_load<BM, BN>(a, r1, 32 * (kt + 3), s, m0, n0);
+      }
+      __syncthreads();
+      if (kt + 1 >= nk) break;
+      if (kt + 2 < nk) {
+        fwd_store<BM, BN>(lds, r0, s);
+        if (kt + 4 < nk) fwd_load<BM, BN>(a, r0, 32 * (kt + 4), s, m0, n0);
+      }
+      __syncthreads();
+    }
+    return;   // the consumers' epilogue needs no barrier with the splitters past the last k-tile
+  }
+  const int wm = (wave >> 1) * (BM / 2), wn = (wave & 1) * (BN / 2);
+  const int lr = lane & 31, lh = lane >> 5;
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const unsigned char* buf = lds + (kt & 1) * FB;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 fa[TM][3], fb[TN][3];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int off = xo(wm + 32 * i + lr, 2 * s + lh);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) fa[i][p] = *reinterpret_cast<const bf16x8*>(buf + p * BM * 64 + off);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int off = xo(wn + 32 * j + lr, 2 * s + lh);
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          fb[j][p] = *reinterpret_cast<const bf16x8*>(buf + 3 * BM * 64 + p * BN * 64 + off);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma6(fb[j], fa[i], acc[i][j]);
+    }
+    __syncthreads();
+  }
+  // epilogue: 128-wide wave tiles stage 32 rows in LDS (whole 256-B row runs); 64-wide ones store
+  // straight from the accumulators (gemm_x6g_kernel's two forms).  The planes are free (every
+  // splitter has passed the last barrier and writes no more).
+  if constexpr (BN >= 128) {
+    constexpr int WC = TN * 32, PITCH = WC + 4, C4 = WC / 4;
+    float* stg = reinterpret_cast<float*>(lds) + wave * 32 * PITCH;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4)
+          *reinterpret_cast<float4*>(stg + lr * PITCH + j * 32 + 8 * r4 + 4 * lh) =
+              make_float4(acc[i][j][4 * r4], acc[i][j][4 * r4 + 1], acc[i][j][4 * r4 + 2], acc[i][j][4 * r4 + 3]);
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int it = 0; it < 32 * C4 / 64; ++it) {
+        const int qq = lane + 64 * it, row = qq / C4, c4 = qq % C4;
+        const float4 v = *reinterpret_cast<const float4*>(stg + row * PITCH + 4 * c4);
+        const int m = m0 + wm + i * 32 + row;
+        if (m < a.M) store4(a, 0, m, n0 + wn + 4 * c4, v);
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wm + i * 32 + lr;
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) {
+          const int n = n0 + wn + j * 32 + 8 * r4 + 4 * lh;
+          const float4 v = make_float4(acc[i][j][4 * r4], acc[i][j][4 * r4 + 1], acc[i][j][4 * r4 + 2],
+                                       acc[i][j][4 * r4 + 3]);
+          if (m < a.M) store4(a, 0, m, n, v);
+        }
+    }
+  }
+}
+
+void launch_x6s(GemmArgs a, int bm, int bn, hipStream_t s, const GemmBatch* gbp) {
+  GemmBatch none;
+  none.n = 0;
+  const GemmBatch& gb = gbp ? *gbp : none;
+  auto go = [&](auto kern, int BM_, int BN_) {
+    a.tiles_n = (a.N + BN_ - 1) / BN_;
+    a.tiles_mn = a.tiles_n * ((a.M + BM_ - 1) / BM_);
+    a.ntiles = a.tiles_mn;
+    a.nsplit = 1;
+    a.ws = nullptr;
+    klaunch(kern, (unsigned)a.tiles_mn * (unsigned)(gb.n > 0 ? gb.n : 1), WT, 0, s, a, gb);
+  };
+  if (bm == 128 && bn == 128) go(gemm_x6s_kernel<128, 128>, 128, 128);
+  else if (bm == 128) go(gemm_x6s_kernel<128, 64>, 128, 64);
+  else if (bn == 128) go(gemm_x6s_kernel<64, 128>, 64, 128);
+  else go(gemm_x6s_kernel<64, 64>, 64, 64);
+}
+
 void launch_x6s_wgrad(GemmArgs a, int splits, hipStream_t s, int max_grid) {
   a.tiles_n = (a.N + TBN - 1) / TBN;
   a.tiles_mn = a.tiles_n * ((a.M + TBM - 1) / TBM);

@@ -1065,6 +1065,54 @@ def test_batched_gemm_matches_single_products(M, N, K, epi, n, gemm_mode):
         assert rel_err(Cs[i], exact) < TOL
 
 
+@pytest.mark.parametrize("M,N,K,epi,beta,n", [(19200, 1024, 256, 0, 0.0, 1), (19200, 256, 256, 3, 0.0, 1),
+                                              (19200, 512, 256, 1, 0.0, 1), (19200, 256, 1024, 3, 1.0, 1),
+                                              (2100, 256, 512, 2, 0.0, 1), (6400, 1024, 256, 0, 0.0, 3),
+                                              (6400, 256, 256, 3, 1.0, 4)])
+def test_specialized_products_bitwise(M, N, K, epi, beta, n):
+    """The warp-specialized k-contiguous product kernel (gemm_wsp.hip, mrg_gemm_set_wgrad_kernel bit 2)
+    gives bitwise the LDS-DMA kernel's C = epi(A W^T + beta C + bias) for every tile shape the
+    dispatcher picks (128x128 at N >= 1024, 64x64 at N = K = 256, else 64x128), ragged M, every
+    epilogue, accumulation into C, and the batched form."""
+    import ctypes
+    from multimodalreactiongeneration_amd import _lib as L
+    from multimodalreactiongeneration_amd import functional as Fn
+    lib = L.load()
+    g = torch.Generator().manual_seed(M + N + K + n + epi)
+    As = [torch.randn(M, K, generator=g).to(DEV) for _ in range(n)]
+    Ws = [(torch.randn(N, K, generator=g) / math.sqrt(K)).to(DEV) for _ in range(n)]
+    bs = [torch.randn(N, generator=g).to(DEV) for _ in range(n)]
+    aux = [torch.randn(M, N, generator=g).to(DEV) for _ in range(n)] if epi >= 2 else None
+    C0 = [torch.randn(M, N, generator=g).to(DEV) for _ in range(n)]
+    VP = ctypes.c_void_p
+    arr = lambda v: (VP * n)(*[VP(t.data_ptr()) for t in v])  # noqa: E731
+    out = []
+    for wsp in (0, 2):
+        old = lib.mrg_gemm_set_wgrad_kernel(wsp)
+        Cs = [c.clone() for c in C0]
+        if n == 1:
+            L.check(lib.mrg_gemm_f32_ex(M, N, K, 1.0, VP(As[0].data_ptr()), 0, K, 0, 0, VP(Ws[0].data_ptr()), 1, K, 0,
+                                        0, beta, VP(Cs[0].data_ptr()), N, VP(bs[0].data_ptr()), epi,
+                                        None if aux is None else VP(aux[0].data_ptr()), N, None, 1, None, None, 0.0,
+                                        None, Fn._stream()), "single")
+        else:
+            L.check(lib.mrg_gemm_x6g_batched(n, M, N, K, 1.0, arr(As), K, arr(Ws), K, beta, arr(Cs), N, arr(bs), epi,
+                                             None if aux is None else arr(aux), N, 0, Fn._stream()), "batched")
+        torch.cuda.synchronize()
+        lib.mrg_gemm_set_wgrad_kernel(old)
+        out.append(Cs)
+    for i in range(n):
+        assert torch.equal(out[1][i], out[0][i]), i
+        exact = As[i].double() @ Ws[i].double().T + bs[i].double() + beta * C0[i].double()
+        if epi == 1:
+            exact = exact.clamp_min(0)
+        elif epi == 2:
+            exact = exact * (aux[i].double() > 0)
+        elif epi == 3:
+            exact = exact + aux[i].double()
+        assert rel_err(out[1][i], exact) < TOL
+
+
 @pytest.mark.parametrize("n,rows,E", [(11, 3840, 256), (3, 70, 512), (16, 32, 36)])
 def test_batched_layernorm_matches_single(n, rows, E):
     """mrg_residual_layernorm_{fwd,bwd}_batched: each problem bitwise equal to the row-mapped single
