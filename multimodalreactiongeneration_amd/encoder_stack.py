@@ -45,9 +45,9 @@ from .functional import _ptr, _stream, gemm, _dx_gemm, _wt_note, _gbuf, _on_side
 # gradients run beside the backward recurrences (longer recurrences leave them more room): A/B on one
 # box 50 / 60 / 75 / 100 / 150 / 300 -> 21.80 / 21.68 / 21.53 / 21.29 / 21.55 / 23.05 ms/step (r03)
 # weight gradients per (layer, chunk) as each chunk's backward completes (1), or per layer once its
-# chunk 0 is done (0): the per-chunk form starts the products diagonals earlier, so fewer of them are
-# left for the end of the backward, where no recurrence is left to hide them
-CHUNK_WGRAD = os.environ.get("MRG_STACK_CHUNK_WGRAD", "1") == "1"
+# chunk 0 is done (0, default).  The per-chunk form starts the products diagonals earlier but issues
+# three times as many (smaller) products: measured 22.47 vs 21.15 ms/step (r04, A/B on one box)
+CHUNK_WGRAD = os.environ.get("MRG_STACK_CHUNK_WGRAD", "0") == "1"
 # one side-stream fork per weight-gradient product instead of one per layer (a capture regression case:
 # tests/test_gpu_capture.py)
 SPLIT_FORKS = os.environ.get("MRG_STACK_SPLIT_FORKS", "0") == "1"
