@@ -63,15 +63,42 @@ struct Octets {
   float a[2][8], b[2][8];
 };
 
-__device__ __forceinline__ void load_tile(const GemmArgs& a, Octets& r, int kt0, int kh, int x, int m0, int n0) {
-  const bool am = m0 + x < a.M, bn = n0 + x < a.N;
+// Rows past the edge load the last row (straight-line loads, no branches: the compiler then keeps
+// every load of both tiles in flight); their products land in outputs that are never stored.
+// MAPPED = 0: plain rows (off(k) = k ld); 1: two-level RowMaps (the time-shifted dW_hh operands),
+// offsets stepped through the 8 k of an octet from one division, branch-free.
+template <bool MAPPED>
+__device__ __forceinline__ void octet_off(const RowMap& m, int k0, long (&off)[8]) {
+  if constexpr (!MAPPED) {
 #pragma unroll
-  for (int o = 0; o < 2; ++o) {
+    for (int j = 0; j < 8; ++j) off[j] = (long)(k0 + j) * m.ld_lo;
+  } else {
+    const int rd = m.rdiv > 0 ? m.rdiv : 0x7fffffff;
+    int q = k0 / rd, r = k0 - q * rd;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int k = kt0 + 8 * (kh + 2 * o) + j;
-      r.a[o][j] = am ? a.A[a.amap.off(k) + m0 + x] : 0.0f;
-      r.b[o][j] = bn ? a.B[a.bmap.off(k) + n0 + x] : 0.0f;
+      off[j] = (long)q * m.ld_hi + (long)r * m.ld_lo;
+      const bool wrap = r + 1 == rd;
+      r = wrap ? 0 : r + 1;
+      q = wrap ? q + 1 : q;
+    }
+  }
+}
+
+template <bool MAPPED>
+__device__ __forceinline__ void load_tile(const GemmArgs& a, Octets& r, int kt0, int kh, int x, int m0, int n0) {
+  const float* pa = a.A + min(m0 + x, a.M - 1);
+  const float* pb = a.B + min(n0 + x, a.N - 1);
+#pragma unroll
+  for (int o = 0; o < 2; ++o) {
+    const int k0 = kt0 + 8 * (kh + 2 * o);
+    long oa[8], ob[8];
+    octet_off<MAPPED>(a.amap, k0, oa);
+    octet_off<MAPPED>(a.bmap, k0, ob);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      r.a[o][j] = pa[oa[j]];
+      r.b[o][j] = pb[ob[j]];
     }
   }
 }
@@ -92,12 +119,21 @@ __device__ __forceinline__ void store_planes(unsigned char* buf, const Octets& r
   }
 }
 
+// a workgroup barrier the compiler may not schedule work across (it otherwise hoists the next half's
+// split above the barrier, which needs that half's loads: vmcnt(0) where vmcnt(4) would do)
+__device__ __forceinline__ void fenced_sync() {
+  __builtin_amdgcn_sched_barrier(0);
+  __syncthreads();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 __device__ __forceinline__ float octet_sum(const float (&v)[8]) {  // gemm_glds.hip's tree
   return ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
 }
 
 }  // namespace
 
+template <bool MAPPED>
 __global__ __launch_bounds__(WT, 1) void gemm_x6s_wgrad_kernel(GemmArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned char lds[2 * PB];
   __shared__ float rsum[TBM];
@@ -111,38 +147,41 @@ __global__ __launch_bounds__(WT, 1) void gemm_x6s_wgrad_kernel(GemmArgs a) {
     const int m0 = (tr / a.tiles_n) * TBM, n0 = (tr % a.tiles_n) * TBN;
     const int kbeg = z * a.kchunk, kend = min(a.K, kbeg + a.kchunk);
     const int nk = (kend - kbeg) / 32;
+    if (nk <= 0) continue;   // (uniform across the workgroup)
     if (splitter) {
-      const int s = tid - 256, x = s & 127, kh = s >> 7;
+      // branch-free k-tile pairs: loads past the last k-tile re-read it and stores past it fill the
+      // buffer nobody reads that half, so the compiler keeps both tiles' loads in flight (counted
+      // vmcnt waits instead of vmcnt(0) at every branch join)
+      const int s = tid - 256, x = s & 127, kh = __builtin_amdgcn_readfirstlane(s >> 7);   // wave-uniform
       const bool do_asum = a.asum && n0 == 0;
+      const int last = kbeg + 32 * (nk - 1);
       float cs = 0.0f;
       Octets r0, r1;
-      if (nk > 0) load_tile(a, r0, kbeg, kh, x, m0, n0);
-      if (nk > 1) load_tile(a, r1, kbeg + 32, kh, x, m0, n0);
-      if (nk > 0) {
-        if (do_asum) { cs += octet_sum(r0.a[0]); cs += octet_sum(r0.a[1]); }
-        store_planes(lds, r0, kh, x);
-      }
-      if (nk > 2) load_tile(a, r0, kbeg + 64, kh, x, m0, n0);
-      __syncthreads();
-      // k-tile kt + 1 into buffer (kt + 1) & 1 while the consumers multiply kt; two tiles in flight
+      load_tile<MAPPED>(a, r0, kbeg, kh, x, m0, n0);
+      load_tile<MAPPED>(a, r1, min(kbeg + 32, last), kh, x, m0, n0);
+      if (do_asum) { cs += octet_sum(r0.a[0]); cs += octet_sum(r0.a[1]); }
+      store_planes(lds, r0, kh, x);
+      load_tile<MAPPED>(a, r0, min(kbeg + 64, last), kh, x, m0, n0);
+      fenced_sync();
       for (int kt = 0; kt < nk; kt += 2) {
-        if (kt + 1 < nk) {
-          if (do_asum) { cs += octet_sum(r1.a[0]); cs += octet_sum(r1.a[1]); }
-          store_planes(lds + PB, r1, kh, x);
-          if (kt + 3 < nk) load_tile(a, r1, kbeg + 32 * (kt + 3), kh, x, m0, n0);
+        if (do_asum) {
+          const float t0 = octet_sum(r1.a[0]), t1 = octet_sum(r1.a[1]);
+          cs = kt + 1 < nk ? (cs + t0) + t1 : cs;
         }
-        __syncthreads();
-        if (kt + 1 >= nk) break;
-        if (kt + 2 < nk) {
-          if (do_asum) { cs += octet_sum(r0.a[0]); cs += octet_sum(r0.a[1]); }
-          store_planes(lds, r0, kh, x);
-          if (kt + 4 < nk) load_tile(a, r0, kbeg + 32 * (kt + 4), kh, x, m0, n0);
+        store_planes(lds + PB, r1, kh, x);
+        load_tile<MAPPED>(a, r1, min(kbeg + 32 * (kt + 3), last), kh, x, m0, n0);
+        fenced_sync();
+        if (do_asum) {
+          const float t0 = octet_sum(r0.a[0]), t1 = octet_sum(r0.a[1]);
+          cs = kt + 2 < nk ? (cs + t0) + t1 : cs;
         }
-        __syncthreads();
+        store_planes(lds, r0, kh, x);
+        load_tile<MAPPED>(a, r0, min(kbeg + 32 * (kt + 4), last), kh, x, m0, n0);
+        fenced_sync();
       }
       // bias gradient partial: row x = (k-half 0 sum) + (k-half 1 sum), as lanes l and l + 32 combine
       if (do_asum && kh == 1) rsum[x] = cs;
-      __syncthreads();
+      fenced_sync();
       if (do_asum && kh == 0 && m0 + x < a.M) a.asum[(long)z * a.M + m0 + x] = cs + rsum[x];
     } else {
       const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
@@ -155,27 +194,29 @@ __global__ __launch_bounds__(WT, 1) void gemm_x6s_wgrad_kernel(GemmArgs a) {
 #pragma unroll
           for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
       __syncthreads();
-      for (int kt = 0; kt < nk; ++kt) {
-        const unsigned char* buf = lds + (kt & 1) * PB;
+      for (int kt = 0; kt < nk + (nk & 1); ++kt) {   // k-tile pairs, as the splitters
+        if (kt < nk) {
+          const unsigned char* buf = lds + (kt & 1) * PB;
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          bf16x8 fa[2][3], fb[2][3];
+          for (int s = 0; s < 2; ++s) {
+            bf16x8 fa[2][3], fb[2][3];
 #pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            const int off = xo(wm + 32 * i + lr, 2 * s + lh);
+            for (int i = 0; i < 2; ++i) {
+              const int off = xo(wm + 32 * i + lr, 2 * s + lh);
 #pragma unroll
-            for (int p = 0; p < 3; ++p) fa[i][p] = *reinterpret_cast<const bf16x8*>(buf + p * PL + off);
+              for (int p = 0; p < 3; ++p) fa[i][p] = *reinterpret_cast<const bf16x8*>(buf + p * PL + off);
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const int off = xo(wn + 32 * j + lr, 2 * s + lh);
+#pragma unroll
+              for (int p = 0; p < 3; ++p) fb[j][p] = *reinterpret_cast<const bf16x8*>(buf + (3 + p) * PL + off);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+              for (int j = 0; j < 2; ++j) acc[i][j] = mfma6(fb[j], fa[i], acc[i][j]);
           }
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const int off = xo(wn + 32 * j + lr, 2 * s + lh);
-#pragma unroll
-            for (int p = 0; p < 3; ++p) fb[j][p] = *reinterpret_cast<const bf16x8*>(buf + (3 + p) * PL + off);
-          }
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) acc[i][j] = mfma6(fb[j], fa[i], acc[i][j]);
         }
         __syncthreads();
       }
@@ -225,21 +266,26 @@ struct FwdUnits {
   float v[U][8];
 };
 
+// the U operand rows' k-octet base pointers of splitter thread s (edge rows: the last row), once per tile
 template <int BM, int BN>
-__device__ __forceinline__ void fwd_load(const GemmArgs& a, FwdUnits<BM, BN>& r, int kt0, int s, int m0, int n0) {
+__device__ __forceinline__ void fwd_rows(const GemmArgs& a, const float* (&rp)[FwdUnits<BM, BN>::U], int s, int m0,
+                                         int n0) {
 #pragma unroll
   for (int q = 0; q < FwdUnits<BM, BN>::U; ++q) {
     const int u = s + 256 * q, row = u >> 2, c = u & 3;
     const bool isa = row < BM;
-    const int gr = isa ? m0 + row : n0 + row - BM;
-    const bool ok = isa ? gr < a.M : gr < a.N;
-    const float* p = isa ? a.A + a.amap.off(ok ? gr : 0) : a.B + a.bmap.off(ok ? gr : 0);
-    p += kt0 + 8 * c;
-    float4 x0 = make_float4(0.f, 0.f, 0.f, 0.f), x1 = x0;
-    if (ok) {
-      x0 = *reinterpret_cast<const float4*>(p);
-      x1 = *reinterpret_cast<const float4*>(p + 4);
-    }
+    const int gr = isa ? min(m0 + row, a.M - 1) : min(n0 + row - BM, a.N - 1);
+    rp[q] = (isa ? a.A + a.amap.off(gr) : a.B + a.bmap.off(gr)) + 8 * c;
+  }
+}
+
+template <int BM, int BN>
+__device__ __forceinline__ void fwd_load(const float* const (&rp)[FwdUnits<BM, BN>::U], FwdUnits<BM, BN>& r, int kt0) {
+#pragma unroll
+  for (int q = 0; q < FwdUnits<BM, BN>::U; ++q) {
+    const float* p = rp[q] + kt0;
+    const float4 x0 = *reinterpret_cast<const float4*>(p);
+    const float4 x1 = *reinterpret_cast<const float4*>(p + 4);
     r.v[q][0] = x0.x; r.v[q][1] = x0.y; r.v[q][2] = x0.z; r.v[q][3] = x0.w;
     r.v[q][4] = x1.x; r.v[q][5] = x1.y; r.v[q][6] = x1.z; r.v[q][7] = x1.w;
   }
@@ -283,26 +329,24 @@ __global__ __launch_bounds__(WT, 1) void gemm_x6s_kernel(GemmArgs a_in, GemmBatc
   }
   const int m0 = (t / a.tiles_n) * BM, n0 = (t % a.tiles_n) * BN;
   const int nk = a.K / 32;
-  if (wave >= 4) {
-    const int s = tid - 256;
+  if (nk <= 0) return;
+  if (wave >= 4) {   // branch-free k-tile pairs (see gemm_x6s_wgrad_kernel)
+    const int s = tid - 256, last = 32 * (nk - 1);
+    const float* rp[FwdUnits<BM, BN>::U];
+    fwd_rows<BM, BN>(a, rp, s, m0, n0);
     FwdUnits<BM, BN> r0, r1;
-    if (nk > 0) fwd_load<BM, BN>(a, r0, 0, s, m0, n0);
-    if (nk > 1) fwd_load<BM, BN>(a, r1, 32, s, m0, n0);
-    if (nk > 0) fwd_store<BM, BN>(lds, r0, s);
-    if (nk > 2) fwd_load<BM, BN>(a, r0, 64, s, m0, n0);
-    __syncthreads();
+    fwd_load<BM, BN>(rp, r0, 0);
+    fwd_load<BM, BN>(rp, r1, min(32, last));
+    fwd_store<BM, BN>(lds, r0, s);
+    fwd_load<BM, BN>(rp, r0, min(64, last));
+    fenced_sync();
     for (int kt = 0; kt < nk; kt += 2) {
-      if (kt + 1 < nk) {
-        fwd_store<BM, BN>(lds + FB, r1, s);
-        if (kt + 3 < nk) fwd_load<BM, BN>(a, r1, 32 * (kt + 3), s, m0, n0);
-      }
-      __syncthreads();
-      if (kt + 1 >= nk) break;
-      if (kt + 2 < nk) {
-        fwd_store<BM, BN>(lds, r0, s);
-        if (kt + 4 < nk) fwd_load<BM, BN>(a, r0, 32 * (kt + 4), s, m0, n0);
-      }
-      __syncthreads();
+      fwd_store<BM, BN>(lds + FB, r1, s);
+      fwd_load<BM, BN>(rp, r1, min(32 * (kt + 3), last));
+      fenced_sync();
+      fwd_store<BM, BN>(lds, r0, s);
+      fwd_load<BM, BN>(rp, r0, min(32 * (kt + 4), last));
+      fenced_sync();
     }
     return;   // the consumers' epilogue needs no barrier with the splitters past the last k-tile
   }
@@ -316,28 +360,30 @@ __global__ __launch_bounds__(WT, 1) void gemm_x6s_kernel(GemmArgs a_in, GemmBatc
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
   __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const unsigned char* buf = lds + (kt & 1) * FB;
+  for (int kt = 0; kt < nk + (nk & 1); ++kt) {
+    if (kt < nk) {
+      const unsigned char* buf = lds + (kt & 1) * FB;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 fa[TM][3], fb[TN][3];
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 fa[TM][3], fb[TN][3];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int off = xo(wm + 32 * i + lr, 2 * s + lh);
+        for (int i = 0; i < TM; ++i) {
+          const int off = xo(wm + 32 * i + lr, 2 * s + lh);
 #pragma unroll
-        for (int p = 0; p < 3; ++p) fa[i][p] = *reinterpret_cast<const bf16x8*>(buf + p * BM * 64 + off);
+          for (int p = 0; p < 3; ++p) fa[i][p] = *reinterpret_cast<const bf16x8*>(buf + p * BM * 64 + off);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int off = xo(wn + 32 * j + lr, 2 * s + lh);
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+            fb[j][p] = *reinterpret_cast<const bf16x8*>(buf + 3 * BM * 64 + p * BN * 64 + off);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma6(fb[j], fa[i], acc[i][j]);
       }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int off = xo(wn + 32 * j + lr, 2 * s + lh);
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-          fb[j][p] = *reinterpret_cast<const bf16x8*>(buf + 3 * BM * 64 + p * BN * 64 + off);
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma6(fb[j], fa[i], acc[i][j]);
     }
     __syncthreads();
   }
@@ -409,7 +455,8 @@ void launch_x6s_wgrad(GemmArgs a, int splits, hipStream_t s, int max_grid) {
   a.nsplit = splits;
   unsigned grid = (unsigned)a.ntiles;
   if (max_grid > 0 && grid > (unsigned)max_grid) grid = (unsigned)max_grid & ~7u ? (unsigned)max_grid & ~7u : 8u;
-  klaunch(gemm_x6s_wgrad_kernel, grid, WT, 0, s, a);
+  if (a.amap.rdiv > 0 || a.bmap.rdiv > 0) klaunch(gemm_x6s_wgrad_kernel<true>, grid, WT, 0, s, a);
+  else klaunch(gemm_x6s_wgrad_kernel<false>, grid, WT, 0, s, a);
 }
 
 }  // namespace mrg

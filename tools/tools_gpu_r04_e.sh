@@ -16,6 +16,10 @@ for i in 1 2; do
     echo "block_stack=$v run $i: $(grep -o '"ms_per_step": [0-9.]*' $O/bench_bs$v.$i.log | head -1)"
   done
 done
+for c in 75 150; do
+  MRG_BLOCK_CHUNK=$c timeout -k 10 300 python -u bench.py --secondary 0 --cpu-baseline 0 --steps 30 > $O/bench_chunk$c.log 2>&1 || exit $?
+  echo "block_chunk=$c: $(grep -o '"ms_per_step": [0-9.]*' $O/bench_chunk$c.log | head -1)"
+done
 cd /tmp
 for v in 0 1; do
   MRG_BLOCK_STACK=$v timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_bs$v -o run -- \
