@@ -47,6 +47,7 @@ from .functional import _ptr, _stream, gemm, _dx_gemm, _wt_note, _gbuf, _on_side
 # time steps per chunk; MRG_BLOCK_CHUNK overrides (0 turns the wavefront off: per-block schedule)
 CHUNK = int(os.environ.get("MRG_BLOCK_CHUNK", "100"))
 _BMAX = 16
+RUNS = [0]   # forward passes through the wavefront (tests check the schedule they compare really ran)
 
 # per block: LSTM block (w_ih, w_hh, b_ih, b_hh, ln1 w, ln1 b, ff w, ff b, ln2 w, ln2 b),
 # per integrator (in_w, in_b, out_w, out_b, ln1 w, ln1 b, ff w, ff b, ln2 w, ln2 b),
@@ -104,18 +105,19 @@ class _Block:
 
 class _BlockStackFn(Function):
     """spec = (nblocks, n integrators, heads, causal, eps, chunk, sinks); tensors = x [B, T, E],
-    kv_0..kv_{n-1}, qpad, kpad_0..kpad_{n-1} (uint8 or None), then per block 10 + 10 n + 2 + 6
-    parameters.  Returns the last block's output [B, T, E] (batch-major)."""
+    kv_0..kv_{n-1}, qpad_0..qpad_{n-1}, kpad_0..kpad_{n-1} (uint8 or None, one mask per integrator),
+    then per block 10 + 10 n + 2 + 6 parameters.  Returns the last block's output [B, T, E]."""
 
     @staticmethod
     @Fn._keeps_precision
     def forward(ctx, spec, x, *t):
         nb, n, heads, causal, eps, tc, sinks = spec
+        RUNS[0] += 1
         kvs = list(t[:n])
-        qpad = t[n]
-        kpads = list(t[n + 1:2 * n + 1])
+        qpads = list(t[n:2 * n])
+        kpads = list(t[2 * n:3 * n])
         per = _PL + _PI * n + 2 + _PF
-        pr = t[2 * n + 1:]
+        pr = t[3 * n:]
         blocks = [_Block(pr[per * k:per * (k + 1)], n) for k in range(nb)]
         _lib.require_device(x)
         lib = _lib.load()
@@ -166,7 +168,7 @@ class _BlockStackFn(Function):
 
         ck = _chunks(T, tc)
         pool = _RingPool(sum(1 for _ in ck) * nb, lib.mrg_lstm_fwd_xbuf_bytes(B, E) // 8, dev)
-        pads = [_ptr(qpad) if causal else None] + [_ptr(kp) if causal else None for kp in kpads]
+        pads = [(_ptr(qp) if causal else None, _ptr(kp) if causal else None) for qp, kp in zip(qpads, kpads)]
         for d in range(nb + len(ck) - 1):
             probs = [(k, c, ck[c][0], ck[c][1]) for k in range(nb) for c in [d - k] if 0 <= c < len(ck)]
             _BlockStackFn._fwd_diagonal(lib, probs, blocks, S, KV, Tks, pads, B, T, E, n, heads, causal, scale, eps,
@@ -174,7 +176,7 @@ class _BlockStackFn(Function):
 
         y = torch.empty(B, T, E, **f32)
         _lib.check(lib.mrg_swap01(T, B, E, _ptr(S[-1]["out"]), _ptr(y), 0.0, _stream()), "swap01")
-        ctx.save_for_backward(x, *kv2, *[qpad, *kpads])
+        ctx.save_for_backward(x, *kv2, *qpads, *kpads)
         ctx.blocks, ctx.S, ctx.KV, ctx.Tks, ctx.pads = blocks, S, KV, Tks, pads
         ctx.spec = (nb, n, heads, causal, eps, tc, sinks, B, T, E, Hb, scale)
         ctx.kv_need = [ctx.needs_input_grad[2 + i] for i in range(n)]
@@ -215,7 +217,7 @@ class _BlockStackFn(Function):
                         rc = lib.mrg_attention_fwd_chunk(
                             B, heads, t1 - t0, Tk, D, t0, T, _p(S[k]["Q"][i], t0 * B * E), E, B * E,
                             _ptr(KV[k][i]), Tk * 2 * E, 2 * E, _p(KV[k][i], E), Tk * 2 * E, 2 * E,
-                            _p(S[k]["O"][i], t0 * B * E), E, B * E, _ptr(lse), pads[0], pads[1 + i], int(causal),
+                            _p(S[k]["O"][i], t0 * B * E), E, B * E, _ptr(lse), pads[i][0], pads[i][1], int(causal),
                             scale, _stream())
                     _lib.check(rc, "attention fwd chunk (block stack)")
             _bgemm(lib, N, E, E, [(_p(S[k]["O"][i], r0 * E), blocks[k].integ[i][2], _p(S[k]["A"][i], r0 * E),
@@ -357,7 +359,7 @@ class _BlockStackFn(Function):
                         rc = lib.mrg_attention_bwd_chunk(
                             B, heads, t1 - t0, Tk, D, t0, T, _p(S[k]["Q"][i], t0 * B * E), E, B * E,
                             _ptr(KV[k][i]), Tk * 2 * E, 2 * E, _p(KV[k][i], E), Tk * 2 * E, 2 * E,
-                            _p(S[k]["O"][i], t0 * B * E), E, B * E, _ptr(S[k]["lse"][(i, c)]), pads[0], pads[1 + i],
+                            _p(S[k]["O"][i], t0 * B * E), E, B * E, _ptr(S[k]["lse"][(i, c)]), pads[i][0], pads[i][1],
                             int(causal), scale, _p(G[k]["dO"][i], t0 * B * E), E, B * E,
                             _p(G[k]["dQ"][i], t0 * B * E), E, B * E, _ptr(G[k]["dKV"][i]), Tk * 2 * E, 2 * E,
                             _p(G[k]["dKV"][i], E), Tk * 2 * E, 2 * E, acc, _ptr(ws), _stream())
@@ -466,12 +468,13 @@ def _chunk_pairs(t0, t1, T, Tk, causal):
     return sum(i // r + 1 for i in range(t0, t1))
 
 
-def block_stack(x, kvs, qpad, kpads, blocks: Sequence[Sequence[torch.Tensor]], heads, causal, eps, sinks,
+def block_stack(x, kvs, qpads, kpads, blocks: Sequence[Sequence[torch.Tensor]], heads, causal, eps, sinks,
                 chunk: int = 0) -> torch.Tensor:
     """Blocks 1.. of the metaformer as one (block, chunk) wavefront op; see the module docstring.
-    blocks[k] = the 10 + 10 n + 2 + 6 parameters of block k (_Block order)."""
+    blocks[k] = the 10 + 10 n + 2 + 6 parameters of block k (_Block order); qpads / kpads: each
+    integrator's padding flags (gen_attention_mask's per-modality masks)."""
     n = len(kvs)
-    flat = [x, *kvs, qpad, *kpads]
+    flat = [x, *kvs, *qpads, *kpads]
     for b in blocks:
         flat += list(b)
     return _BlockStackFn.apply((len(blocks), n, int(heads), bool(causal), float(eps), int(chunk or CHUNK),

@@ -391,12 +391,12 @@ class MultiModalMetaformer(nn.Module):
             flat.append([*layer, *[t for p in params for t in p], cw, cb, mods[0].weight, mods[0].bias,
                          mods[2].weight, mods[2].bias, ff.layer_norm.weight, ff.layer_norm.bias])
         heads, causal, qpads, kpads, om = fa0
-        if len(eps_all) != 1 or any(q is not qpads[0] for q in qpads):
+        if len(eps_all) != 1:
             return None
         if x.shape[2] // heads not in (8, 16, 32, 64):
             return None
         sinks = [getattr(kv, "_mrg_kv_sink", None) for kv in om]
-        return block_stack(x, list(om), qpads[0], kpads, flat, heads, causal, eps_all.pop(), sinks)
+        return block_stack(x, list(om), qpads, kpads, flat, heads, causal, eps_all.pop(), sinks)
 
     def _fast_eligible(self) -> bool:
         if self.interlayer_residual:

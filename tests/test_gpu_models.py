@@ -751,10 +751,12 @@ def test_block_stack_matches_per_block_schedule(chunk, ratio, B, T):
             m.metaformer.use_block_stack = use
             for p in m.parameters():
                 p.grad = None
+            runs = BS.RUNS[0]
             y = m(*clone_batch(batch, DEV)[:-1])[0]
             loss = m.training_step(clone_batch(batch, DEV))["loss"]
             loss.backward()
             torch.cuda.synchronize()
+            assert BS.RUNS[0] - runs == (2 if use else 0)   # the schedule under test really ran
             out.append((y.detach().clone(), loss.detach().clone(),
                         {k: p.grad.detach().clone() for k, p in m.named_parameters()}))
     finally:

@@ -88,7 +88,7 @@ def main():
         kpads = [torch.zeros(B, T * ratio, dtype=torch.uint8), torch.zeros(B, T, dtype=torch.uint8)]
         for chunk in (7, 40):
             mock.calls.clear()
-            y = BS.block_stack(x, kvs, qpad, kpads, blocks, 4, True, 1e-5, sinks, chunk=chunk)
+            y = BS.block_stack(x, kvs, [qpad, qpad], kpads, blocks, 4, True, 1e-5, sinks, chunk=chunk)
             nf = len(mock.calls)
             y.backward(torch.ones_like(y))
             print(f"ratio {ratio} T {T} chunk {chunk}: forward {nf} calls, backward {len(mock.calls) - nf}; "
