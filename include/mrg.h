@@ -258,10 +258,13 @@ int mrg_attention_bwd(int B, int heads, int Tq, int Tk, int D,
                       float* dv, long dv_bs, long dv_ts, float* workspace, hipStream_t stream);
 
 /* Query-chunk forms (the metaformer blocks' (block, time-chunk) wavefront): q / o / dout / dq point at
- * the chunk's first query row, lse and the workspace are chunk-sized [B, heads, Tq]; the Tq queries
- * are rows [q_off, q_off + Tq) of a Tq_full-query sequence (the mask rule uses global indices and
- * Tk / Tq_full); qpad is the whole sequence's [B, Tq_full] flags.  kv_accumulate = 1 adds the
- * chunk's dK / dV share into dk / dv (key blocks no query of the chunk sees are not touched).  */
+ * the chunk's first query row; the Tq queries are rows [q_off, q_off + Tq) of a Tq_full-query
+ * sequence (the mask rule uses global indices and Tk / Tq_full); lse, the workspace and qpad are the
+ * whole sequence's [B, heads, Tq_full] / [B, Tq_full] arrays.  bwd passes: 1 = dQ (and the chunk's
+ * delta into the workspace), 2 = dK / dV from the lse / delta already there, 3 = both; a pass-2 call
+ * over q_off = 0, Tq = Tq_full after every chunk's pass-1 call gives the whole sequence's dK / dV.
+ * kv_accumulate = 1 adds a chunk's dK / dV share into dk / dv (key blocks no query of the chunk sees
+ * are not touched).  */
 int mrg_attention_fwd_chunk(int B, int heads, int Tq, int Tk, int D, int q_off, int Tq_full,
                             const float* q, long q_bs, long q_ts, const float* k, long k_bs, long k_ts,
                             const float* v, long v_bs, long v_ts, float* o, long o_bs, long o_ts,
@@ -273,8 +276,8 @@ int mrg_attention_bwd_chunk(int B, int heads, int Tq, int Tk, int D, int q_off, 
                             const float* lse, const unsigned char* qpad, const unsigned char* kpad,
                             int causal, float scale, const float* dout, long do_bs, long do_ts,
                             float* dq, long dq_bs, long dq_ts, float* dk, long dk_bs, long dk_ts,
-                            float* dv, long dv_bs, long dv_ts, int kv_accumulate, float* workspace,
-                            hipStream_t stream);
+                            float* dv, long dv_bs, long dv_ts, int passes, int kv_accumulate,
+                            float* workspace, hipStream_t stream);
 
 /* ---------------------------------------------------------------- LayerNorm
  * y = LayerNorm(a + b) (ResidualConnection.forward, residual_connection.py:

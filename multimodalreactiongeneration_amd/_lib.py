@@ -99,7 +99,7 @@ SIGNATURES = {
                                         P, c_long, c_long, P, c_long, c_long, P, c_long, c_long,
                                         P, c_long, c_long, P, P, P, c_int, c_float,
                                         P, c_long, c_long, P, c_long, c_long, P, c_long, c_long,
-                                        P, c_long, c_long, c_int, P, P]),
+                                        P, c_long, c_long, c_int, c_int, P, P]),
     "mrg_residual_layernorm_fwd": (c_int, [c_int, c_int, P, P, P, P, c_float, P, P, P, P]),
     "mrg_residual_layernorm_bwd_workspace_bytes": (c_size, [c_int, c_int]),
     "mrg_residual_layernorm_bwd": (c_int, [c_int, c_int, P, P, P, P, P, P, P, P, P, c_int, P, P]),

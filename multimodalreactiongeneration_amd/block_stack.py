@@ -156,7 +156,7 @@ class _BlockStackFn(Function):
                       ri2=torch.empty(n, rows, **f32), cat=torch.empty(T, B, n * E, **f32),
                       f=torch.empty(T, B, E, **f32), h1=torch.empty(T, B, Hb, **f32), h2=torch.empty(T, B, E, **f32),
                       out=torch.empty(T, B, E, **f32), m3=torch.empty(rows, **f32), r3=torch.empty(rows, **f32),
-                      lse={})
+                      lse=torch.empty(n, B, heads, T, **f32))
             st.update(w_hh=bl.lstm[1], b_hh=bl.lstm[3])
             S.append(st)
             w_ih, _, _, _, _, _, w_ff = bl.lstm[:7]
@@ -210,15 +210,13 @@ class _BlockStackFn(Function):
                                    _ptr(blocks[k].integ[i][1]), None) for k, r0 in lst for i in range(n)], E, E, dev=dev)
             for k, c, t0, t1 in grp:
                 for i in range(n):
-                    lse = torch.empty(B, heads, t1 - t0, device=dev, dtype=torch.float32)
-                    S[k]["lse"][(i, c)] = lse
                     Tk = Tks[i]
                     with Fn._probe("attn_fwd", 4.0 * D * B * heads * _chunk_pairs(t0, t1, T, Tk, causal)):
                         rc = lib.mrg_attention_fwd_chunk(
                             B, heads, t1 - t0, Tk, D, t0, T, _p(S[k]["Q"][i], t0 * B * E), E, B * E,
                             _ptr(KV[k][i]), Tk * 2 * E, 2 * E, _p(KV[k][i], E), Tk * 2 * E, 2 * E,
-                            _p(S[k]["O"][i], t0 * B * E), E, B * E, _ptr(lse), pads[i][0], pads[i][1], int(causal),
-                            scale, _stream())
+                            _p(S[k]["O"][i], t0 * B * E), E, B * E, _ptr(S[k]["lse"][i]), pads[i][0], pads[i][1],
+                            int(causal), scale, _stream())
                     _lib.check(rc, "attention fwd chunk (block stack)")
             _bgemm(lib, N, E, E, [(_p(S[k]["O"][i], r0 * E), blocks[k].integ[i][2], _p(S[k]["A"][i], r0 * E),
                                    _ptr(blocks[k].integ[i][3]), None) for k, r0 in lst for i in range(n)], E, E, dev=dev)
@@ -269,7 +267,7 @@ class _BlockStackFn(Function):
                           dKV=[torch.empty(B, Tks[i], 2 * E, **f32) for i in range(n)],
                           de=torch.empty(T, B, E, **f32), g2=torch.empty(T, B, E, **f32),
                           du=torch.empty(T, B, E, **f32), g1=torch.empty(T, B, E, **f32),
-                          dG=torch.empty(T, B, 4 * E, **f32),
+                          dG=torch.empty(T, B, 4 * E, **f32), dlt=torch.empty(n, B, heads, T, **f32),
                           ws1=torch.empty(nblk * 2 * E, **f32), ws2=torch.empty(nblk * 2 * E, **f32),
                           wsi1=torch.empty(n, nblk * 2 * E, **f32), wsi2=torch.empty(n, nblk * 2 * E, **f32),
                           ws3=torch.empty(nblk * 2 * E, **f32),
@@ -349,21 +347,21 @@ class _BlockStackFn(Function):
                                  for k, c, r0 in lst for i in range(n)])
             _bgemm(lib, N, E, E, [(_p(G[k]["G1"][i], r0 * E), blocks[k].integ[i][2], _p(G[k]["dO"][i], r0 * E), None,
                                    None) for k, c, r0 in lst for i in range(n)], E, E, transposed=True, dev=dev)
+            # attention: each chunk's dQ pass (+ its delta rows); after a block's last chunk (c == 0 here)
+            # one dK / dV pass over the whole sequence from the stored log-sum-exp / delta rows
             for k, c, t0, t1 in grp:
                 for i in range(n):
                     Tk = Tks[i]
-                    ws = Fn._ws(lib.mrg_attention_bwd_workspace_bytes(B, heads, t1 - t0), dev)
-                    # the last chunk (the first one here) writes every key's dK / dV, earlier ones add
-                    acc = 0 if c == nck - 1 else 1
+                    args = [_ptr(KV[k][i]), Tk * 2 * E, 2 * E, _p(KV[k][i], E), Tk * 2 * E, 2 * E]
                     with Fn._probe("attn_bwd", 10.0 * D * B * heads * _chunk_pairs(t0, t1, T, Tk, causal)):
-                        rc = lib.mrg_attention_bwd_chunk(
-                            B, heads, t1 - t0, Tk, D, t0, T, _p(S[k]["Q"][i], t0 * B * E), E, B * E,
-                            _ptr(KV[k][i]), Tk * 2 * E, 2 * E, _p(KV[k][i], E), Tk * 2 * E, 2 * E,
-                            _p(S[k]["O"][i], t0 * B * E), E, B * E, _ptr(S[k]["lse"][(i, c)]), pads[i][0], pads[i][1],
-                            int(causal), scale, _p(G[k]["dO"][i], t0 * B * E), E, B * E,
-                            _p(G[k]["dQ"][i], t0 * B * E), E, B * E, _ptr(G[k]["dKV"][i]), Tk * 2 * E, 2 * E,
-                            _p(G[k]["dKV"][i], E), Tk * 2 * E, 2 * E, acc, _ptr(ws), _stream())
-                    _lib.check(rc, "attention bwd chunk (block stack)")
+                        for q0, q1, passes in ((t0, t1, 1),) + (((0, T, 2),) if c == 0 else ()):
+                            rc = lib.mrg_attention_bwd_chunk(
+                                B, heads, q1 - q0, Tk, D, q0, T, _p(S[k]["Q"][i], q0 * B * E), E, B * E, *args,
+                                _p(S[k]["O"][i], q0 * B * E), E, B * E, _ptr(S[k]["lse"][i]), pads[i][0], pads[i][1],
+                                int(causal), scale, _p(G[k]["dO"][i], q0 * B * E), E, B * E,
+                                _p(G[k]["dQ"][i], q0 * B * E), E, B * E, _ptr(G[k]["dKV"][i]), Tk * 2 * E, 2 * E,
+                                _p(G[k]["dKV"][i], E), Tk * 2 * E, 2 * E, passes, 0, _ptr(G[k]["dlt"][i]), _stream())
+                            _lib.check(rc, "attention bwd chunk (block stack)")
             # de = sum_i (dQ_i W_q_i + G1_i): the first integrator's product stores, the others add
             for i in range(n):
                 _bgemm(lib, N, E, E, [(_p(G[k]["dQ"][i], r0 * E), blocks[k].integ[i][0][:E], _p(G[k]["de"], r0 * E),

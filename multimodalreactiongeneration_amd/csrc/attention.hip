@@ -53,7 +53,14 @@ struct AttnArgs {
   int q_off, Tqf;
   long qp_bs;
   int kv_acc;
+  // lse / delta rows: [B, Hh, st_ld] arrays, this call's queries at column st_off (chunk calls hand in
+  // the whole sequence's statistics: st_ld = Tqf, st_off = q_off)
+  int st_ld, st_off;
 };
+
+__device__ __forceinline__ long stat_row(const AttnArgs& a, int b, int h, int qi) {
+  return ((long)b * a.Hh + h) * a.st_ld + a.st_off + qi;
+}
 
 // exclusive upper bound of the keys query i may see (causal rule only; Tk when not causal)
 __device__ __forceinline__ int key_bound(const AttnArgs& a, int i) {
@@ -359,7 +366,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   if (qi < a.Tq) {
     const float inv = (l == 0.0f) ? NAN : 1.0f / l;  // l == 0 (fully masked row) -> NaN like softmax(-inf row)
     store_row<D>(a.o + (long)b * a.o_bs + (long)qi * a.o_ts + hoff, lg, a.ovec, o, inv);
-    if (lg == 0) a.lse[((long)b * a.Hh + h) * a.Tq + qi] = (l == 0.0f) ? NAN : m + __logf(l);
+    if (lg == 0) a.lse[stat_row(a, b, h, qi)] = (l == 0.0f) ? NAN : m + __logf(l);
   }
 }
 
@@ -404,7 +411,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
   }
   dsum += __shfl_xor(dsum, 16, 64);
   dsum += __shfl_xor(dsum, 32, 64);
-  const long rowi = ((long)b * a.Hh + h) * a.Tq + qi;
+  const long rowi = stat_row(a, b, h, qi);
   const float lse = qv ? a.lse[rowi] : 0.0f;
   const float dl = dsum;
   if (qv && lg == 0) a.dlt[rowi] = dsum;
@@ -540,7 +547,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
     td.template store<C::SA>(Ds);
     if (threadIdx.x < TT) {
       const int qq = qt0 + threadIdx.x;
-      const long ri = ((long)b * a.Hh + h) * a.Tq + qq;
+      const long ri = stat_row(a, b, h, qq);
       Ls[threadIdx.x] = qq < a.Tq ? a.lse[ri] : 0.0f;
       Dl[threadIdx.x] = qq < a.Tq ? a.dlt[ri] : 0.0f;
     }
@@ -637,7 +644,7 @@ static AttnArgs attn_base(int B, int Hh, int Tq, int Tk, const float* q, long q_
   a.v = v; a.v_bs = v_bs; a.v_ts = v_ts; a.o = const_cast<float*>(o); a.o_bs = o_bs; a.o_ts = o_ts;
   a.lse = const_cast<float*>(lse); a.qpad = qpad; a.kpad = kpad; a.B = B; a.Hh = Hh; a.Tq = Tq; a.Tk = Tk;
   a.causal = causal; a.scale = scale;
-  a.q_off = 0; a.Tqf = Tq; a.qp_bs = Tq; a.kv_acc = 0;
+  a.q_off = 0; a.Tqf = Tq; a.qp_bs = Tq; a.kv_acc = 0; a.st_ld = Tq; a.st_off = 0;
   return a;
 }
 
@@ -710,11 +717,14 @@ MRG_API int mrg_attention_bwd(int B, int Hh, int Tq, int Tk, int D,
   return check_launch("attn_bwd_dkv_kernel");
 }
 
-// Query-chunk forms (the block-level (block, time-chunk) wavefront, metaformer_stack.py): the Tq
-// query rows handed in (q, o, dout, dq: pointers to the chunk's first row; lse and the workspace:
-// chunk-sized [B, heads, Tq]) are rows [q_off, q_off + Tq) of a Tq_full-query sequence; qpad is the
-// whole sequence's [B, Tq_full] flags.  bwd with kv_accumulate = 1 ADDS the chunk's share into
-// dk / dv (only the key blocks some query of the chunk sees are touched).
+// Query-chunk forms (the block-level (block, time-chunk) wavefront, block_stack.py): the Tq query
+// rows handed in (q, o, dout, dq: pointers to the chunk's first row) are rows [q_off, q_off + Tq) of
+// a Tq_full-query sequence; lse, the workspace (delta) and qpad are the whole sequence's
+// [B, heads, Tq_full] / [B, Tq_full] arrays (the chunk's columns at q_off).  bwd passes: 1 = dQ (+ the
+// chunk's delta into the workspace), 2 = dK / dV from the lse / delta already there (a later call
+// over q_off = 0, Tq = Tq_full: the whole sequence's dK / dV once every chunk's dQ pass has run), 3 =
+// both; with kv_accumulate = 1 the dK / dV pass ADDS the chunk's share (only the key blocks some
+// query of the chunk sees are touched).
 MRG_API int mrg_attention_fwd_chunk(int B, int Hh, int Tq, int Tk, int D, int q_off, int Tq_full,
                                     const float* q, long q_bs, long q_ts, const float* k, long k_bs, long k_ts,
                                     const float* v, long v_bs, long v_ts, float* o, long o_bs, long o_ts,
@@ -728,7 +738,7 @@ MRG_API int mrg_attention_fwd_chunk(int B, int Hh, int Tq, int Tk, int D, int q_
               "attention fwd: K/V rows must be 16-B aligned (strides multiple of 4 floats)");
   AttnArgs a = attn_base(B, Hh, Tq, Tk, q, q_bs, q_ts, k, k_bs, k_ts, v, v_bs, v_ts, o, o_bs, o_ts, lse,
                          qpad ? qpad + q_off : nullptr, kpad, causal, scale);
-  a.q_off = q_off; a.Tqf = Tq_full; a.qp_bs = Tq_full;
+  a.q_off = q_off; a.Tqf = Tq_full; a.qp_bs = Tq_full; a.st_ld = Tq_full; a.st_off = q_off;
   a.qvec = rows16(q, q_bs, q_ts) && (D % 4) == 0;
   a.ovec = rows16(o, o_bs, o_ts) && (D % 4) == 0;
   dim3 grid(Hh, B, (Tq + 63) / 64);
@@ -742,27 +752,32 @@ MRG_API int mrg_attention_bwd_chunk(int B, int Hh, int Tq, int Tk, int D, int q_
                                     const float* lse, const unsigned char* qpad, const unsigned char* kpad,
                                     int causal, float scale, const float* dout, long do_bs, long do_ts,
                                     float* dq, long dq_bs, long dq_ts, float* dk, long dk_bs, long dk_ts,
-                                    float* dv, long dv_bs, long dv_ts, int kv_accumulate, float* workspace,
-                                    hipStream_t stream) {
+                                    float* dv, long dv_bs, long dv_ts, int passes, int kv_accumulate,
+                                    float* workspace, hipStream_t stream) {
   if (int e = attn_check(D, Tq_full, Tk, causal)) return e;
   MRG_REQUIRE(q_off >= 0 && Tq >= 0 && q_off + Tq <= Tq_full, "attention bwd chunk: rows [%d, %d) outside %d",
               q_off, q_off + Tq, Tq_full);
   if (B == 0 || Tq == 0 || Tk == 0) return 0;
   MRG_REQUIRE(rows16(q, q_bs, q_ts) && rows16(k, k_bs, k_ts) && rows16(v, v_bs, v_ts) &&
               rows16(dout, do_bs, do_ts), "attention bwd: Q/K/V/dO rows must be 16-B aligned");
-  MRG_REQUIRE(workspace != nullptr, "attention bwd: workspace (B*heads*Tq floats) required");
+  MRG_REQUIRE(workspace != nullptr, "attention bwd: workspace (B*heads*Tq_full floats) required");
+  MRG_REQUIRE(passes >= 1 && passes <= 3, "attention bwd chunk: passes %d (1 dQ, 2 dK/dV, 3 both)", passes);
   AttnArgs a = attn_base(B, Hh, Tq, Tk, q, q_bs, q_ts, k, k_bs, k_ts, v, v_bs, v_ts, o, o_bs, o_ts, lse,
                          qpad ? qpad + q_off : nullptr, kpad, causal, scale);
   a.q_off = q_off; a.Tqf = Tq_full; a.qp_bs = Tq_full; a.kv_acc = kv_accumulate ? 1 : 0;
+  a.st_ld = Tq_full; a.st_off = q_off;
   a.dout = dout; a.do_bs = do_bs; a.do_ts = do_ts; a.dlt = workspace;
   a.dq = dq; a.dq_bs = dq_bs; a.dq_ts = dq_ts; a.dk = dk; a.dk_bs = dk_bs; a.dk_ts = dk_ts;
   a.dv = dv; a.dv_bs = dv_bs; a.dv_ts = dv_ts;
   a.qvec = 1;
   a.ovec = rows16(o, o_bs, o_ts);
   a.dkvvec = rows16(dk, dk_bs, dk_ts) && rows16(dv, dv_bs, dv_ts);
-  dim3 gq(Hh, B, (Tq + 63) / 64);
-  MRG_ATTN_DISPATCH(attn_bwd_dq_kernel, gq, a);
-  if (check_launch("attn_bwd_dq_kernel")) return 1;
+  if (passes & 1) {   // dQ and delta (the dK / dV pass reads delta from the workspace)
+    dim3 gq(Hh, B, (Tq + 63) / 64);
+    MRG_ATTN_DISPATCH(attn_bwd_dq_kernel, gq, a);
+    if (check_launch("attn_bwd_dq_kernel")) return 1;
+  }
+  if (!(passes & 2)) return 0;
   // accumulating: only the key blocks the chunk's last query can see (the rest get nothing)
   int tk = Tk;
   if (a.kv_acc && causal) {

@@ -424,6 +424,11 @@ static int g_mx_min_bs = [] {
   const char* e = getenv("MRG_LSTM_MX_MIN_BS");
   return e ? atoi(e) : 4;
 }();
+// the backward's own threshold (MRG_LSTM_MX_MIN_BS_BWD, default: the forward's)
+static int g_mx_min_bs_bwd = [] {
+  const char* e = getenv("MRG_LSTM_MX_MIN_BS_BWD");
+  return e ? atoi(e) : 0;
+}();
 
 // batch tile the VALU launchers would pick (smallest fitting; 0 = none fits)
 template <typename K1, typename K2, typename K4, typename K8, typename K16>
@@ -476,7 +481,7 @@ static int launch_bwd(const LstmBwdArgs& a, int force_bs, int cus, hipStream_t s
   if (H == 256 && G == 8 && g_mx && force_bs <= 0 && (!a.stamps || g_mx == 2) && g_bwd_blocks_per_cu <= 1) {
     const int bs = valu_bs(lstm_bwd_kernel<H, G, 1>, lstm_bwd_kernel<H, G, 2>, lstm_bwd_kernel<H, G, 4>,
                            lstm_bwd_kernel<H, G, 8>, lstm_bwd_kernel<H, G, 16>, NT, a.nprob, a.B, G, cus);
-    if (g_mx == 2 || bs == 0 || bs >= g_mx_min_bs) {
+    if (g_mx == 2 || bs == 0 || bs >= (g_mx_min_bs_bwd > 0 ? g_mx_min_bs_bwd : g_mx_min_bs)) {
       const int r = launch_bwd_mx(a, cus, s);
       if (r != 0) return r < 0 ? 1 : 0;
     }

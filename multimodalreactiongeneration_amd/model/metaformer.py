@@ -350,9 +350,10 @@ class MultiModalMetaformer(nn.Module):
             return None
         return encoder_stack([(f, e.weight, e.bias, l) for f, e, l in zip(feats, embs, layers)], eps)
 
-    # ---- MI355X schedule: blocks 1.. as one (block, time-chunk) wavefront (block_stack.py); on by
-    # default, MRG_BLOCK_STACK=0 (or MRG_BLOCK_CHUNK=0) keeps the block-by-block schedule
-    use_block_stack = os.environ.get("MRG_BLOCK_STACK", "1") == "1"
+    # ---- MI355X schedule: blocks 1.. as one (block, time-chunk) wavefront (block_stack.py).  Opt-in
+    # (MRG_BLOCK_STACK=1): at B=64 T=300 it saves ~1 ms of recurrence time but its chunked GEMMs,
+    # attention and LayerNorms cost as much again, 21.6 vs 21.2 ms/step replayed
+    use_block_stack = os.environ.get("MRG_BLOCK_STACK", "0") == "1"
 
     def _stack_blocks(self, x, other_modals, attn_mask):
         """The output of blocks 1.. through block_stack.block_stack, or None when a block is outside its

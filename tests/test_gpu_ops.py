@@ -1243,8 +1243,9 @@ def test_fill_zero_any_alignment_and_size():
                                                 (300, 150, True, (0, 150, 300)), (100, 100, False, (0, 50, 100))])
 def test_attention_query_chunks_match_whole(Tq, Tk, causal, cuts):
     """mrg_attention_{fwd,bwd}_chunk over query chunks (the block wavefront's form) vs one whole call:
-    outputs, log-sum-exp and dQ bitwise (every query's arithmetic is the same), dK / dV accumulated
-    chunk by chunk within fp32 reordering; ragged padding flags included."""
+    outputs, log-sum-exp and dQ bitwise (every query's arithmetic is the same); dK / dV either
+    accumulated chunk by chunk (passes 3, kv_accumulate) within fp32 reordering, or from one pass-2
+    call over the whole sequence after the chunks' dQ passes (bitwise); ragged padding flags included."""
     from multimodalreactiongeneration_amd import _lib
     from multimodalreactiongeneration_amd.functional import _ptr, _stream
     lib = _lib.load()
@@ -1270,22 +1271,28 @@ def test_attention_query_chunks_match_whole(Tq, Tk, causal, cuts):
     dq, dk, dv = torch.empty(B, Tq, E, **f), torch.empty(B, Tk, E, **f), torch.empty(B, Tk, E, **f)
     ws = torch.empty(B * Hh * Tq, **f)
     assert lib.mrg_attention_bwd(B, Hh, Tq, Tk, D, *bwd_args(q, o, lse, do, dq, dk, dv), _ptr(ws), _stream()) == 0
-    oc, dqc = torch.full_like(o, 7.0), torch.full_like(dq, 7.0)
+    oc, dqc, dqs = torch.full_like(o, 7.0), torch.full_like(dq, 7.0), torch.full_like(dq, 7.0)
     dkc, dvc = torch.zeros_like(dk), torch.zeros_like(dv)
+    dks, dvs = torch.full_like(dk, 7.0), torch.full_like(dv, 7.0)
+    lc = torch.full_like(lse, 7.0)
+    wsc, wss = torch.empty(B * Hh * Tq, **f), torch.empty(B * Hh * Tq, **f)
+
+    def chunk_bwd(q0, n, dqx, dkx, dvx, passes, acc, wsx):
+        return lib.mrg_attention_bwd_chunk(
+            B, Hh, n, Tk, D, q0, Tq, _ptr(q, q0 * E), Tq * E, E, _ptr(k), Tk * E, E, _ptr(v), Tk * E, E,
+            _ptr(oc, q0 * E), Tq * E, E, _ptr(lc), _ptr(qpad), _ptr(kpad), int(causal), sc, _ptr(do, q0 * E),
+            Tq * E, E, _ptr(dqx, q0 * E), Tq * E, E, _ptr(dkx), Tk * E, E, _ptr(dvx), Tk * E, E, passes, acc,
+            _ptr(wsx), _stream())
     for q0, q1 in zip(cuts[:-1], cuts[1:]):
         n = q1 - q0
-        lc = torch.empty(B, Hh, n, **f)
         assert lib.mrg_attention_fwd_chunk(B, Hh, n, Tk, D, q0, Tq, _ptr(q, q0 * E), Tq * E, E, _ptr(k), Tk * E, E,
                                            _ptr(v), Tk * E, E, _ptr(oc, q0 * E), Tq * E, E, _ptr(lc), _ptr(qpad),
                                            _ptr(kpad), int(causal), sc, _stream()) == 0
-        wsc = torch.empty(B * Hh * n, **f)
-        assert lib.mrg_attention_bwd_chunk(
-            B, Hh, n, Tk, D, q0, Tq, _ptr(q, q0 * E), Tq * E, E, _ptr(k), Tk * E, E, _ptr(v), Tk * E, E,
-            _ptr(oc, q0 * E), Tq * E, E, _ptr(lc), _ptr(qpad), _ptr(kpad), int(causal), sc, _ptr(do, q0 * E),
-            Tq * E, E, _ptr(dqc, q0 * E), Tq * E, E, _ptr(dkc), Tk * E, E, _ptr(dvc), Tk * E, E, 1, _ptr(wsc),
-            _stream()) == 0
-        torch.cuda.synchronize()
-        assert torch.equal(lc, lse[:, :, q0:q1])
+        assert chunk_bwd(q0, n, dqc, dkc, dvc, 3, 1, wsc) == 0
+        assert chunk_bwd(q0, n, dqs, dks, dvs, 1, 0, wss) == 0
+    assert chunk_bwd(0, Tq, dqs, dks, dvs, 2, 0, wss) == 0
     torch.cuda.synchronize()
-    assert torch.equal(oc, o) and torch.equal(dqc, dq)
+    assert torch.equal(lc, lse)
+    assert torch.equal(oc, o) and torch.equal(dqc, dq) and torch.equal(dqs, dq)
+    assert torch.equal(dks, dk) and torch.equal(dvs, dv)
     assert rel_err(dkc, dk) < 1e-5 and rel_err(dvc, dv) < 1e-5
