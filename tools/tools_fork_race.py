@@ -70,8 +70,13 @@ def main():
         for mode in ("side", "side_delay", "replay", "replay_delay"):
             g = grads(m, opt, batch, mode)
             bad = [k for k in ref if not torch.equal(g[k], ref[k])]
-            print(f"split_forks={int(split)} {mode:13s}: {len(bad)} params differ from the one-stream backward"
-                  + (f" e.g. {bad[:4]}" if bad else ""), flush=True)
+            print(f"split_forks={int(split)} {mode:13s}: {len(bad)} params differ from the one-stream backward",
+                  flush=True)
+            if bad and mode == "replay":
+                for k in bad:
+                    d = (g[k] - ref[k]).abs().max().item()
+                    print(f"    {k}: max|diff| {d:.3e} max|ref| {ref[k].abs().max().item():.3e} "
+                          f"replay all -1: {bool((g[k] == -1).all())}", flush=True)
         del m, opt
         torch.cuda.synchronize()
 
