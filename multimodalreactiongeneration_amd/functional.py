@@ -371,6 +371,48 @@ def set_wgrad_defer(on: bool) -> bool:
     return prev
 
 
+# --- fork points under capture.  Measured (round 4, tools/tools_fork_variants.py, tools_fork_race.py):
+# several side-stream forks from ONE point of the main stream (no main-stream node between them, e.g.
+# one fork per weight-gradient product) capture into a graph whose edges are exactly the streams'
+# order (tools/tools_capture_dot.py + tools_dot_deps.py), with no cross-stream address reuse
+# (tools/tools_capture_alias.py) and no hand-off timeout, and the eager step is bitwise right with
+# either stream delayed; yet its replay gives wrong gradients, deterministically, unless the HIP graph
+# executor runs on one queue (DEBUG_HIP_FORCE_GRAPH_QUEUES=1) or a main-stream node separates the forks.
+# So the executor mis-orders that topology (each fork's first side node has two predecessors: the
+# same main node again and the previous side node).  The guard: a fork from the main-stream point
+# the side stream already waited on adds no second wait (the side stream is ordered after that point
+# already), so the redundant edges are never captured.
+_HIP_CAPINFO = [None]
+_LAST_FORK = {}   # device -> the capture point (capture id, main-stream dependency nodes) of the last fork
+_FORK_GUARD = [os.environ.get("MRG_FORK_GUARD", "1") != "0"]   # 0: diagnostics only (tools_fork_variants.py)
+
+
+def _capture_point(stream):
+    """(capture id, the stream's current dependency node handles) while `stream` is capturing, else None."""
+    if _HIP_CAPINFO[0] is None:
+        f = ctypes.CDLL("libamdhip64.so").hipStreamGetCaptureInfo_v2
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_ulonglong),
+                      ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.POINTER(ctypes.c_void_p)),
+                      ctypes.POINTER(ctypes.c_size_t)]
+        _HIP_CAPINFO[0] = f
+    st, cid, graph = ctypes.c_int(0), ctypes.c_ulonglong(0), ctypes.c_void_p()
+    deps, n = ctypes.POINTER(ctypes.c_void_p)(), ctypes.c_size_t(0)
+    rc = _HIP_CAPINFO[0](ctypes.c_void_p(stream.cuda_stream), ctypes.byref(st), ctypes.byref(cid),
+                         ctypes.byref(graph), ctypes.byref(deps), ctypes.byref(n))
+    if rc != 0 or st.value != 1:   # hipStreamCaptureStatusActive
+        return None
+    return (cid.value,) + tuple(deps[i] for i in range(n.value))
+
+
+def _fork(key, s, cur):
+    """s.wait_stream(cur), skipped under capture when s already waited on cur's current point."""
+    point = _capture_point(cur) if _FORK_GUARD[0] and torch.cuda.is_current_stream_capturing() else None
+    if point is None or _LAST_FORK.get(key) != point:
+        s.wait_stream(cur)
+    _LAST_FORK[key] = point
+
+
 def _ensure_join(key, cur, s, task):
     if key not in _JOIN_PENDING:
         def join(cur=cur, s=s, key=key):
@@ -398,9 +440,10 @@ def _flush_deferred(key, device, cap=0, after=None):
     cur = torch.cuda.current_stream(dev)
     s = _SIDE[key]
     if after is None:
-        s.wait_stream(cur)
+        _fork(key, s, cur)
     else:
         s.wait_event(after)
+        _LAST_FORK[key] = None
     lib = _lib.load()
     prev = lib.mrg_gemm_set_blocks_per_cu(cap) if cap else None
     try:
@@ -497,7 +540,7 @@ class _side:
         if s is None:
             s = _SIDE[key] = torch.cuda.Stream(device=dev)
         _ensure_join(key, cur, s, task)
-        s.wait_stream(cur)
+        _fork(key, s, cur)
         for t in self.keep:
             if t is not None:
                 t.record_stream(s)

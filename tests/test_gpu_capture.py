@@ -63,11 +63,13 @@ def test_capture_keeps_side_stream_order_across_forks(pattern):
     assert (x[0].item(), y[0].item(), z[0].item(), w[0].item()) == (1.0, 2.0, 3.0, 4.0)
 
 
-@pytest.mark.parametrize("split", [False, True])
-def test_replayed_step_bitwise_eager_fork_patterns(split):
-    """The lstmformer step (B = 64, T = 300, weight gradients deferred beside the backward recurrences)
-    captured and replayed twice: every gradient bitwise the eager one, with one side-stream fork per
-    encoder layer (default) and with one fork per product (encoder_stack.SPLIT_FORKS)."""
+@pytest.mark.parametrize("split,defer", [(False, True), (True, True), (True, False), (False, False)])
+def test_replayed_step_bitwise_eager_fork_patterns(split, defer):
+    """The lstmformer step (B = 64, T = 300) captured and replayed twice: every gradient bitwise the
+    eager one, with one side-stream fork per encoder layer (default) and with one fork per product
+    (encoder_stack.SPLIT_FORKS), weight gradients deferred beside the backward recurrences (default)
+    or forked where they are ready.  (True, False) is the pattern whose replay was wrong before the
+    fork-point guard (functional._fork: several forks from one main-stream point)."""
     from multimodalreactiongeneration_amd import configs as C
     from multimodalreactiongeneration_amd import encoder_stack as ES
     from multimodalreactiongeneration_amd import functional as Fn
@@ -84,7 +86,7 @@ def test_replayed_step_bitwise_eager_fork_patterns(split):
         opt.zero_grad()
         m.training_step(list(batch))["loss"].backward()
     prev = ES.SPLIT_FORKS
-    prev_side, prev_defer = Fn.set_wgrad_stream(True), Fn.set_wgrad_defer(True)
+    prev_side, prev_defer = Fn.set_wgrad_stream(True), Fn.set_wgrad_defer(defer)
     try:
         ES.SPLIT_FORKS = split
         step()

@@ -36,6 +36,20 @@ def _enter(self):
 
 
 Fn._side.__enter__ = _enter
+_orig_exit = Fn._side.__exit__
+MAIN_DELAY = [0.0]
+
+
+def _exit(self, *exc):
+    on_side = self.ctx is not None
+    r = _orig_exit(self, *exc)
+    if on_side and MAIN_DELAY[0] > 0:   # the main stream runs late: the side stream gets ahead of it
+        _lib.check(_lib.load().mrg_debug_busy(1, 64, 256, MAIN_DELAY[0], torch.cuda.current_stream().cuda_stream),
+                   "busy")
+    return r
+
+
+Fn._side.__exit__ = _exit
 
 
 def grads(m, opt, batch, mode):
@@ -43,6 +57,7 @@ def grads(m, opt, batch, mode):
         opt.zero_grad()
         m.training_step(list(batch))["loss"].backward()
     DELAY[0] = 300.0 if mode.endswith("_delay") else 0.0
+    MAIN_DELAY[0] = 300.0 if mode.endswith("_maindelay") else 0.0
     Fn.set_wgrad_stream(mode != "noside")
     if mode.startswith("replay"):
         step()
@@ -53,7 +68,7 @@ def grads(m, opt, batch, mode):
     else:
         step()
     torch.cuda.synchronize()
-    DELAY[0] = 0.0
+    DELAY[0] = MAIN_DELAY[0] = 0.0
     return {k: p.grad.clone() for k, p in m.named_parameters()}
 
 
@@ -67,12 +82,12 @@ def main():
         opt = m.configure_optimizers()["optimizer"]
         batch = make_batch(B=64, T=300, ratio=1, seed=5, device="cuda:0")
         ref = grads(m, opt, batch, "noside")
-        for mode in ("side", "side_delay", "replay", "replay_delay"):
+        for mode in ("side", "side_delay", "side_maindelay", "replay", "replay_delay", "replay_maindelay"):
             g = grads(m, opt, batch, mode)
             bad = [k for k in ref if not torch.equal(g[k], ref[k])]
             print(f"split_forks={int(split)} {mode:13s}: {len(bad)} params differ from the one-stream backward",
                   flush=True)
-            if bad and mode == "replay":
+            if bad and mode == "side_maindelay":
                 for k in bad:
                     d = (g[k] - ref[k]).abs().max().item()
                     print(f"    {k}: max|diff| {d:.3e} max|ref| {ref[k].abs().max().item():.3e} "
