@@ -61,6 +61,9 @@ int mrg_probe_stop(float* ms, int* tags, int cap);
 /* Tuning knob: number of workgroups that share one batch row group at H = 256
  * (8 or 16; default 8).  Process-wide; set before capture, not during. */
 int mrg_lstm_config(int group256);
+/* Solo (one-workgroup, LDS-exchange) recurrence groups at H <= 128: 1 on (default), 0 off; returns the
+ * previous setting. */
+int mrg_lstm_set_solo(int on);
 /* Diagnostics only: record per-step phase clocks (s_memtime) of block 0 of the next
  * LSTM launches into buf ([T][8] u64); null disables.  Never in timed runs. */
 int mrg_lstm_debug_stamps(void* buf);

@@ -28,6 +28,11 @@
 // placement affects speed only, never correctness.  Every spin is bounded and
 // reports through *err.
 //
+// Solo groups (G = 1, H <= 128, the default there: mrg_lstm_set_solo): one workgroup holds all of
+// W_hh (at H = 128, 1024 threads x 64 values) and exchanges h / dh through its LDS, so a step has no
+// hand-off through L2 and the workgroups of a launch never wait on each other (no co-residency
+// requirement: a grid larger than the GPU still completes).
+//
 // Backward runs the same decomposition in reverse time: a member owns the
 // same U units, computes dG for them, then the partial products
 // P_j[b][:] = dG_j[b] W_hh[rows_j, :] over ALL H outputs; the exchange is a
@@ -43,17 +48,23 @@ namespace mrg {
 //   H = 256, G = 16 : 256 threads (64 W_hh values per lane), 4 workgroups per CU
 //   H <= 128        : 256 threads, 2 workgroups per CU
 // waves_per_simd bounds VGPRs at 512 / waves (128 here) so the whole grid stays resident.
+//   H = 128, G = 1  : 1024 threads (64 W_hh values per lane), 1 workgroup per CU (a "solo" group)
 template <int H, int G>
 struct LstmNT {
-  static constexpr int value = (H >= 256 && H / G >= 32) ? 512 : 256;
-  static constexpr int waves_per_simd = H >= 256 ? 4 : 2;
+  static constexpr int value = (G == 1 && H == 128) ? 1024 : (H >= 256 && H / G >= 32) ? 512 : 256;
+  static constexpr int waves_per_simd = (H >= 256 || value == 1024) ? 4 : 2;
 };
+
+// batch tiles a (H, G) kernel can hold (every cell thread in the block)
+template <int H, int G, int BS>
+constexpr bool tile_ok() { return BS * (H / G) <= LstmNT<H, G>::value && (G > 1 || H < 128 || BS <= 8); }
 
 template <int H, int G, int BS>
 __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_simd)) void lstm_fwd_kernel(LstmFwdArgs args) {
   constexpr int NT = LstmNT<H, G>::value;
   constexpr int U = H / G;
   constexpr int R = 4 * U;
+  constexpr bool SOLO = G == 1;
   // register blocking of the recurrent GEMV: a thread owns RT gate rows x KL hidden inputs, the
   // KC lanes of a row group split the hidden dimension (DPP-reduced), so every h value read from
   // LDS feeds RT FMAs (the GEMV is LDS-issue bound otherwise)
@@ -173,7 +184,11 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
       float ig = sigmoidf_(zi), fg = sigmoidf_(zf), gg = tanhf_(zg), og = sigmoidf_(zo);
       c = fg * c + ig * gg;
       h = og * tanhf_(c);
-      if (!(args.inject == 1 && j == 0 && tt == 0)) put_granule(xb + ((long)par * B + bg) * H + hcol, (unsigned)(tt + 1), h, local);
+      if constexpr (SOLO) {
+        hs[cb][cu / KL][cu % KL] = h;   // after the GEMV's reads (barrier above), before the next (below)
+      } else if (!(args.inject == 1 && j == 0 && tt == 0)) {
+        put_granule(xb + ((long)par * B + bg) * H + hcol, (unsigned)(tt + 1), h, local);
+      }
       P.y[(long)bg * P.y_bs + (long)t * P.y_ts + hcol] = h;
       float* gs = P.gates + (long)bg * P.g_bs + (long)t * P.g_ts + hcol;
       gs[0] = ig; gs[H] = fg; gs[2 * H] = gg; gs[3 * H] = og;
@@ -184,7 +199,7 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
     // 4. gather h_t of the whole group.  Done by the waves after the cell waves: on gfx9 one vmcnt
     // covers loads and stores, so a wave that just issued the y/gates/cs stores and the gx prefetch
     // would wait for all of them before its first poll returned.
-    if (tt + 1 < T && tid >= GOFF) {
+    if (!SOLO && tt + 1 < T && tid >= GOFF) {
       const int gt = tid - GOFF;
       const int nvalid = min(BS, B - b0) * H;
       unsigned long long* rb = xb + ((long)par * B + b0) * H;
@@ -217,6 +232,7 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
   constexpr int NT = LstmNT<H, G>::value;
   constexpr int U = H / G;
   constexpr int R = 4 * U;
+  constexpr bool SOLO = G == 1;
   // a thread owns OT consecutive outputs (hidden units of dh_{t-1}) x RL gate rows; the RC lanes of
   // an output group split the rows (DPP-reduced): each dG value read from LDS feeds OT FMAs
   constexpr int RC = (H >= 128) ? 8 : 16;
@@ -227,6 +243,7 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
                 (U % OT) == 0, "bad LSTM bwd tiling");
   __shared__ __attribute__((aligned(16))) float dgl[BS][RC][RLP];
   __shared__ float sv[2][7][BS * U];  // saved i, f, g, o, c_t, c_{t-1}, dy of the cells, by step parity
+  __shared__ float dhs[SOLO ? BS : 1][SOLO ? H : 1];  // solo: dh_{t-1} of the step, summed in place
   constexpr int CW = (BS * U + 63) / 64;
   // no spare waves for the io role at the largest batch tiles: the cell threads then move their own
   // saved activations (same schedule: stage step tt+1, prefetch tt+2, after the step's GEMV)
@@ -307,14 +324,18 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
     MRG_STAMP(0);
     if (cvalid) {
       if (tt > 0) {
-        const int par = (tt - 1) & 1;
-        unsigned long long* g = xb + ((long)par * B + bg) * xstride_b + (long)j * H + cu;
-        float gv[G];
-        get_granules<G>(g, U, (unsigned)tt, gv, args.err, dead);
-        float s = 0.0f;
+        if constexpr (SOLO) {
+          dhrec = dhs[cb][cu];
+        } else {
+          const int par = (tt - 1) & 1;
+          unsigned long long* g = xb + ((long)par * B + bg) * xstride_b + (long)j * H + cu;
+          float gv[G];
+          get_granules<G>(g, U, (unsigned)tt, gv, args.err, dead);
+          float s = 0.0f;
 #pragma unroll
-        for (int src = 0; src < G; ++src) s += gv[src];
-        dhrec = s;
+          for (int src = 0; src < G; ++src) s += gv[src];
+          dhrec = s;
+        }
       }
       MRG_STAMP(1);
       const int sl = tt & 1;
@@ -370,7 +391,14 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
         for (int o = 0; o < OT; ++o) acc[o] = group_sum<RC>(acc[o]);
         // every lane of the RC group holds the sums: lanes rc < OT each publish granule o = rc, so
         // a wave's puts are contiguous 8-B granules in ONE store instruction (full 128-B lines)
-        if (rc < OT && b0 + b < B && !(args.inject == 2 && j == 0 && tt == 0)) {
+        if constexpr (SOLO) {
+          if (rc < OT) {   // all reads of dhs this step were before the barrier above
+            float v = acc[0];
+#pragma unroll
+            for (int o = 1; o < OT; ++o) v = (rc == o) ? acc[o] : v;
+            dhs[b][ogr * OT + rc] = v;
+          }
+        } else if (rc < OT && b0 + b < B && !(args.inject == 2 && j == 0 && tt == 0)) {
           const int h0 = ogr * OT;
           const int dest = h0 / U, du = h0 % U;
           float v = acc[0];
@@ -398,14 +426,18 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
   }
   if (cvalid) {
     if (P.dh0) {
-      const int par = (T - 1) & 1;
-      unsigned long long* g = xb + ((long)par * B + bg) * xstride_b + (long)j * H + cu;
-      float gv[G];
-      get_granules<G>(g, U, (unsigned)T, gv, args.err, dead);
-      float s = 0.0f;
+      if constexpr (SOLO) {
+        P.dh0[(long)bg * H + hcol] = dhs[cb][cu];
+      } else {
+        const int par = (T - 1) & 1;
+        unsigned long long* g = xb + ((long)par * B + bg) * xstride_b + (long)j * H + cu;
+        float gv[G];
+        get_granules<G>(g, U, (unsigned)T, gv, args.err, dead);
+        float s = 0.0f;
 #pragma unroll
-      for (int src = 0; src < G; ++src) s += gv[src];
-      P.dh0[(long)bg * H + hcol] = s;
+        for (int src = 0; src < G; ++src) s += gv[src];
+        P.dh0[(long)bg * H + hcol] = s;
+      }
     }
     if (P.dc0) P.dc0[(long)bg * H + hcol] = dcn;
   }
@@ -442,28 +474,41 @@ static int valu_bs(K1 k1, K2 k2, K4 k4, K8 k8, K16 k16, int nt, int nprob, int B
   return 0;
 }
 
+// one candidate batch tile: launch when it fits (or, for a solo group, when it is the last candidate:
+// its workgroups never wait on each other, so a grid larger than the GPU still completes)
+template <int BS, typename Args, typename K>
+static bool try_tile(K kernel, int nt, long nblk, int cus, bool last_solo, hipStream_t s, const Args& a) {
+  if (!fits(kernel, nt, nblk, cus) && !last_solo) return false;
+  klaunch(kernel, nblk, nt, 0, s, a);
+  return true;
+}
+
 template <int H, int G>
 static int launch_fwd(const LstmFwdArgs& a, int force_bs, int cus, hipStream_t s) {
   constexpr int NT = LstmNT<H, G>::value;
   const long groups1 = a.B;
-  if (H == 256 && G == 8 && g_mx && force_bs <= 0 && (!a.stamps || g_mx == 2)) {
-    const int bs = valu_bs(lstm_fwd_kernel<H, G, 1>, lstm_fwd_kernel<H, G, 2>, lstm_fwd_kernel<H, G, 4>,
-                           lstm_fwd_kernel<H, G, 8>, lstm_fwd_kernel<H, G, 16>, NT, a.nprob, a.B, G, cus);
-    if (g_mx == 2 || bs == 0 || bs >= g_mx_min_bs) {
-      const int r = launch_fwd_mx(a, cus, s);
-      if (r != 0) return r < 0 ? 1 : 0;
+  if constexpr (H == 256 && G == 8) {
+    if (g_mx && force_bs <= 0 && (!a.stamps || g_mx == 2)) {
+      const int bs = valu_bs(lstm_fwd_kernel<H, G, 1>, lstm_fwd_kernel<H, G, 2>, lstm_fwd_kernel<H, G, 4>,
+                             lstm_fwd_kernel<H, G, 8>, lstm_fwd_kernel<H, G, 16>, NT, a.nprob, a.B, G, cus);
+      if (g_mx == 2 || bs == 0 || bs >= g_mx_min_bs) {
+        const int r = launch_fwd_mx(a, cus, s);
+        if (r != 0) return r < 0 ? 1 : 0;
+      }
     }
   }
-  for (int bs = 1; bs <= 16; bs *= 2) {
+  constexpr int BMAX = tile_ok<H, G, 16>() ? 16 : tile_ok<H, G, 8>() ? 8 : tile_ok<H, G, 4>() ? 4 : 2;
+  for (int bs = 1; bs <= BMAX; bs *= 2) {
     if (force_bs > 0 && bs != force_bs) continue;
     long nblk = (long)a.nprob * ((groups1 + bs - 1) / bs) * G;
-    bool ok;
+    const bool last = G == 1 && (bs == BMAX || bs == force_bs);
+    bool ok = false;
     switch (bs) {
-      case 1: ok = fits(lstm_fwd_kernel<H, G, 1>, NT, nblk, cus); if (ok) klaunch(lstm_fwd_kernel<H, G, 1>, nblk, NT, 0, s, a); break;
-      case 2: ok = fits(lstm_fwd_kernel<H, G, 2>, NT, nblk, cus); if (ok) klaunch(lstm_fwd_kernel<H, G, 2>, nblk, NT, 0, s, a); break;
-      case 4: ok = fits(lstm_fwd_kernel<H, G, 4>, NT, nblk, cus); if (ok) klaunch(lstm_fwd_kernel<H, G, 4>, nblk, NT, 0, s, a); break;
-      case 8: ok = fits(lstm_fwd_kernel<H, G, 8>, NT, nblk, cus); if (ok) klaunch(lstm_fwd_kernel<H, G, 8>, nblk, NT, 0, s, a); break;
-      default: ok = fits(lstm_fwd_kernel<H, G, 16>, NT, nblk, cus); if (ok) klaunch(lstm_fwd_kernel<H, G, 16>, nblk, NT, 0, s, a); break;
+      case 1: ok = try_tile<1>(lstm_fwd_kernel<H, G, 1>, NT, nblk, cus, last, s, a); break;
+      case 2: ok = try_tile<2>(lstm_fwd_kernel<H, G, 2>, NT, nblk, cus, last, s, a); break;
+      case 4: if constexpr (tile_ok<H, G, 4>()) ok = try_tile<4>(lstm_fwd_kernel<H, G, 4>, NT, nblk, cus, last, s, a); break;
+      case 8: if constexpr (tile_ok<H, G, 8>()) ok = try_tile<8>(lstm_fwd_kernel<H, G, 8>, NT, nblk, cus, last, s, a); break;
+      default: if constexpr (tile_ok<H, G, 16>()) ok = try_tile<16>(lstm_fwd_kernel<H, G, 16>, NT, nblk, cus, last, s, a); break;
     }
     if (ok) return check_launch("lstm_fwd_kernel");
   }
@@ -478,25 +523,29 @@ template <int H, int G>
 static int launch_bwd(const LstmBwdArgs& a, int force_bs, int cus, hipStream_t s) {
   constexpr int NT = LstmNT<H, G>::value;
   // (the MFMA form runs one workgroup per CU, within a cap of one: mrg_lstm_set_blocks_per_cu)
-  if (H == 256 && G == 8 && g_mx && force_bs <= 0 && (!a.stamps || g_mx == 2) && g_bwd_blocks_per_cu <= 1) {
-    const int bs = valu_bs(lstm_bwd_kernel<H, G, 1>, lstm_bwd_kernel<H, G, 2>, lstm_bwd_kernel<H, G, 4>,
-                           lstm_bwd_kernel<H, G, 8>, lstm_bwd_kernel<H, G, 16>, NT, a.nprob, a.B, G, cus);
-    if (g_mx == 2 || bs == 0 || bs >= (g_mx_min_bs_bwd > 0 ? g_mx_min_bs_bwd : g_mx_min_bs)) {
-      const int r = launch_bwd_mx(a, cus, s);
-      if (r != 0) return r < 0 ? 1 : 0;
+  if constexpr (H == 256 && G == 8) {
+    if (g_mx && force_bs <= 0 && (!a.stamps || g_mx == 2) && g_bwd_blocks_per_cu <= 1) {
+      const int bs = valu_bs(lstm_bwd_kernel<H, G, 1>, lstm_bwd_kernel<H, G, 2>, lstm_bwd_kernel<H, G, 4>,
+                             lstm_bwd_kernel<H, G, 8>, lstm_bwd_kernel<H, G, 16>, NT, a.nprob, a.B, G, cus);
+      if (g_mx == 2 || bs == 0 || bs >= (g_mx_min_bs_bwd > 0 ? g_mx_min_bs_bwd : g_mx_min_bs)) {
+        const int r = launch_bwd_mx(a, cus, s);
+        if (r != 0) return r < 0 ? 1 : 0;
+      }
     }
   }
-  for (int bs = 1; bs <= 16; bs *= 2) {
+  constexpr int BMAX = tile_ok<H, G, 16>() ? 16 : tile_ok<H, G, 8>() ? 8 : tile_ok<H, G, 4>() ? 4 : 2;
+  for (int bs = 1; bs <= BMAX; bs *= 2) {
     if (force_bs > 0 && bs != force_bs) continue;
     long nblk = (long)a.nprob * ((a.B + bs - 1) / bs) * G;
-    if (force_bs <= 0 && g_bwd_blocks_per_cu > 0 && bs < 16 && nblk > (long)g_bwd_blocks_per_cu * cus) continue;
-    bool ok;
+    const bool last = G == 1 && (bs == BMAX || bs == force_bs);
+    if (force_bs <= 0 && g_bwd_blocks_per_cu > 0 && bs < BMAX && nblk > (long)g_bwd_blocks_per_cu * cus) continue;
+    bool ok = false;
     switch (bs) {
-      case 1: ok = fits(lstm_bwd_kernel<H, G, 1>, NT, nblk, cus); if (ok) klaunch(lstm_bwd_kernel<H, G, 1>, nblk, NT, 0, s, a); break;
-      case 2: ok = fits(lstm_bwd_kernel<H, G, 2>, NT, nblk, cus); if (ok) klaunch(lstm_bwd_kernel<H, G, 2>, nblk, NT, 0, s, a); break;
-      case 4: ok = fits(lstm_bwd_kernel<H, G, 4>, NT, nblk, cus); if (ok) klaunch(lstm_bwd_kernel<H, G, 4>, nblk, NT, 0, s, a); break;
-      case 8: ok = fits(lstm_bwd_kernel<H, G, 8>, NT, nblk, cus); if (ok) klaunch(lstm_bwd_kernel<H, G, 8>, nblk, NT, 0, s, a); break;
-      default: ok = fits(lstm_bwd_kernel<H, G, 16>, NT, nblk, cus); if (ok) klaunch(lstm_bwd_kernel<H, G, 16>, nblk, NT, 0, s, a); break;
+      case 1: ok = try_tile<1>(lstm_bwd_kernel<H, G, 1>, NT, nblk, cus, last, s, a); break;
+      case 2: ok = try_tile<2>(lstm_bwd_kernel<H, G, 2>, NT, nblk, cus, last, s, a); break;
+      case 4: if constexpr (tile_ok<H, G, 4>()) ok = try_tile<4>(lstm_bwd_kernel<H, G, 4>, NT, nblk, cus, last, s, a); break;
+      case 8: if constexpr (tile_ok<H, G, 8>()) ok = try_tile<8>(lstm_bwd_kernel<H, G, 8>, NT, nblk, cus, last, s, a); break;
+      default: if constexpr (tile_ok<H, G, 16>()) ok = try_tile<16>(lstm_bwd_kernel<H, G, 16>, NT, nblk, cus, last, s, a); break;
     }
     if (ok) return check_launch("lstm_bwd_kernel");
   }
@@ -507,7 +556,14 @@ static int launch_bwd(const LstmBwdArgs& a, int force_bs, int cus, hipStream_t s
 
 static int g_group256 = 8;  // members per group at H = 256 (8 or 16), mrg_lstm_config
 
-static int group_size(int H) {
+// solo groups (G = 1) at H <= 128: MRG_LSTM_SOLO=0 / mrg_lstm_set_solo(0) restores the multi-member groups
+static int g_solo = [] {
+  const char* e = getenv("MRG_LSTM_SOLO");
+  return (e && atoi(e) == 0) ? 0 : 1;
+}();
+
+// members per group without solo groups (the hand-off ring is sized for these)
+static int ring_group_size(int H) {
   switch (H) {
     case 256: return g_group256;
     case 128: return 8;
@@ -516,6 +572,11 @@ static int group_size(int H) {
     case 16: return 1;
     default: return 0;
   }
+}
+
+static int group_size(int H) {
+  const int g = ring_group_size(H);
+  return (g > 0 && H <= 128 && g_solo) ? 1 : g;
 }
 
 }  // namespace mrg
@@ -553,7 +614,7 @@ MRG_API int mrg_lstm_debug_stamps(void* buf) {
 MRG_API size_t mrg_lstm_fwd_xbuf_bytes(int B, int H) { return (size_t)2 * B * H * 8; }
 MRG_API size_t mrg_lstm_bwd_xbuf_bytes(int B, int H) {
   // sized for the largest group the runtime may select, so mrg_lstm_config can change it
-  int G = H == 256 ? 16 : group_size(H);
+  int G = H == 256 ? 16 : ring_group_size(H);
   return (size_t)2 * B * (G > 0 ? G : 1) * H * 8;
 }
 
@@ -575,6 +636,13 @@ MRG_API int mrg_lstm_set_mx(int mode, int min_bs) {
   const int prev = g_mx;
   g_mx = mode;
   if (min_bs > 0) g_mx_min_bs = min_bs;
+  return prev;
+}
+
+// Tuning: solo (one-workgroup) groups at H <= 128 on / off.  Returns the previous setting.
+MRG_API int mrg_lstm_set_solo(int on) {
+  const int prev = g_solo;
+  g_solo = on ? 1 : 0;
   return prev;
 }
 
@@ -621,9 +689,9 @@ MRG_API int mrg_lstm_fwd(int nprob, int B, int T, int H,
   if (cus <= 0) cus = device_cus();
   switch (H) {
     case 256: return G == 8 ? launch_fwd<256, 8>(a, force_bs, cus, stream) : launch_fwd<256, 16>(a, force_bs, cus, stream);
-    case 128: return launch_fwd<128, 8>(a, force_bs, cus, stream);
-    case 64: return launch_fwd<64, 4>(a, force_bs, cus, stream);
-    case 32: return launch_fwd<32, 2>(a, force_bs, cus, stream);
+    case 128: return G == 1 ? launch_fwd<128, 1>(a, force_bs, cus, stream) : launch_fwd<128, 8>(a, force_bs, cus, stream);
+    case 64: return G == 1 ? launch_fwd<64, 1>(a, force_bs, cus, stream) : launch_fwd<64, 4>(a, force_bs, cus, stream);
+    case 32: return G == 1 ? launch_fwd<32, 1>(a, force_bs, cus, stream) : launch_fwd<32, 2>(a, force_bs, cus, stream);
     case 16: return launch_fwd<16, 1>(a, force_bs, cus, stream);
   }
   return 2;
@@ -662,9 +730,9 @@ MRG_API int mrg_lstm_bwd(int nprob, int B, int T, int H,
   if (cus <= 0) cus = device_cus();
   switch (H) {
     case 256: return G == 8 ? launch_bwd<256, 8>(a, force_bs, cus, stream) : launch_bwd<256, 16>(a, force_bs, cus, stream);
-    case 128: return launch_bwd<128, 8>(a, force_bs, cus, stream);
-    case 64: return launch_bwd<64, 4>(a, force_bs, cus, stream);
-    case 32: return launch_bwd<32, 2>(a, force_bs, cus, stream);
+    case 128: return G == 1 ? launch_bwd<128, 1>(a, force_bs, cus, stream) : launch_bwd<128, 8>(a, force_bs, cus, stream);
+    case 64: return G == 1 ? launch_bwd<64, 1>(a, force_bs, cus, stream) : launch_bwd<64, 4>(a, force_bs, cus, stream);
+    case 32: return G == 1 ? launch_bwd<32, 1>(a, force_bs, cus, stream) : launch_bwd<32, 2>(a, force_bs, cus, stream);
     case 16: return launch_bwd<16, 1>(a, force_bs, cus, stream);
   }
   return 2;

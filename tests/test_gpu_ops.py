@@ -683,6 +683,7 @@ def test_lstm_local_handoff_is_bitwise_the_agent_one(H, B):
     x = torch.randn(B, T, H, generator=g)
     h0, c0 = torch.randn(B, H, generator=g), torch.randn(B, H, generator=g)
     outs = []
+    prev_solo = lib.mrg_lstm_set_solo(0)   # the hand-off rings (solo groups at H <= 128 have none)
     try:
         for local in (1, 0):
             _lib.check(lib.mrg_lstm_set_local_handoff(local), "local")
@@ -695,8 +696,66 @@ def test_lstm_local_handoff_is_bitwise_the_agent_one(H, B):
             outs.append([y.detach(), hT.detach(), cT.detach(), xx.grad] + [p.grad for p in ps])
     finally:
         lib.mrg_lstm_set_local_handoff(1)
+        lib.mrg_lstm_set_solo(prev_solo)
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("H,nprob,B,T,rev,state", [(128, 2, 64, 40, True, True), (128, 1, 37, 29, False, False),
+                                                   (64, 3, 20, 33, False, True), (32, 2, 5, 17, True, False),
+                                                   (128, 1, 2100, 3, False, True)])
+def test_lstm_solo_groups_vs_oracle(H, nprob, B, T, rev, state):
+    """Solo recurrence groups (one workgroup holds W_hh, h / dh exchanged through its LDS; the default
+    at H <= 128) vs the oracle, and vs the multi-member hand-off groups: outputs, final states and
+    every gradient.  B = 2100 at H = 128 is a grid larger than the GPU holds at once (its workgroups
+    never wait on each other, so it completes)."""
+    from multimodalreactiongeneration_amd import _lib
+    from multimodalreactiongeneration_amd import functional as Fn
+    from oracle import mrg_oracle as O
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(H * 7 + B)
+    s = 1.0 / math.sqrt(H)
+    data = []
+    for _ in range(nprob):
+        w = [torch.randn(4 * H, H, generator=g) * s for _ in range(2)]
+        bb = [torch.randn(4 * H, generator=g) * s for _ in range(2)]
+        x = torch.randn(B, T, H, generator=g)
+        h0 = torch.randn(B, H, generator=g) * 0.5 if state else None
+        c0 = torch.randn(B, H, generator=g) * 0.5 if state else None
+        data.append((x, w, bb, h0, c0))
+    outs = {}
+    for solo in (1, 0):
+        prev = lib.mrg_lstm_set_solo(solo)
+        try:
+            res = []
+            for x, w, bb, h0, c0 in data:
+                ps = [_param(t) for t in (w[0], w[1], bb[0], bb[1])]
+                xx = x.to(DEV).requires_grad_(True)
+                hd = h0.to(DEV).requires_grad_(True) if state else None
+                cd = c0.to(DEV).requires_grad_(True) if state else None
+                y, hT, cT = Fn.lstm_layer(xx, *ps, hd, cd, reverse=rev)
+                (y.square().sum() + hT.square().sum() + cT.sum()).backward()
+                torch.cuda.synchronize()
+                Fn.check_errors()
+                res.append([y.detach(), hT.detach(), cT.detach(), xx.grad] + [p.grad for p in ps] +
+                           ([hd.grad, cd.grad] if state else []))
+            outs[solo] = res
+        finally:
+            lib.mrg_lstm_set_solo(prev)
+    if B <= 64:   # the oracle at small sizes
+        for (x, w, bb, h0, c0), got in zip(data, outs[1]):
+            xr = x.clone().requires_grad_(True)
+            rw = [t.clone().requires_grad_(True) for t in (w[0], w[1], bb[0], bb[1])]
+            hr = h0.clone().requires_grad_(True) if state else None
+            cr = c0.clone().requires_grad_(True) if state else None
+            yr, hTr, cTr = O.lstm_layer(xr, *rw, hr, cr, reverse=rev)
+            (yr.square().sum() + hTr.square().sum() + cTr.sum()).backward()
+            ref = [yr, hTr, cTr, xr.grad] + [t.grad for t in rw] + ([hr.grad, cr.grad] if state else [])
+            for a, r in zip(got, ref):
+                assert rel_err(a, r.detach()) < TOL
+    for a_list, b_list in zip(outs[1], outs[0]):
+        for a, b in zip(a_list, b_list):
+            assert rel_err(a, b) < TOL
 
 
 @pytest.mark.parametrize("resln,masked", [(False, False), (True, False), (True, True)])
@@ -972,6 +1031,7 @@ def test_lstm_handoff_timeout_skips_adamw_and_raises():
     opt = FusedAdamW(ws + bs, lr=1e-3)
     x = torch.randn(B, T, H, device=DEV)
     before = opt.flat.clone()
+    prev_solo = L.load().mrg_lstm_set_solo(0)   # a hand-off ring to drop (solo groups have none)
     L.check(L.load().mrg_lstm_debug_inject(1), "inject")
     y, _, _ = Fn.lstm_layer(x, ws[0], ws[1], bs[0], bs[1])
     y.square().sum().backward()
@@ -987,6 +1047,7 @@ def test_lstm_handoff_timeout_skips_adamw_and_raises():
     opt.step()
     torch.cuda.synchronize()
     Fn.check_errors()
+    L.load().mrg_lstm_set_solo(prev_solo)
     assert not torch.equal(opt.flat, before)
 
 
