@@ -70,7 +70,8 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
   // LDS feeds RT FMAs (the GEMV is LDS-issue bound otherwise)
   // (KC = 8 lanes x 2 rows measured fastest at H = 256: 3 DPP levels, 128-B LDS reads per lane; 16 x 4
   // at batch tiles >= 4 (half the LDS reads of h, one more DPP level) measured 5-23 % slower, r03)
-  constexpr int KC = (H >= 128) ? (2 * NT / R) : ((H / 4 < 16) ? H / 4 : 16);
+  // (solo groups at H = 128: 8 lanes x 4 rows, half the LDS reads of h per FMA of 4 x 2)
+  constexpr int KC = (SOLO && H == 128) ? 8 : (H >= 128) ? (2 * NT / R) : ((H / 4 < 16) ? H / 4 : 16);
   constexpr int RT = R * KC / NT;
   constexpr int KL = H / KC;
   constexpr int KLP = ((KL / 4) % 2 == 0) ? KL + 4 : KL;  // odd 16-B chunk pitch: conflict-free b128
@@ -235,7 +236,7 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
   constexpr bool SOLO = G == 1;
   // a thread owns OT consecutive outputs (hidden units of dh_{t-1}) x RL gate rows; the RC lanes of
   // an output group split the rows (DPP-reduced): each dG value read from LDS feeds OT FMAs
-  constexpr int RC = (H >= 128) ? 8 : 16;
+  constexpr int RC = (H >= 128 && !SOLO) ? 8 : 16;
   constexpr int OT = RC * H / NT;
   constexpr int RL = R / RC;
   constexpr int RLP = ((RL / 4) % 2 == 0) ? RL + 4 : RL;
