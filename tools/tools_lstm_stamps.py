@@ -12,7 +12,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # repo root
 from multimodalreactiongeneration_amd import _lib, functional as Fn  # noqa: E402
 
-H, B, T = 256, 64, 300
+H, B, T = int(os.environ.get("H", "256")), 64, 300
 dev = "cuda:0"
 lib = _lib.load()
 FWD = ["gemv", "reduce+pre", "sync1", "cell+publish", "gather", "sync2"]
