@@ -987,8 +987,10 @@ class _LSTMFn(Function):
     """``nprob`` same-shape single-layer LSTM directions in one persistent launch.
 
     tensors = [x, w_ih, w_hh, b_ih, b_hh, h0, c0] * nprob (h0/c0 may be None).
-    concat: all problems share x and write one [B, T, nprob*H] output
-    (bidirectional layer: forward then reverse, like nn.LSTM).
+    concat: True = all problems share x and write one [B, T, nprob*H] output (bidirectional layer:
+    forward then reverse, like nn.LSTM); an int g = consecutive groups of g problems, each group
+    sharing its x and writing one [B, T, g*H] output (several bidirectional layers on different
+    inputs in one launch: g = 2); False = one output per problem.
     Outputs: (y...) then (hT_i, cT_i) per problem.
     """
 
@@ -1011,9 +1013,13 @@ class _LSTMFn(Function):
         if not lib.mrg_lstm_supported_hidden(H):
             raise RuntimeError(f"LSTM hidden size {H} not supported by libmrg (16/32/64/128/256)")
         xs = [p[0].contiguous() for p in probs]
+        gs = nprob if concat is True else (1 if concat is False else int(concat))   # problems per output
+        if nprob % gs or (resln and gs > 1):
+            raise ValueError(f"lstm: {nprob} problems do not form groups of {gs}")
+        concat = gs > 1
         gxs, ys, y_ptrs, y_bs, y_ts = [], [], [], [], []
         if concat:
-            ycat = torch.empty(B, T, nprob * H, device=dev, dtype=torch.float32)
+            ycats = [torch.empty(B, T, gs * H, device=dev, dtype=torch.float32) for _ in range(nprob // gs)]
         for i, p in enumerate(probs):
             x, w_ih, b_ih = xs[i], p[1], p[3]
             In_i = x.shape[2]
@@ -1022,9 +1028,9 @@ class _LSTMFn(Function):
             _wt_note(w_ih, B * T, ctx.needs_input_grad[1 + K * i])
             gxs.append(gx)
             if concat:
-                y_ptrs.append(_ptr(ycat, i * H))
-                y_bs.append(T * nprob * H)
-                y_ts.append(nprob * H)
+                y_ptrs.append(_ptr(ycats[i // gs], (i % gs) * H))
+                y_bs.append(T * gs * H)
+                y_ts.append(gs * H)
             else:
                 y = torch.empty(B, T, H, device=dev, dtype=torch.float32)
                 ys.append(y)
@@ -1058,11 +1064,11 @@ class _LSTMFn(Function):
             _lib.cu_count(dev.index or 0), force_bs, _stream())
         pr.__exit__()
         _lib.check(rc, "lstm fwd")
-        ctx.spec = (nprob, concat, tuple(reverse), force_bs, B, T, H, resln)
+        ctx.spec = (nprob, gs, tuple(reverse), force_bs, B, T, H, resln)
         ctx.has_h0 = [h is not None for h in h0]
         ctx.has_c0 = [c is not None for c in c0]
         ctx.y_layout = (y_bs, y_ts)
-        yout = [ycat] if concat else ys
+        yout = ycats if concat else ys
         save = []
         uout = []
         for i, p in enumerate(probs):
@@ -1073,7 +1079,8 @@ class _LSTMFn(Function):
                 save += [p[7], p[8], mean, rstd]
         save += yout
         ctx.save_for_backward(*save)
-        ctx.shared_x = [any(probs[i][0] is probs[k][0] for k in range(i)) for i in range(nprob)]
+        # each problem's x owner: the first problem holding the same tensor (its dx collects theirs)
+        ctx.x_owner = [next(k for k in range(i + 1) if probs[k][0] is probs[i][0]) for i in range(nprob)]
         outs = list(uout if resln else yout)
         for i in range(nprob):
             outs += [hT[i], cT[i]]
@@ -1082,14 +1089,15 @@ class _LSTMFn(Function):
     @staticmethod
     @_keeps_precision
     def backward(ctx, *grads):
-        nprob, concat, reverse, force_bs, B, T, H, resln = ctx.spec
+        nprob, gs, reverse, force_bs, B, T, H, resln = ctx.spec
+        concat = gs > 1
         saved = ctx.saved_tensors
         S = 13 if resln else 9
         per = [saved[S * i:S * i + S] for i in range(nprob)]
         yout = saved[S * nprob:]
         dev = yout[0].device
         lib = _lib.load()
-        ny = 1 if concat else nprob
+        ny = nprob // gs
         gy = list(grads[:ny])
         gstate = grads[ny:]
         res = [None] * nprob  # residual-branch gradient g_i of LN(y_i + x_i), added by the dX GEMM
@@ -1104,7 +1112,7 @@ class _LSTMFn(Function):
         y_bs, y_ts = ctx.y_layout
         dy_ptr, dy_bs, dy_ts = [], [], []
         for i in range(nprob):
-            g = gy[0] if concat else gy[i]
+            g = gy[i // gs]
             if g is None:
                 dy_ptr.append(None)
                 dy_bs.append(0)
@@ -1112,8 +1120,8 @@ class _LSTMFn(Function):
             else:
                 g = g.contiguous()
                 if concat:
-                    gy[0] = g
-                    dy_ptr.append(_ptr(g, i * H))
+                    gy[i // gs] = g
+                    dy_ptr.append(_ptr(g, (i % gs) * H))
                 else:
                     gy[i] = g
                     dy_ptr.append(_ptr(g))
@@ -1152,7 +1160,7 @@ class _LSTMFn(Function):
         flush_beside_recurrence(dev, mark)
 
         out = [None]
-        dx_first = None
+        dx_of = {}   # first problem of each shared x -> its dx (the others add into it)
         for i in range(nprob):
             x, w_ih, w_hh, b_ih, b_hh, _g, _c, h0, _c0 = per[i][:9]
             In = x.shape[2]
@@ -1161,8 +1169,8 @@ class _LSTMFn(Function):
             gw = _gbuf(w_hh)
             if gw is not None and T > 1:
                 # sum_t dG_t^T h_{t-1}: forward dir pairs (dG[t], y[t-1]); reverse (dG[t], y[t+1])
-                yb = yout[0] if concat else yout[i]
-                yoff = i * H if concat else 0
+                yb = yout[i // gs]
+                yoff = (i % gs) * H
                 a_off = 0 if reverse[i] else 4 * H
                 b_off = yoff + (y_ts[i] if reverse[i] else 0)
                 _wgrad(_ptr(g, a_off), 4 * H, _ptr(yb, b_off), y_ts[i], B * (T - 1), 4 * H, H, gw, dev,
@@ -1179,8 +1187,9 @@ class _LSTMFn(Function):
                    keep=(g, x))
             dx = None
             if need[1 + K * i]:
-                if ctx.shared_x[i] and dx_first is not None:
-                    _dx_gemm(rows, In, 4 * H, _ptr(g), 4 * H, w_ih, _ptr(dx_first), In, beta=1.0, device=dev)
+                owner = ctx.x_owner[i]
+                if owner != i and owner in dx_of:
+                    _dx_gemm(rows, In, 4 * H, _ptr(g), 4 * H, w_ih, _ptr(dx_of[owner]), In, beta=1.0, device=dev)
                 else:
                     dx = torch.empty(B, T, In, device=dev, dtype=torch.float32)
                     if res[i] is not None:  # dx = dG W_ih + g (residual branch in the epilogue)
@@ -1188,8 +1197,7 @@ class _LSTMFn(Function):
                                  ldaux=In, device=dev)
                     else:
                         _dx_gemm(rows, In, 4 * H, _ptr(g), 4 * H, w_ih, _ptr(dx), In, device=dev)
-                    if dx_first is None:
-                        dx_first = dx
+                    dx_of[i] = dx
             out += [dx, None, None, None, None, dh0[i], dc0[i]] + ([None, None] if resln else [])
         return tuple(out)
 
@@ -1305,6 +1313,21 @@ def lstm_layers_batched(problems: Sequence[Sequence], force_bs=0):
                 for p in problems]
     outs = _LSTMFn.apply((n, False, (False,) * n, force_bs, eps), *flat)
     return list(outs[:n])
+
+
+def lstm_bidirectional_layers(layers, force_bs=0):
+    """Several independent bidirectional nn.LSTM layers (zero initial state) in ONE persistent launch:
+    layers = [(x [B, T, In_i], fw, bw)] with fw / bw = (w_ih, w_hh, b_ih, b_hh), the same B, T and
+    hidden size.  Returns [(y [B, T, 2H], hT [2, B, H], cT [2, B, H])] per layer."""
+    flat, rev = [], []
+    for x, fw, bw in layers:
+        flat += [x, *fw, None, None, x, *bw, None, None]
+        rev += [False, True]
+    n = len(layers)
+    outs = _LSTMFn.apply((2 * n, 2, tuple(rev), force_bs, None), *flat)
+    ys, st = outs[:n], outs[n:]
+    return [(ys[k], torch.stack([st[4 * k], st[4 * k + 2]]), torch.stack([st[4 * k + 1], st[4 * k + 3]]))
+            for k in range(n)]
 
 
 def lstm_bidirectional_layer(x, fw, bw, h0=None, c0=None, force_bs=0):

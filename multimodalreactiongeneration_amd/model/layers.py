@@ -177,6 +177,11 @@ class LSTM(nn.Module):
                 getattr(self, f"bias_ih_{sfx}"), getattr(self, f"bias_hh_{sfx}"))
 
     def forward(self, x, hx=None):
+        pre = self.__dict__.pop("_paired_out", None)   # computed in a shared launch (paired_lstm_layerd)
+        if pre is not None:
+            if pre[0] is not x:
+                raise RuntimeError("LSTM: a paired result was left for a different input")
+            return pre[1]
         if self.dropout and self.training and self.num_layers > 1:
             _unsupported("LSTM inter-layer dropout")
         D = 2 if self.bidirectional else 1
@@ -406,6 +411,43 @@ class LSTMLayerd(nn.Module):
         for i, block in enumerate(self.lstm_layered):
             input_tensor, _ = block(input_tensor, None if hxs is None else hxs[i])
         return input_tensor, hxs
+
+
+def _block_lstm(block):
+    """The LSTM inside an LSTMBlock (through its ResidualConnection and LSTMModule), or None."""
+    m = block.lstm_module
+    m = getattr(m, "module", m)
+    lstm = getattr(m, "lstm_module", None)
+    return lstm if isinstance(lstm, LSTM) else None
+
+
+def paired_lstm_layerd(stacks, xs):
+    """Independent LSTMLayerd stacks over their own inputs (SimpleLSTM's acoustic and motion encoders,
+    simple_lstm.py:146-207) with block i's bidirectional recurrences of ALL stacks in one persistent
+    launch (functional.lstm_bidirectional_layers), the rest of each block as usual.  Returns the
+    stacks' outputs, or None when they are outside that form (different depth, hidden size, B or T,
+    multi-layer LSTMs, one direction)."""
+    nb = len(stacks[0].lstm_layered)
+    if any(len(st.lstm_layered) != nb for st in stacks) or len({tuple(x.shape[:2]) for x in xs}) != 1:
+        return None
+    lstms = [[_block_lstm(b) for b in st.lstm_layered] for st in stacks]
+    for col in zip(*lstms):
+        if any(l is None or l.num_layers != 1 or not l.bidirectional for l in col):
+            return None
+        if len({l.hidden_size for l in col}) != 1:
+            return None
+    xs = list(xs)
+    for i in range(nb):
+        res = Fn.lstm_bidirectional_layers([(x, ls[i].direction_params(0, False), ls[i].direction_params(0, True))
+                                            for x, ls in zip(xs, lstms)])
+        for k, (st, ls) in enumerate(zip(stacks, lstms)):
+            y, hT, cT = res[k]
+            ls[i]._paired_out = (xs[k], (y, (hT, cT)))
+            try:
+                xs[k], _ = st.lstm_layered[i](xs[k], None)
+            finally:
+                ls[i].__dict__.pop("_paired_out", None)
+    return xs
 
 
 class MultiModalAttentionBlockSequential(nn.Module):

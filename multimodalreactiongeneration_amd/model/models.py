@@ -23,6 +23,7 @@ from __future__ import annotations
 
 import functools
 import math
+import os
 from collections import OrderedDict
 from typing import Any, Dict, List, Tuple
 
@@ -32,7 +33,8 @@ from torch import nn
 from .. import functional as Fn
 from ..configs import as_attr
 from ..optim import FusedAdamW
-from .layers import Linear, LSTMSampler, LSTMLayerd, MultimodalAttention, ResidualConnection, run_sequential_ffn
+from .layers import (Linear, LSTMSampler, LSTMLayerd, MultimodalAttention, ResidualConnection, paired_lstm_layerd,
+                     run_sequential_ffn)
 from .masks import gen_attention_mask
 from .metaformer import MultiModalMetaformer
 from .mixers import mixer_layerd_argments_select, feedforward_block_argments
@@ -608,10 +610,17 @@ class SimpleLSTM(LightningSurface):
         self.all_static = cfg.get("all_static", False)
         self.delta_order = metrics.delta_order
 
+    # MI355X schedule: the acoustic and motion encoders' block-i recurrences share one launch
+    # (layers.paired_lstm_layerd); MRG_PAIR_ENCODERS=0 runs the encoders one after the other
+    pair_encoders = os.environ.get("MRG_PAIR_ENCODERS", "1") == "1"
+
     @_in_precision
     def forward(self, acoustic_feature, motion_feature):
-        ae = self.acoustic_encoder(acoustic_feature)
-        me = self.motion_encoder(motion_feature)
+        enc_a, enc_m = self.acoustic_encoder, self.motion_encoder
+        xa, xm = enc_a.embed_layer(acoustic_feature), enc_m.embed_layer(motion_feature)
+        out = paired_lstm_layerd([enc_a.acostic_lstm, enc_m.motion_lstm], [xa, xm]) if self.pair_encoders \
+            else None
+        ae, me = out if out is not None else (enc_a.acostic_lstm(xa)[0], enc_m.motion_lstm(xm)[0])
         return self.motion_decoder(self.multimodal_att(me, ae))
 
     def lossfun(self):

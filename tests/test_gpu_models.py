@@ -369,6 +369,46 @@ def test_simple_lstm_benchmark_width_vs_oracle():
     assert worst[0] < TOL, worst
 
 
+@pytest.mark.parametrize("precision", ["32", "bf16"])
+def test_simple_lstm_paired_encoders_match_sequential(precision):
+    """configs[1] (B=64, T=300): the acoustic and motion encoders' recurrences sharing one launch per
+    block (layers.paired_lstm_layerd, the default) give bitwise the loss and gradients of the two
+    encoders run one after the other; the pairing did run (both LSTMs' paired results consumed)."""
+    from multimodalreactiongeneration_amd import configs as C
+    from multimodalreactiongeneration_amd.model import SimpleLSTM
+    from multimodalreactiongeneration_amd.model import layers as LY
+    from multimodalreactiongeneration_amd.synthetic import make_simple_batch
+    cfg, oc, me = C.simple_lstm_config()
+    torch.manual_seed(4)
+    m = SimpleLSTM(cfg, oc, me).to(DEV)
+    m.set_precision(precision)
+    a, mo, t = (x.to(DEV) for x in make_simple_batch(B=64, T=300, seed=23))
+    calls = []
+    orig = LY.paired_lstm_layerd
+
+    def spy(stacks, xs):
+        out = orig(stacks, xs)
+        calls.append(out is not None)
+        return out
+    res = {}
+    try:
+        LY_models = __import__("multimodalreactiongeneration_amd.model.models", fromlist=["x"])
+        LY_models.paired_lstm_layerd = spy
+        for pair in (True, False):
+            m.pair_encoders = pair
+            for p in m.parameters():
+                p.grad = None
+            loss, _ = _train_step(m, (a, mo, t))
+            res[pair] = (loss.detach().clone(), [p.grad.clone() for p in m.parameters()])
+    finally:
+        LY_models.paired_lstm_layerd = orig
+        m.pair_encoders = type(m).pair_encoders
+    assert calls == [True]
+    assert torch.equal(res[True][0], res[False][0])
+    for g1, g0 in zip(res[True][1], res[False][1]):
+        assert torch.equal(g1, g0)
+
+
 def test_metaformer_q9_benchmark_width_vs_oracle():
     """Benchmark architecture (H=256, 5 blocks, 5 encoder layers, r=1), 24 frames, ragged: the
     scheduled-sampling training loss over the Q9 broadcast target + every gradient, and the
