@@ -34,6 +34,12 @@ def check_form_modal_num(modal_num: int, sameone, msg: str = None) -> list:
     return sameone
 
 
+
+# the fused integrator also serves the T = 1 frames of autoregressive generation (one launch per
+# batched projection / LayerNorm instead of per-integrator modules, no mask or concat glue);
+# MRG_FUSED_T1=0 keeps those frames on the per-module path
+_FUSED_MIN_T = 1 if os.environ.get("MRG_FUSED_T1", "1") == "1" else 2
+
 class MultiModalEmbedding(nn.Module):
     def __init__(self, modal_num: int, mixer_configs):
         super().__init__()
@@ -102,7 +108,7 @@ class IntegrateModalBlock(nn.Module):
         form (integrate.py, block_stack.py), or None when the block is outside it."""
         from .masks import BlockCausalMask
         if not (self.use_fused and isinstance(main_modal, torch.Tensor) and main_modal.is_cuda
-                and main_modal.dim() == 3 and main_modal.shape[1] > 1 and all(h is None for h in hxs)):
+                and main_modal.dim() == 3 and main_modal.shape[1] >= _FUSED_MIN_T and all(h is None for h in hxs)):
             return None
         B, T, E = main_modal.shape
         n = len(self.integrators)
