@@ -599,10 +599,13 @@ static bool try_tile(K kernel, int nt, long nblk, int cus, bool last_solo, hipSt
   return true;
 }
 
-// one-barrier solo forward (lstm_fwd_solo_kernel); MRG_LSTM_SOLO1=0 keeps the two-barrier solo form
+// one-barrier solo forward (lstm_fwd_solo_kernel), opt-in MRG_LSTM_SOLO1=1.  Measured (r04,
+// profiles/r04_lstm_solo1.txt, B = 64, T = 300, ns per step at one problem): H = 128 1245 vs 1054 for
+// the two-barrier solo form, H = 64 775 vs 924, H = 32 823 vs 632; C2 12.35 vs 11.95 ms/step.  With
+// one lane in KC running each cell, the cell phase serialises within the wave.
 static int g_solo1 = [] {
   const char* e = getenv("MRG_LSTM_SOLO1");
-  return (e && atoi(e) == 0) ? 0 : 1;
+  return (e && atoi(e) == 1) ? 1 : 0;
 }();
 
 template <int H>
