@@ -41,7 +41,7 @@ from torch.autograd import Function
 from . import _lib
 from . import functional as Fn
 from .encoder_stack import (VP, CL, CI, _arr, _bln_fwd, _bln_bwd, _chunks, _groups, _maxp, _RingPool,
-                            _launch_fwd, _launch_bwd, _ln_blocks, _p)
+                            _launch_fwd, _launch_bwd, _ln_blocks, _ln_rows, _p)
 from .functional import _ptr, _stream, gemm, _dx_gemm, _wt_note, _gbuf, _on_side
 
 # time steps per chunk; MRG_BLOCK_CHUNK overrides (0 turns the wavefront off: per-block schedule)
@@ -421,7 +421,7 @@ class _BlockStackFn(Function):
                 return
             scratch = Fn._ws(2 * E * 4, dev).view(2, E) if (gg is None or gb is None) else None
             _lib.check(lib.mrg_residual_layernorm_param_reduce(
-                nblk * 32, E, _ptr(ws), _ptr(gg if gg is not None else scratch[0]),
+                _ln_rows(lib, nblk, E), E, _ptr(ws), _ptr(gg if gg is not None else scratch[0]),
                 _ptr(gb if gb is not None else scratch[1]), 1, _stream()), "layernorm param reduce")
 
         def sl(p, a, b):

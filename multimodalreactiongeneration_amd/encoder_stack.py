@@ -485,12 +485,13 @@ class _EncoderStackFn(Function):
                  b_div=kw.get("x_div", 0), splits=Fn.wgrad_splits(Nout, Nin, n), device=dev,
                  asum_out=_ptr(kw.get("gb")), asum_out2=_ptr(kw.get("gb2")))
 
+        # the partial blocks to reduce: one chunk's (starting at block bo), or every chunk's
+        nb = gr["nblk"] if (t0 == 0 and t1 == T) else _ln_blocks(lib, rows, H)
+
         def ln_reduce(ws, gg, gb):
-            # the chunk's partial blocks start at block bo; rows = the chunk's rows (the reduce derives
-            # the block count from them as the LayerNorm backward did)
             scratch = Fn._ws(2 * H * 4, dev).view(2, H) if (gg is None or gb is None) else None
             _lib.check(lib.mrg_residual_layernorm_param_reduce(
-                rows, H, _p(ws, bo * 2 * H), _ptr(gg if gg is not None else scratch[0]),
+                _ln_rows(lib, nb, H), H, _p(ws, bo * 2 * H), _ptr(gg if gg is not None else scratch[0]),
                 _ptr(gb if gb is not None else scratch[1]), 1, _stream()), "layernorm param reduce")
 
         parts = [lambda: wg(_p(dG, r0 * 4 * H), 4 * H, _p(st["x"], r0 * H), H, rows, 4 * H, H, gw_ih, gb=first,
@@ -525,6 +526,14 @@ def _ln_blocks(lib, rows, H) -> int:
     """LayerNorm-backward partial blocks of `rows` rows (from the C ABI's workspace size, so the row
     count per block is never restated here)."""
     return int(lib.mrg_residual_layernorm_bwd_workspace_bytes(rows, H)) // (2 * H * 4)
+
+
+def _ln_rows(lib, nblk, H) -> int:
+    """A row count whose parameter reduce covers exactly `nblk` partial blocks: chunks of a length that
+    is not a multiple of the block rows leave a partial block each, so the sum of the chunks' blocks
+    can exceed the blocks of their total rows (B = 4, 100-step chunks: 3 x 13 blocks, not 38)."""
+    rpb = 4096 // _ln_blocks(lib, 4096, H)
+    return nblk * rpb
 
 
 def stack_eligible(H, B) -> bool:

@@ -186,8 +186,8 @@ def test_metaformer_benchmark_width_vs_oracle(ratio, B, T):
     torch.cuda.synchronize()
     ref_loss, ref_y, grads, _ = O.run_train_step(O.metaformer_training_loss, sd, oc, mc, clone_batch(batch))
     assert abs(loss.item() - ref_loss.item()) / abs(ref_loss.item()) < TOL
-    worst = max(rel_err(p.grad, grads[k]) for k, p in m.named_parameters())
-    assert worst < TOL, worst
+    errs = sorted(((rel_err(p.grad, grads[k]), k) for k, p in m.named_parameters()), reverse=True)
+    assert errs[0][0] < TOL, errs[:6]
 
 
 @pytest.mark.parametrize("mode", ["full", "tf", "ss"])
