@@ -32,7 +32,7 @@ METRIC = "training frames/sec/GPU, lstmformer T=300 B=64; 1→8 GPU scaling"
 FP32_MFMA_PEAK_TF = 157.3   # MI355X_MICROARCH.md chip table (f32 matrix, dense)
 BF16_MFMA_PEAK_TF = 2500.0  # MI355X_MICROARCH.md chip table (bf16 matrix, dense)
 HBM_PEAK_GBS = 8000.0
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03_pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r04_pmc_summary.json")
 
 # probe name (functional._probe) -> kernels it brackets; FLOPs are algorithmic
 FAMILIES = {
@@ -56,7 +56,7 @@ PMC_KEYS = {"gemm": "gemm_all", "lstm_fwd": "lstm_fwd", "lstm_bwd": "lstm_bwd",
             "attn_fwd": "attn_fwd_kernel", "attn_bwd": "attn_bwd"}
 
 
-TRACE_SUMMARY = os.path.join(ROOT, "profiles", "r03_trace_roofline.json")
+TRACE_SUMMARY = os.path.join(ROOT, "profiles", "r04_trace_roofline.json")
 
 
 def trace_check(roof):
