@@ -19,4 +19,4 @@ for v in base stack; do
     || { tail -20 $O/bench_$v.log; exit 1; }
   grep -o '"ms_per_step": [0-9.]*' $O/bench_$v.log | head -1
 done
-bash tools/tools_gpu_r03_prof.sh
+bash tools/runs/tools_gpu_r03_prof.sh
