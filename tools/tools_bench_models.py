@@ -64,6 +64,8 @@ def main():
         return main_lws(steps, only, out)
     mc, oc, me = C.simple_lstm_config()
     m = SimpleLSTM(mc, oc, me).to(DEV)
+    prec = os.environ.get("C2_PRECISION", "32")   # "bf16": the BASELINE configs[1] precision
+    m.set_precision(prec)
     opt = m.configure_optimizers()["optimizer"]
     batch = make_simple_batch(B=64, T=300, device=DEV)
 
@@ -72,7 +74,7 @@ def main():
         m.training_step(batch)["loss"].backward()
         opt.step()
     ms = timed(step_simple, steps)
-    out["C2_simple_lstm_fp32_B64_T300" + ("_graph" if GRAPH else "")] = {"ms_per_step": round(ms, 2), "frames_per_s": round(64 * 300 / ms * 1e3)}
+    out[f"C2_simple_lstm_{'fp32' if prec == '32' else prec}_B64_T300" + ("_graph" if GRAPH else "")] = {"ms_per_step": round(ms, 2), "frames_per_s": round(64 * 300 / ms * 1e3)}
     print(json.dumps(out), flush=True)
     if not only:
         main_lws(steps, only, out)
