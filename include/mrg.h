@@ -176,6 +176,23 @@ int mrg_gru_cell_bwd(int B, int H, const float* gates, long g_ld, const float* g
                      long hp_ld, const float* dy, long dy_ld, const float* dh_next, float* dgx, float* dgh,
                      long d_ld, float* dhp, hipStream_t stream);
 
+/* Persistent GRU recurrence (one launch per layer direction; replaces the per-step products + cells
+ * above for torch.nn.GRU at H = 256 / 128 / 64 / 32, mixer_block.py:169-208).  Same tensors as the
+ * per-step path: gx [B, T, 3H] (strides bs / ts), y, gates (r, z, n), ghn; bwd writes dgx / dgh (the
+ * input / weight gradient GEMMs' operands) and dh0.  xbuf: mrg_gru_xbuf_bytes(B, H) zeroed bytes per
+ * launch; err: the device flag a hand-off timeout sets (as mrg_lstm_fwd's).  h0 / dy / dhT / dh0
+ * nullable.  */
+int mrg_gru_supported_hidden(int H);
+size_t mrg_gru_xbuf_bytes(int B, int H);
+int mrg_gru_fwd(int B, int T, int H, const float* gx, long gx_bs, long gx_ts, const float* w_hh,
+                const float* b_hh, const float* h0, float* y, long y_bs, long y_ts, float* gates, long g_bs,
+                long g_ts, float* ghn, long n_bs, long n_ts, int reverse, void* xbuf, int* err, int cus,
+                hipStream_t stream);
+int mrg_gru_bwd(int B, int T, int H, const float* w_hh, const float* gates, long g_bs, long g_ts,
+                const float* ghn, long n_bs, long n_ts, const float* y, long y_bs, long y_ts, const float* h0,
+                const float* dy, long dy_bs, long dy_ts, const float* dhT, float* dgx, float* dgh, long d_bs,
+                long d_ts, float* dh0, int reverse, void* xbuf, int* err, int cus, hipStream_t stream);
+
 /* ---------------------------------------------------------------- scheduled-sampling decode
  * The per-frame kernels of lstm_with_sampling's autoregressive training step
  * (LSTMwithSample.head_motion_generation / generate_one_step, lstm_with_sample.py:379-433), whose

@@ -79,6 +79,12 @@ SIGNATURES = {
     "mrg_lstm_cell_bwd": (c_int, [c_int, c_int, P, P, P, P, c_long, P, P, P, P, P]),
     "mrg_gru_cell_fwd": (c_int, [c_int, c_int, P, c_long, P, P, P, c_long, P, c_long, P, c_long, P, c_long, P]),
     "mrg_gru_cell_bwd": (c_int, [c_int, c_int, P, c_long, P, c_long, P, c_long, P, c_long, P, P, P, c_long, P, P]),
+    "mrg_gru_supported_hidden": (c_int, [c_int]),
+    "mrg_gru_xbuf_bytes": (c_size, [c_int, c_int]),
+    "mrg_gru_fwd": (c_int, [c_int, c_int, c_int, P, c_long, c_long, P, P, P, P, c_long, c_long, P, c_long, c_long,
+                            P, c_long, c_long, c_int, P, P, c_int, P]),
+    "mrg_gru_bwd": (c_int, [c_int, c_int, c_int, P, P, c_long, c_long, P, c_long, c_long, P, c_long, c_long, P,
+                            P, c_long, c_long, P, P, P, c_long, c_long, P, c_int, P, P, c_int, P]),
     "mrg_fbank_finish": (c_int, [c_int, c_int, c_int, P, c_long, P, P, c_long, c_int, c_int, c_long, P, c_long, P]),
     "mrg_feature_delta": (c_int, [c_int, c_int, c_int, P, c_long, c_int, P, P]),
     "mrg_pad_sequences": (c_int, [c_int, c_int, c_int, P, P, c_float, P, P]),

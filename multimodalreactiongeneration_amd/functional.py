@@ -1364,9 +1364,23 @@ class _GRUFn(Function):
         y = torch.empty(B, T, H, device=dev, dtype=torch.float32)
         gates = torch.empty(B, T, H3, device=dev, dtype=torch.float32)
         ghn = torch.empty(B, T, H, device=dev, dtype=torch.float32)
+        h0c = None if h0 is None else h0.contiguous()
+        ctx.persist = _GRU_PERSIST[0] and T > 1 and bool(lib.mrg_gru_supported_hidden(H))
+        if ctx.persist:   # one persistent launch for all steps (gru_rec.hip)
+            xb = zeros(max(1, lib.mrg_gru_xbuf_bytes(B, H) // 8), dtype=torch.int64, device=dev)
+            with _probe("gru_fwd", 6.0 * H * H * B * T):
+                rc = lib.mrg_gru_fwd(B, T, H, _ptr(gx), T * H3, H3, _ptr(w_hh), _ptr(b_hh), _ptr(h0c), _ptr(y), T * H,
+                                     H, _ptr(gates), T * H3, H3, _ptr(ghn), T * H, H, int(bool(reverse)), _ptr(xb),
+                                     _ptr(_err_flag(dev)), _lib.cu_count(dev.index or 0), _stream())
+            _lib.check(rc, "gru fwd")
+            prev = 0 if reverse else T - 1
+            hT = y[:, prev].clone()
+            ctx.reverse = bool(reverse)
+            ctx.save_for_backward(x, w_ih, w_hh, b_ih, b_hh, h0c, y, gates, ghn)
+            ctx.set_materialize_grads(False)
+            return y, hT
         gh = torch.empty(B, H3, device=dev, dtype=torch.float32)
         zero = torch.zeros(B, H3, device=dev, dtype=torch.float32) if h0 is None else None
-        h0c = None if h0 is None else h0.contiguous()
         prev = None
         for t in (range(T - 1, -1, -1) if reverse else range(T)):
             if prev is None:
@@ -1399,7 +1413,17 @@ class _GRUFn(Function):
         dGX = torch.empty(B, T, H3, device=dev, dtype=torch.float32)
         dGH = torch.empty(B, T, H3, device=dev, dtype=torch.float32)
         dh_next = None if dhT is None else dhT.contiguous()
-        for t in (range(T) if reverse else range(T - 1, -1, -1)):
+        need = ctx.needs_input_grad
+        if ctx.persist:
+            xb = zeros(max(1, lib.mrg_gru_xbuf_bytes(B, H) // 8), dtype=torch.int64, device=dev)
+            dh_next = torch.empty(B, H, device=dev, dtype=torch.float32) if (h0c is not None and need[6]) else None
+            with _probe("gru_bwd", 6.0 * H * H * B * T):
+                rc = lib.mrg_gru_bwd(B, T, H, _ptr(w_hh), _ptr(gates), T * H3, H3, _ptr(ghn), T * H, H, _ptr(y), T * H,
+                                     H, _ptr(h0c), _ptr(dy), T * H, H, _ptr(None if dhT is None else dhT.contiguous()),
+                                     _ptr(dGX), _ptr(dGH), T * H3, H3, _ptr(dh_next), int(reverse), _ptr(xb),
+                                     _ptr(_err_flag(dev)), _lib.cu_count(dev.index or 0), _stream())
+            _lib.check(rc, "gru bwd")
+        for t in ((range(T) if reverse else range(T - 1, -1, -1)) if not ctx.persist else ()):
             pt = t + 1 if reverse else t - 1
             if 0 <= pt < T:
                 hp, hp_ld = _ptr(y, pt * H), T * H
@@ -1412,7 +1436,6 @@ class _GRUFn(Function):
                        "gru cell bwd")
             gemm(B, H, H3, _ptr(dGH, t * H3), 0, T * H3, _ptr(w_hh), 0, H, _ptr(dhp), H, beta=1.0, device=dev)
             dh_next = dhp
-        need = ctx.needs_input_grad
         dh0 = dh_next if (h0c is not None and need[6]) else None
         _wgrad(_ptr(dGX), H3, _ptr(x), In, B * T, H3, In, _gbuf(w_ih), dev, gb=_gbuf(b_ih), keep=(dGX, x))
         gw = _gbuf(w_hh)
@@ -1435,6 +1458,10 @@ class _GRUFn(Function):
             dx = torch.empty(B, T, In, device=dev, dtype=torch.float32)
             gemm(B * T, In, H3, _ptr(dGX), 0, H3, _ptr(w_ih), 0, In, _ptr(dx), In, device=dev)
         return None, dx, None, None, None, None, dh0
+
+
+# persistent GRU recurrences (gru_rec.hip); MRG_GRU_PERSIST=0 runs the per-step products + cells
+_GRU_PERSIST = [os.environ.get("MRG_GRU_PERSIST", "1") == "1"]
 
 
 def gru_layer(x, w_ih, w_hh, b_ih, b_hh, h0=None, reverse=False):

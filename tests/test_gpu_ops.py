@@ -955,10 +955,12 @@ def test_adamw_matches_oracle_over_three_steps():
 
 
 @pytest.mark.parametrize("In,H,B,T,bidir,state", [(16, 32, 4, 20, False, False), (24, 32, 3, 9, True, True),
-                                                  (256, 256, 64, 40, False, True)])
+                                                  (256, 256, 64, 40, False, True), (256, 256, 37, 25, True, False),
+                                                  (128, 128, 64, 30, True, True), (40, 64, 9, 17, False, True)])
 def test_gru_vs_torch_fp64(In, H, B, T, bidir, state):
-    """layers.GRU (the GRU cell kernels + few-row GEMMs) vs torch.nn.GRU in fp64: outputs, final
-    states, input / state / every parameter gradient."""
+    """layers.GRU (persistent recurrences, gru_rec.hip: ring groups at H = 256, solo groups below) vs
+    torch.nn.GRU in fp64: outputs, final states, input / state / every parameter gradient (SURVEY 8f
+    rank 4)."""
     from multimodalreactiongeneration_amd.model.layers import GRU
     torch.manual_seed(In + H + T)
     ref = torch.nn.GRU(In, H, num_layers=2, batch_first=True, bidirectional=bidir).double()
@@ -987,6 +989,37 @@ def test_gru_vs_torch_fp64(In, H, B, T, bidir, state):
     gp = dict(g.named_parameters())
     for k, p in ref.named_parameters():
         assert rel_err(gp[k].grad, p.grad) < TOL, k
+
+
+@pytest.mark.parametrize("H,B,T,reverse", [(256, 64, 300, False), (128, 64, 300, True)])
+def test_gru_persistent_matches_per_step(H, B, T, reverse):
+    """The persistent GRU recurrence (one launch per layer direction) vs the per-step products + cell
+    kernels at the GRU config's width (B = 64, T = 300): outputs, final state and every gradient."""
+    from multimodalreactiongeneration_amd import functional as Fn
+    g = torch.Generator().manual_seed(H + T)
+    s = 1.0 / math.sqrt(H)
+    w = [torch.randn(3 * H, H, generator=g) * s for _ in range(2)]
+    bb = [torch.randn(3 * H, generator=g) * s for _ in range(2)]
+    x = torch.randn(B, T, H, generator=g)
+    h0 = torch.randn(B, H, generator=g) * 0.5
+    dy = torch.randn(B, T, H, generator=g)
+    outs = []
+    prev = Fn._GRU_PERSIST[0]
+    try:
+        for persist in (True, False):
+            Fn._GRU_PERSIST[0] = persist
+            ps = [_param(t) for t in (w[0], w[1], bb[0], bb[1])]
+            xx = x.to(DEV).requires_grad_(True)
+            hh = h0.to(DEV).requires_grad_(True)
+            y, hT = Fn.gru_layer(xx, *ps, hh, reverse=reverse)
+            ((y * dy.to(DEV)).sum() + hT.square().sum()).backward()
+            torch.cuda.synchronize()
+            Fn.check_errors()
+            outs.append([y.detach(), hT.detach(), xx.grad, hh.grad] + [p.grad for p in ps])
+    finally:
+        Fn._GRU_PERSIST[0] = prev
+    for a, b in zip(*outs):
+        assert rel_err(a, b) < TOL
 
 
 def test_adamw_graph_replay_follows_lr_scheduler():
