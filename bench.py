@@ -249,12 +249,13 @@ def dry_run(args):
         dist.destroy_process_group()
 
 
-def model_flops_per_frame(cfg, ratio):
-    """Algorithmic training FLOPs per prediction frame (SURVEY §8d formula; train = 3 x fwd)."""
+def model_flops_per_frame(cfg, ratio, gates=4):
+    """Algorithmic training FLOPs per prediction frame (SURVEY §8d formula; train = 3 x fwd); gates = 3
+    for the GRU mixers of config_gru.yaml (every recurrent layer a GRU)."""
     H, Hb, N, E = cfg.hidden_size, cfg.bottleneck_size, cfg.num_block, cfg.encoder_num_layer
     Fa, Fm, T = 40, 6, 1.0
     L = N * T + E * ratio * T + E * T
-    lstm = 16 * H * H * L
+    lstm = 4 * gates * H * H * L
     lin = (4 * T * H * Fm + 2 * ratio * T * H * Fa + 2 * H * H * L
            + N * (12 * T * H * H + 4 * H * H * (ratio * T + T) + 4 * T * H * H + 4 * T * H * Hb)
            + 2 * T * (H * Hb + Hb * Fm))
@@ -602,6 +603,27 @@ def secondary(args, dev):
         "lstmformer autoregressive generation (Metaformer.prediction, full_generation, eval, no grad) "
         "B=64 x 300 frames, HIP graph; one step = one 64-clip batch", ms, B * T, gen_flops_per_frame(mc, 1), "fp32",
         kern, cpu)
+    del m, replay
+
+    progress("lstmformer GRU config")
+    # lstmformer with config_gru.yaml's mixers (every recurrent layer a GRU)
+    mc, oc, me = C.lstmformer_config(ratio=1, emb_mixers=("gru", "gru", "gru"))
+    torch.manual_seed(0)
+    m = Metaformer(mc, oc, me).to(dev)
+    opt = m.configure_optimizers()["optimizer"]
+    batch = make_batch(B=B, T=T, seed=1234, device=dev)
+
+    def step_gru():
+        opt.zero_grad()
+        m.training_step(list(batch))["loss"].backward()
+        opt.step()
+    replay = capture(step_gru, 2, preserve=opt.state_tensors())
+    ms = _timed_replay(replay, K, W)
+    out["lstmformer_gru_train"] = _secondary_entry(
+        "lstmformer train step with config_gru.yaml's GRU mixers (persistent GRU recurrences), B=64 T=300 r=1, "
+        "HIP graph", ms, B * T, model_flops_per_frame(mc, 1, gates=3) + attn_flops_per_frame(mc, 1, T), "fp32",
+        ({}, None), None)
+    del m, opt, replay
     Fn.check_errors()
     return out
 
