@@ -1417,12 +1417,15 @@ class _GRUFn(Function):
         if ctx.persist:
             xb = zeros(max(1, lib.mrg_gru_xbuf_bytes(B, H) // 8), dtype=torch.int64, device=dev)
             dh_next = torch.empty(B, H, device=dev, dtype=torch.float32) if (h0c is not None and need[6]) else None
+            # deferred weight gradients (functional._DEFER) run beside this recurrence, as beside the LSTM's
+            _cap, mark = fork_beside_recurrence(dev)
             with _probe("gru_bwd", 6.0 * H * H * B * T):
                 rc = lib.mrg_gru_bwd(B, T, H, _ptr(w_hh), _ptr(gates), T * H3, H3, _ptr(ghn), T * H, H, _ptr(y), T * H,
                                      H, _ptr(h0c), _ptr(dy), T * H, H, _ptr(None if dhT is None else dhT.contiguous()),
                                      _ptr(dGX), _ptr(dGH), T * H3, H3, _ptr(dh_next), int(reverse), _ptr(xb),
                                      _ptr(_err_flag(dev)), _lib.cu_count(dev.index or 0), _stream())
             _lib.check(rc, "gru bwd")
+            flush_beside_recurrence(dev, mark)
         for t in ((range(T) if reverse else range(T - 1, -1, -1)) if not ctx.persist else ()):
             pt = t + 1 if reverse else t - 1
             if 0 <= pt < T:
