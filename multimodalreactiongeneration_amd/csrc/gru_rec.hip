@@ -195,6 +195,11 @@ __global__ __launch_bounds__((GruFwdCfg<H, G>::NT), (GruFwdCfg<H, G>::WPS)) void
   }
 }
 
+// Backward with the LSTM backward's division of labour (lstm.hip): the cell threads only poll the
+// hand-offs and run the cell; io shadow threads in the waves the cells do not use move the saved
+// values HBM -> LDS two steps ahead and write dgx / dgh, so a cell wave's single vmcnt only ever
+// covers its own polls (gfx9 counts loads and stores together).  Batch tiles whose cells fill the
+// workgroup (no spare waves) let the cells move their own values (SELF_IO).
 template <int H, int G, int BS>
 __global__ __launch_bounds__((GruBwdCfg<H, G>::NT), (GruBwdCfg<H, G>::WPS)) void gru_bwd_kernel(GruBwdArgs P) {
   using C = GruBwdCfg<H, G>;
@@ -203,8 +208,13 @@ __global__ __launch_bounds__((GruBwdCfg<H, G>::NT), (GruBwdCfg<H, G>::WPS)) void
   constexpr int RLP = ((RL / 4) % 2 == 0) ? RL + 4 : RL;
   static_assert(OT >= 1 && OT <= RC && OT * NT == RC * H && (RL % 4) == 0 && BS * U <= NT && (U % OT) == 0,
                 "bad GRU bwd tiling");
-  __shared__ __attribute__((aligned(16))) float dgl[BS][RC][RLP];
+  __shared__ __attribute__((aligned(16))) float dgl[BS][RC][RLP];   // dgh rows of the step (GEMV operand)
+  __shared__ float dxn[BS * U];                                     // dgx's n column (dgh's is dn' r)
+  __shared__ float sv[2][6][BS * U];   // r, z, n, hn, h_prev, dy of the cells, by step parity
   __shared__ float dhs[SOLO ? BS : 1][SOLO ? H : 1];
+  constexpr int CW = (BS * U + 63) / 64;
+  constexpr bool SELF_IO = CW * 64 + BS * U > NT;
+  constexpr int IOFF = SELF_IO ? 0 : CW * 64;
 
   int prob, grp, j;
   const int ngroups = (P.B + BS - 1) / BS;
@@ -228,23 +238,34 @@ __global__ __launch_bounds__((GruBwdCfg<H, G>::NT), (GruBwdCfg<H, G>::WPS)) void
   float direct = 0.0f;   // dh_{t+1} z_{t+1} of this cell's unit, carried in processing order
   float dhrec = 0.0f;
   if (cvalid && P.dhT) dhrec = P.dhT[(long)bg * H + hcol];
-  // saved values of processing step tt2: r, z, n, hn, h_prev, dy
-  float sv[6], nx[6];
-  auto load_sv = [&](int tt2, float (&o)[6]) {
-    if (!cvalid || tt2 >= T) return;
+
+  // io role: the shadow of cell (ib, iu)
+  const int iot = tid - IOFF;
+  const bool io = iot >= 0 && iot < BS * U;
+  const int ib = io ? iot / U : 0, iu = iot % U, ibg = b0 + ib;
+  const bool iovalid = io && ibg < B;
+  const int iocol = j * U + iu;
+  float pf[6];
+  auto io_load = [&](int tt2) {   // saved values of processing step tt2 -> pf
+    if (!iovalid || tt2 >= T) return;
     const int t = P.reverse ? tt2 : T - 1 - tt2;
     const int tp = P.reverse ? t + 1 : t - 1;
-    const float* gs = P.gates + (long)bg * P.g_bs + (long)t * P.g_ts + hcol;
-    o[0] = gs[0]; o[1] = gs[H]; o[2] = gs[2 * H];
-    o[3] = P.ghn[(long)bg * P.n_bs + (long)t * P.n_ts + hcol];
-    o[4] = (tp >= 0 && tp < T) ? P.y[(long)bg * P.y_bs + (long)tp * P.y_ts + hcol]
-                               : (P.h0 ? P.h0[(long)bg * H + hcol] : 0.0f);
-    o[5] = P.dy ? P.dy[(long)bg * P.dy_bs + (long)t * P.dy_ts + hcol] : 0.0f;
+    const float* gs = P.gates + (long)ibg * P.g_bs + (long)t * P.g_ts + iocol;
+    pf[0] = gs[0]; pf[1] = gs[H]; pf[2] = gs[2 * H];
+    pf[3] = P.ghn[(long)ibg * P.n_bs + (long)t * P.n_ts + iocol];
+    pf[4] = (tp >= 0 && tp < T) ? P.y[(long)ibg * P.y_bs + (long)tp * P.y_ts + iocol]
+                                : (P.h0 ? P.h0[(long)ibg * H + iocol] : 0.0f);
+    pf[5] = P.dy ? P.dy[(long)ibg * P.dy_bs + (long)t * P.dy_ts + iocol] : 0.0f;
   };
+  auto io_stage = [&](int tt2) {   // pf -> the sv slot of step tt2
+    if (!iovalid || tt2 >= T) return;
 #pragma unroll
-  for (int q = 0; q < 6; ++q) sv[q] = nx[q] = 0.0f;
-  load_sv(0, sv);
-  load_sv(1, nx);
+    for (int q = 0; q < 6; ++q) sv[tt2 & 1][q][iot] = pf[q];
+  };
+  io_load(0);
+  io_stage(0);
+  io_load(1);
+  __syncthreads();
 
   unsigned long long* xb = P.xbuf;
   const long xstride_b = (long)G * H;   // per batch row: [dest G][src G][U]
@@ -254,6 +275,7 @@ __global__ __launch_bounds__((GruBwdCfg<H, G>::NT), (GruBwdCfg<H, G>::WPS)) void
                                        : 0;
   for (int tt = 0; tt < T; ++tt) {
     const int t = P.reverse ? tt : T - 1 - tt;
+    const int r0 = cu, r1 = U + cu, r2 = 2 * U + cu;
     if (cvalid) {
       if (tt > 0) {
         float s;
@@ -270,31 +292,24 @@ __global__ __launch_bounds__((GruBwdCfg<H, G>::NT), (GruBwdCfg<H, G>::WPS)) void
         }
         dhrec = s + direct;
       }
-      const float r = sv[0], z = sv[1], n = sv[2], hn = sv[3], hprev = sv[4];
-      const float dh = sv[5] + dhrec;
+      const int sl = tt & 1;
+      const float r = sv[sl][0][tid], z = sv[sl][1][tid], n = sv[sl][2][tid];
+      const float hn = sv[sl][3][tid], hprev = sv[sl][4][tid];
+      const float dh = sv[sl][5][tid] + dhrec;
       const float dn = dh * (1.0f - z);
       const float dz = dh * (hprev - n);
       const float dpn = dn * (1.0f - n * n);
       const float dr = dpn * hn;
-      const float dpr = dr * r * (1.0f - r);
-      const float dpz = dz * z * (1.0f - z);
       direct = dh * z;
-      float* ox = P.dgx + (long)bg * P.d_bs + (long)t * P.d_ts + hcol;
-      float* oh = P.dgh + (long)bg * P.d_bs + (long)t * P.d_ts + hcol;
-      ox[0] = dpr; ox[H] = dpz; ox[2 * H] = dpn;
-      oh[0] = dpr; oh[H] = dpz; oh[2 * H] = dpn * r;
-      const int r0 = cu, r1 = U + cu, r2 = 2 * U + cu;
-      dgl[cb][r0 / RL][r0 % RL] = dpr;
-      dgl[cb][r1 / RL][r1 % RL] = dpz;
+      dgl[cb][r0 / RL][r0 % RL] = dr * r * (1.0f - r);
+      dgl[cb][r1 / RL][r1 % RL] = dz * z * (1.0f - z);
       dgl[cb][r2 / RL][r2 % RL] = dpn * r;
-#pragma unroll
-      for (int q = 0; q < 6; ++q) sv[q] = nx[q];
-      load_sv(tt + 2, nx);
+      dxn[tid] = dpn;
     } else if (cell) {
-      const int r0 = cu, r1 = U + cu, r2 = 2 * U + cu;
       dgl[cb][r0 / RL][r0 % RL] = 0.0f;
       dgl[cb][r1 / RL][r1 % RL] = 0.0f;
       dgl[cb][r2 / RL][r2 % RL] = 0.0f;
+      dxn[tid] = 0.0f;
     }
     __syncthreads();
     // partial dh_{t-1}[b][hout] = sum over this member's rows of dgh[b][row] W_hh[row][hout]
@@ -332,6 +347,17 @@ __global__ __launch_bounds__((GruBwdCfg<H, G>::NT), (GruBwdCfg<H, G>::WPS)) void
         }
       }
     }
+    if (iovalid) {
+      // dgx / dgh of this step (still in LDS until the barrier), then stage step tt+1, prefetch tt+2
+      const int ir0 = iu, ir1 = U + iu, ir2 = 2 * U + iu;
+      const float gr = dgl[ib][ir0 / RL][ir0 % RL], gz = dgl[ib][ir1 / RL][ir1 % RL];
+      float* ox = P.dgx + (long)ibg * P.d_bs + (long)t * P.d_ts + iocol;
+      float* oh = P.dgh + (long)ibg * P.d_bs + (long)t * P.d_ts + iocol;
+      ox[0] = gr; ox[H] = gz; ox[2 * H] = dxn[iot];
+      oh[0] = gr; oh[H] = gz; oh[2 * H] = dgl[ib][ir2 / RL][ir2 % RL];
+      io_stage(tt + 1);
+      io_load(tt + 2);
+    }
     __syncthreads();
   }
   if (cvalid && P.dh0) {
@@ -351,9 +377,16 @@ __global__ __launch_bounds__((GruBwdCfg<H, G>::NT), (GruBwdCfg<H, G>::WPS)) void
   }
 }
 
+// ring size at H = 256: 8 members (U = 32) by default, 4 (U = 64, twice the GEMV per member, half
+// the members per hand-off) with MRG_GRU_GROUP256=4
+static int g_gru_group256 = [] {
+  const char* e = getenv("MRG_GRU_GROUP256");
+  return (e && atoi(e) == 4) ? 4 : 8;
+}();
+
 static int gru_group(int H) {
   switch (H) {
-    case 256: return 8;
+    case 256: return g_gru_group256;
     case 128: case 64: case 32: return 1;
     default: return 0;
   }
@@ -416,7 +449,7 @@ MRG_API int mrg_gru_supported_hidden(int H) { return gru_group(H) > 0; }
 
 // hand-off ring bytes of one persistent GRU launch (fwd and bwd), zeroed by the caller before each
 MRG_API size_t mrg_gru_xbuf_bytes(int B, int H) {
-  const int G = gru_group(H);
+  const int G = H == 256 ? 8 : gru_group(H);   // the largest ring a launch may take
   return (size_t)2 * B * (G > 0 ? G : 1) * H * 8;
 }
 
@@ -436,7 +469,7 @@ MRG_API int mrg_gru_fwd(int B, int T, int H, const float* gx, long gx_bs, long g
   a.B = B; a.T = T; a.reverse = reverse ? 1 : 0; a.local = 1; a.err = err;
   if (cus <= 0) cus = device_cus();
   switch (H) {
-    case 256: return gru_launch_fwd<256, 8>(a, cus, stream);
+    case 256: return G == 4 ? gru_launch_fwd<256, 4>(a, cus, stream) : gru_launch_fwd<256, 8>(a, cus, stream);
     case 128: return gru_launch_fwd<128, 1>(a, cus, stream);
     case 64: return gru_launch_fwd<64, 1>(a, cus, stream);
     default: return gru_launch_fwd<32, 1>(a, cus, stream);
@@ -459,7 +492,7 @@ MRG_API int mrg_gru_bwd(int B, int T, int H, const float* w_hh, const float* gat
   a.B = B; a.T = T; a.reverse = reverse ? 1 : 0; a.local = 1; a.err = err;
   if (cus <= 0) cus = device_cus();
   switch (H) {
-    case 256: return gru_launch_bwd<256, 8>(a, cus, stream);
+    case 256: return G == 4 ? gru_launch_bwd<256, 4>(a, cus, stream) : gru_launch_bwd<256, 8>(a, cus, stream);
     case 128: return gru_launch_bwd<128, 1>(a, cus, stream);
     case 64: return gru_launch_bwd<64, 1>(a, cus, stream);
     default: return gru_launch_bwd<32, 1>(a, cus, stream);
