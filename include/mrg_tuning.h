@@ -59,8 +59,11 @@ int mrg_probe_tag(int tag);
 int mrg_probe_stop(float* ms, int* tags, int cap);
 
 /* Tuning knob: number of workgroups that share one batch row group at H = 256
- * (8 or 16; default 8).  Process-wide; set before capture, not during. */
+ * (4, 8 or 16; default 8; 4 measured 2 ms slower on the headline step, r04).  Process-wide; set before capture, not during. */
 int mrg_lstm_config(int group256);
+/* Tuning knob: members of a persistent GRU ring at H = 256 (4, default, or 8); returns the previous
+ * setting.  Process-wide; set before capture, not during. */
+int mrg_gru_config(int group256);
 /* Solo (one-workgroup, LDS-exchange) recurrence groups at H <= 128: 1 on (default), 0 off; returns the
  * previous setting. */
 int mrg_lstm_set_solo(int on);

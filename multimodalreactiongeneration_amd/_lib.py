@@ -74,6 +74,7 @@ SIGNATURES = {
                              PP, PP, PP, PI, PP, PL, P, c_int, c_int, P]),
     "mrg_lstm_config": (c_int, [c_int]),
     "mrg_lstm_set_solo": (c_int, [c_int]),
+    "mrg_gru_config": (c_int, [c_int]),
     "mrg_lstm_set_mx": (c_int, [c_int, c_int]),
     "mrg_lstm_cell_fwd": (c_int, [c_int, c_int, P, c_long, P, P, P, P, P, c_long, P, P]),
     "mrg_lstm_cell_bwd": (c_int, [c_int, c_int, P, P, P, P, c_long, P, P, P, P, P]),

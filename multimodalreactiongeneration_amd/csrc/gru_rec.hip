@@ -377,11 +377,12 @@ __global__ __launch_bounds__((GruBwdCfg<H, G>::NT), (GruBwdCfg<H, G>::WPS)) void
   }
 }
 
-// ring size at H = 256: 8 members (U = 32) by default, 4 (U = 64, twice the GEMV per member, half
-// the members per hand-off) with MRG_GRU_GROUP256=4
+// ring size at H = 256: 4 members (U = 64, 768 / 512 threads) by default, measured 0.7-1.0 ms faster
+// on the GRU config than 8 (U = 32; profiles/r04_gru_persistent.txt); MRG_GRU_GROUP256=8 or
+// mrg_gru_config(8) selects 8
 static int g_gru_group256 = [] {
   const char* e = getenv("MRG_GRU_GROUP256");
-  return (e && atoi(e) == 4) ? 4 : 8;
+  return (e && atoi(e) == 8) ? 8 : 4;
 }();
 
 static int gru_group(int H) {
@@ -446,6 +447,13 @@ static int gru_launch_bwd(const GruBwdArgs& a, int cus, hipStream_t s) {
 using namespace mrg;
 
 MRG_API int mrg_gru_supported_hidden(int H) { return gru_group(H) > 0; }
+
+MRG_API int mrg_gru_config(int group256) {
+  MRG_REQUIRE(group256 == 4 || group256 == 8, "mrg_gru_config: group must be 4 or 8");
+  const int prev = g_gru_group256;
+  g_gru_group256 = group256;
+  return prev;
+}
 
 // hand-off ring bytes of one persistent GRU launch (fwd and bwd), zeroed by the caller before each
 MRG_API size_t mrg_gru_xbuf_bytes(int B, int H) {

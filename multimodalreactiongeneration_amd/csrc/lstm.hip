@@ -46,12 +46,15 @@ namespace mrg {
 // Threads per workgroup and resident workgroups per CU for a (hidden size, group size):
 //   H = 256, G = 8  : 512 threads (64 W_hh values per lane), 2 workgroups per CU
 //   H = 256, G = 16 : 256 threads (64 W_hh values per lane), 4 workgroups per CU
+//   H = 256, G = 4  : 1024 threads (64 W_hh values per lane), 1 workgroup per CU
 //   H <= 128        : 256 threads, 2 workgroups per CU
 // waves_per_simd bounds VGPRs at 512 / waves (128 here) so the whole grid stays resident.
 //   H = 128, G = 1  : 1024 threads (64 W_hh values per lane), 1 workgroup per CU (a "solo" group)
 template <int H, int G>
 struct LstmNT {
-  static constexpr int value = (G == 1 && H == 128) ? 1024 : (H >= 256 && H / G >= 32) ? 512 : 256;
+  static constexpr int value = ((G == 1 && H == 128) || (G == 4 && H == 256)) ? 1024
+                               : (H >= 256 && H / G >= 32)                    ? 512
+                                                                              : 256;
   static constexpr int waves_per_simd = (H >= 256 || value == 1024) ? 4 : 2;
 };
 
@@ -703,7 +706,11 @@ static int launch_bwd(const LstmBwdArgs& a, int force_bs, int cus, hipStream_t s
   return 4;
 }
 
-static int g_group256 = 8;  // members per group at H = 256 (8 or 16), mrg_lstm_config
+static int g_group256 = [] {  // members per group at H = 256 (4, 8 or 16), mrg_lstm_config / MRG_LSTM_GROUP256
+  const char* e = getenv("MRG_LSTM_GROUP256");
+  const int g = e ? atoi(e) : 8;
+  return (g == 4 || g == 16) ? g : 8;
+}();
 
 // solo groups (G = 1) at H <= 128: MRG_LSTM_SOLO=0 / mrg_lstm_set_solo(0) restores the multi-member groups
 static int g_solo = [] {
@@ -797,7 +804,7 @@ MRG_API int mrg_lstm_set_solo(int on) {
 
 // Tuning: workgroups per recurrence group at H = 256 (8 or 16).  Affects the bwd xbuf size.
 MRG_API int mrg_lstm_config(int group256) {
-  MRG_REQUIRE(group256 == 8 || group256 == 16, "mrg_lstm_config: group must be 8 or 16");
+  MRG_REQUIRE(group256 == 4 || group256 == 8 || group256 == 16, "mrg_lstm_config: group must be 4, 8 or 16");
   g_group256 = group256;
   return 0;
 }
@@ -837,7 +844,9 @@ MRG_API int mrg_lstm_fwd(int nprob, int B, int T, int H,
   }
   if (cus <= 0) cus = device_cus();
   switch (H) {
-    case 256: return G == 8 ? launch_fwd<256, 8>(a, force_bs, cus, stream) : launch_fwd<256, 16>(a, force_bs, cus, stream);
+    case 256: return G == 8   ? launch_fwd<256, 8>(a, force_bs, cus, stream)
+                     : G == 4 ? launch_fwd<256, 4>(a, force_bs, cus, stream)
+                              : launch_fwd<256, 16>(a, force_bs, cus, stream);
     case 128: return G == 1 ? launch_fwd<128, 1>(a, force_bs, cus, stream) : launch_fwd<128, 8>(a, force_bs, cus, stream);
     case 64: return G == 1 ? launch_fwd<64, 1>(a, force_bs, cus, stream) : launch_fwd<64, 4>(a, force_bs, cus, stream);
     case 32: return G == 1 ? launch_fwd<32, 1>(a, force_bs, cus, stream) : launch_fwd<32, 2>(a, force_bs, cus, stream);
@@ -878,7 +887,9 @@ MRG_API int mrg_lstm_bwd(int nprob, int B, int T, int H,
   }
   if (cus <= 0) cus = device_cus();
   switch (H) {
-    case 256: return G == 8 ? launch_bwd<256, 8>(a, force_bs, cus, stream) : launch_bwd<256, 16>(a, force_bs, cus, stream);
+    case 256: return G == 8   ? launch_bwd<256, 8>(a, force_bs, cus, stream)
+                     : G == 4 ? launch_bwd<256, 4>(a, force_bs, cus, stream)
+                              : launch_bwd<256, 16>(a, force_bs, cus, stream);
     case 128: return G == 1 ? launch_bwd<128, 1>(a, force_bs, cus, stream) : launch_bwd<128, 8>(a, force_bs, cus, stream);
     case 64: return G == 1 ? launch_bwd<64, 1>(a, force_bs, cus, stream) : launch_bwd<64, 4>(a, force_bs, cus, stream);
     case 32: return G == 1 ? launch_bwd<32, 1>(a, force_bs, cus, stream) : launch_bwd<32, 2>(a, force_bs, cus, stream);

@@ -991,11 +991,16 @@ def test_gru_vs_torch_fp64(In, H, B, T, bidir, state):
         assert rel_err(gp[k].grad, p.grad) < TOL, k
 
 
-@pytest.mark.parametrize("H,B,T,reverse", [(256, 64, 300, False), (128, 64, 300, True)])
-def test_gru_persistent_matches_per_step(H, B, T, reverse):
+@pytest.mark.parametrize("H,B,T,reverse,group", [(256, 64, 300, False, 4), (256, 64, 300, True, 8),
+                                                 (128, 64, 300, True, 1)])
+def test_gru_persistent_matches_per_step(H, B, T, reverse, group):
     """The persistent GRU recurrence (one launch per layer direction) vs the per-step products + cell
-    kernels at the GRU config's width (B = 64, T = 300): outputs, final state and every gradient."""
+    kernels at the GRU config's width (B = 64, T = 300): outputs, final state and every gradient, for
+    both ring sizes at H = 256 (mrg_gru_config)."""
     from multimodalreactiongeneration_amd import functional as Fn
+    from multimodalreactiongeneration_amd import _lib as L
+    lib = L.load()
+    prev_group = lib.mrg_gru_config(group) if H == 256 else None
     g = torch.Generator().manual_seed(H + T)
     s = 1.0 / math.sqrt(H)
     w = [torch.randn(3 * H, H, generator=g) * s for _ in range(2)]
@@ -1018,6 +1023,8 @@ def test_gru_persistent_matches_per_step(H, B, T, reverse):
             outs.append([y.detach(), hT.detach(), xx.grad, hh.grad] + [p.grad for p in ps])
     finally:
         Fn._GRU_PERSIST[0] = prev
+        if prev_group is not None:
+            lib.mrg_gru_config(prev_group)
     for a, b in zip(*outs):
         assert rel_err(a, b) < TOL
 
