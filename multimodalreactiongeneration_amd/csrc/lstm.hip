@@ -719,6 +719,13 @@ static int g_solo = [] {
 }();
 
 // members per group without solo groups (the hand-off ring is sized for these)
+// forward-only ring size at H = 256 (MRG_LSTM_GROUP256_FWD = 4 / 8 / 16; unset: the shared setting)
+static int g_fwd_group256 = [] {
+  const char* e = getenv("MRG_LSTM_GROUP256_FWD");
+  const int g = e ? atoi(e) : 0;
+  return (g == 4 || g == 8 || g == 16) ? g : 0;
+}();
+
 static int ring_group_size(int H) {
   switch (H) {
     case 256: return g_group256;
@@ -822,6 +829,7 @@ MRG_API int mrg_lstm_fwd(int nprob, int B, int T, int H,
   MRG_REQUIRE(nprob >= 1 && nprob <= MAXP, "mrg_lstm_fwd: nprob %d out of range", nprob);
   int G = group_size(H);
   MRG_REQUIRE(G > 0, "mrg_lstm_fwd: unsupported hidden size %d", H);
+  if (H == 256 && g_fwd_group256) G = g_fwd_group256;
   if (B == 0 || T == 0) return 0;
   LstmFwdArgs a;
   memset(&a, 0, sizeof(a));
