@@ -53,11 +53,49 @@ __device__ __forceinline__ f32x4mx mx_mfma6(const bf16x8 (&a)[3], const bf16x8 (
 // global W_hh row of a member's local gate row r (gate-major: r = q * U + u)
 __device__ __forceinline__ int mx_grow(int j, int r) { return (r / MX_U) * MX_H + j * MX_U + (r % MX_U); }
 
+// ds_read_b128 outside the compiler's view: its waitcnt pass would put a vmcnt(0) (the LDS-DMA alias rule)
+// before every LDS read that follows an LDS-DMA issue, stalling the product on the prefetch; the
+// caller waits with lgkmcnt itself
+__device__ __forceinline__ bf16x8 mx_lds_b128(const void* p) {
+  typedef unsigned u32x4r __attribute__((ext_vector_type(4)));
+  const unsigned a = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+  u32x4r v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a) : "memory");
+  return __builtin_bit_cast(bf16x8, v);
+}
+__device__ __forceinline__ float mx_lds_f32(const void* p) {
+  const unsigned a = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+  float v;
+  asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+// the wait for those reads, tied to their results (a bare asm wait would let the compiler schedule
+// the consumers above it)
+__device__ __forceinline__ void mx_lds_wait3(bf16x8 (&f)[3]) {
+  typedef unsigned u32x4r __attribute__((ext_vector_type(4)));
+  u32x4r a = __builtin_bit_cast(u32x4r, f[0]), b = __builtin_bit_cast(u32x4r, f[1]),
+         c = __builtin_bit_cast(u32x4r, f[2]);
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b), "+v"(c)::"memory");
+  f[0] = __builtin_bit_cast(bf16x8, a); f[1] = __builtin_bit_cast(bf16x8, b); f[2] = __builtin_bit_cast(bf16x8, c);
+}
+__device__ __forceinline__ void mx_lds_wait8(float (&x)[4], float (&y)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(y[0]), "+v"(y[1]), "+v"(y[2]), "+v"(y[3])::"memory");
+}
+// a step barrier with no fence: LDS writes complete (lgkmcnt), LDS-DMA in flight left in flight (a
+// __syncthreads would wait vmcnt(0) for it)
+__device__ __forceinline__ void mx_step_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 __global__ __launch_bounds__(MX_NT, 1) void lstm_fwd_mx_kernel(LstmFwdArgs args) {
   constexpr int H = MX_H, G = MX_G, BS = MX_BS, U = MX_U;
   constexpr int WP = MX_HPB / 2;  // 32-bit words per plane row
   __shared__ __attribute__((aligned(16))) unsigned hp[3][BS][WP];
   __shared__ __attribute__((aligned(16))) float pre[BS][MX_RP];
+  __shared__ __attribute__((aligned(16))) float gxs[3][4][BS * U];   // Gx of step mod 3, by LDS-DMA
   __shared__ int xcc_flag;
   int prob, grp, j;
   const int ngroups = (args.B + BS - 1) / BS;
@@ -84,7 +122,7 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_fwd_mx_kernel(LstmFwdArgs args)
   const int bg = b0 + cb;
   const bool cvalid = bg < B;
   const int hcol = j * U + cu;
-  float c = 0.0f, h = 0.0f, bh[4] = {0.f, 0.f, 0.f, 0.f}, gxv[4] = {0.f, 0.f, 0.f, 0.f};
+  float c = 0.0f, h = 0.0f, bh[4] = {0.f, 0.f, 0.f, 0.f};
   if (cvalid) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) bh[q] = P.b_hh[q * H + hcol];
@@ -102,14 +140,21 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_fwd_mx_kernel(LstmFwdArgs args)
     put_planes(b, k, ok ? P.h0[(long)(b0 + b) * P.h0_bs + k] : 0.0f,
                ok ? P.h0[(long)(b0 + b) * P.h0_bs + k + 1] : 0.0f);
   }
-  auto load_gx = [&](int t) {
-    if (cvalid) {
-      const float* g = P.gx + (long)bg * P.gx_bs + (long)t * P.gx_ts + hcol;
+  // Gx of processing step tt2 -> LDS slot tt2 % 3 by LDS-DMA (wave w moves its own 64 cells), issued
+  // after the step's gather so the next gather's wait (vmcnt, in order on gfx9) finds it landed and
+  // no Gx load sits in front of a hand-off poll; rows past B read row B - 1 (never used)
+  auto gx_issue = [&](int tt2) {
+    if (tt2 >= T) return;
+    const int t2 = P.reverse ? T - 1 - tt2 : tt2;
+    const float* g = P.gx + (long)min(bg, B - 1) * P.gx_bs + (long)t2 * P.gx_ts + hcol;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) gxv[q] = g[q * H];
-    }
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_global_load_lds((const void*)(g + q * H),
+                                       (__attribute__((address_space(3))) void*)&gxs[tt2 % 3][q][64 * wave], 4, 0, 0);
   };
-  load_gx(P.reverse ? T - 1 : 0);
+  gx_issue(0);
+  gx_issue(1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   // ring: [parity][B][H / 2] pair granules (units 2p, 2p + 1 of a row)
   unsigned long long* xb = P.xbuf;
@@ -127,22 +172,31 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_fwd_mx_kernel(LstmFwdArgs args)
     for (int s = 0; s < 8; ++s) {
       bf16x8 fa[3];
 #pragma unroll
-      for (int p = 0; p < 3; ++p) fa[p] = *reinterpret_cast<const bf16x8*>(&hp[p][ar][(32 * s + ak) >> 1]);
+      for (int p = 0; p < 3; ++p) fa[p] = mx_lds_b128(&hp[p][ar][(32 * s + ak) >> 1]);
+      mx_lds_wait3(fa);
       acc = mx_mfma6(fa, wf[s], acc);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) pre[4 * (lane >> 4) + i][16 * wave + ar] = acc[i];
     MRG_STAMP(1);
-    __syncthreads();
+    mx_step_barrier();
     MRG_STAMP(2);
     // 2. gates + cell, 3. publish, store, prefetch
     const int par = tt & 1;
     float ig = 0.0f, fg = 0.0f, gg = 0.0f, og = 0.0f;
     if (cvalid) {
-      const float zi = pre[cb][0 * U + cu] + gxv[0] + bh[0];
-      const float zf = pre[cb][1 * U + cu] + gxv[1] + bh[1];
-      const float zg = pre[cb][2 * U + cu] + gxv[2] + bh[2];
-      const float zo = pre[cb][3 * U + cu] + gxv[3] + bh[3];
+      const int sl = tt % 3;
+      float pv[4], gv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        pv[q] = mx_lds_f32(&pre[cb][q * U + cu]);
+        gv[q] = mx_lds_f32(&gxs[sl][q][tid]);
+      }
+      mx_lds_wait8(pv, gv);
+      const float zi = pv[0] + gv[0] + bh[0];
+      const float zf = pv[1] + gv[1] + bh[1];
+      const float zg = pv[2] + gv[2] + bh[2];
+      const float zo = pv[3] + gv[3] + bh[3];
       ig = sigmoidf_(zi); fg = sigmoidf_(zf); gg = tanhf_(zg); og = sigmoidf_(zo);
       c = fg * c + ig * gg;
       h = og * tanhf_(c);
@@ -157,7 +211,6 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_fwd_mx_kernel(LstmFwdArgs args)
       float* gs = P.gates + (long)bg * P.g_bs + (long)t * P.g_ts + hcol;
       gs[0] = ig; gs[H] = fg; gs[2 * H] = gg; gs[3 * H] = og;
       P.cs[(long)bg * P.cs_bs + (long)t * P.cs_ts + hcol] = c;
-      if (tt + 1 < T) load_gx(P.reverse ? t - 1 : t + 1);
     }
     MRG_STAMP(3);
     // 4. gather h_t of the group (BS x H / 2 pair granules, 4 per thread)
@@ -176,8 +229,9 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_fwd_mx_kernel(LstmFwdArgs args)
         put_planes(b, k, ok ? g0[m] : 0.0f, ok ? g1[m] : 0.0f);
       }
     }
+    gx_issue(tt + 2);   // into the slot step tt - 1 used (this wave's own reads of it are done)
     MRG_STAMP(4);
-    __syncthreads();
+    mx_step_barrier();
     MRG_STAMP(5);
   }
   if (cvalid) {
@@ -190,7 +244,7 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_bwd_mx_kernel(LstmBwdArgs args)
   constexpr int H = MX_H, G = MX_G, BS = MX_BS, U = MX_U;
   constexpr int RPB = MX_RPB;
   __shared__ __attribute__((aligned(16))) __bf16 dgp[3][BS][RPB];   // dG as three bf16 planes
-  __shared__ float sv[2][7][BS * U];  // saved i, f, g, o, c_t, c_{t-1}, dy of the cells, by step parity
+  __shared__ __attribute__((aligned(16))) float sv[3][7][BS * U];  // saved i, f, g, o, c_t, c_{t-1}, dy: step mod 3
   __shared__ int xcc_flag;
   int prob, grp, j;
   const int ngroups = (args.B + BS - 1) / BS;
@@ -223,33 +277,40 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_bwd_mx_kernel(LstmBwdArgs args)
     if (P.dcT) dcn = P.dcT[(long)bg * H + hcol];
     if (P.dhT) dhrec = P.dhT[(long)bg * H + hcol];
   }
-  // saved activations of processing step tt2 -> pf (the cell thread moves its own: no spare waves)
-  float pf[7];
-  auto io_load = [&](int tt2) {
-    if (!cvalid || tt2 >= T) return;
+  float c0v = 0.0f;   // c_{t-1} at the sequence edge
+  if (cvalid && P.c0) c0v = P.c0[(long)bg * P.c0_bs + hcol];
+  // saved activations of processing step tt2 -> LDS slot tt2 % 3 by LDS-DMA (global_load_lds_dword: no
+  // VGPRs held in flight); wave w moves its own 64 cells, issued right after the step's hand-off poll so
+  // that the next poll (whose wait covers every older load: gfx9 counts in order) finds them landed —
+  // with the loads issued at the end of the step, each poll waited for them.  Rows past B read row
+  // B - 1 (never used); c_{t-1} at the sequence edge and a null dy are supplied by the cells.
+  auto io_issue = [&](int tt2) {
+    if (tt2 >= T) return;
     const int t = P.reverse ? tt2 : T - 1 - tt2;
     const int tp = P.reverse ? t + 1 : t - 1;
-    const float* gs = P.gates + (long)bg * P.g_bs + (long)t * P.g_ts + hcol;
-    pf[0] = gs[0]; pf[1] = gs[H]; pf[2] = gs[2 * H]; pf[3] = gs[3 * H];
-    pf[4] = P.cs[(long)bg * P.cs_bs + (long)t * P.cs_ts + hcol];
-    pf[5] = (tp >= 0 && tp < T) ? P.cs[(long)bg * P.cs_bs + (long)tp * P.cs_ts + hcol]
-                                : (P.c0 ? P.c0[(long)bg * P.c0_bs + hcol] : 0.0f);
-    pf[6] = P.dy ? P.dy[(long)bg * P.dy_bs + (long)t * P.dy_ts + hcol] : 0.0f;
-  };
-  auto io_stage = [&](int tt2) {
-    if (!cvalid || tt2 >= T) return;
+    const int tq = (tp >= 0 && tp < T) ? tp : t;
+    const int eb = min(bg, B - 1);
+    const float* gs = P.gates + (long)eb * P.g_bs + (long)t * P.g_ts + hcol;
+    const float* src[7] = {gs, gs + H, gs + 2 * H, gs + 3 * H,
+                           P.cs + (long)eb * P.cs_bs + (long)t * P.cs_ts + hcol,
+                           P.cs + (long)eb * P.cs_bs + (long)tq * P.cs_ts + hcol,
+                           P.dy ? P.dy + (long)eb * P.dy_bs + (long)t * P.dy_ts + hcol : gs};
 #pragma unroll
-    for (int q = 0; q < 7; ++q) sv[tt2 & 1][q][tid] = pf[q];
+    for (int q = 0; q < 7; ++q)
+      __builtin_amdgcn_global_load_lds((const void*)src[q],
+                                       (__attribute__((address_space(3))) void*)&sv[tt2 % 3][q][64 * wave], 4, 0, 0);
   };
-  io_load(0);
-  io_stage(0);
-  io_load(1);
+  io_issue(0);
+  io_issue(1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   unsigned long long* xb = P.xbuf;
   const long xstride_b = (long)G * H / 2;  // per batch row: [dest G][src G][U / 2] pair granules
   const int local = args.local ? group_on_one_xcd<G>(xb + ((long)B + b0) * xstride_b, j, args.err, dead, &xcc_flag)
                                : 0;
   const int ar = lane & 15, ak = 8 * (lane >> 4);
+  // the step's barriers: mx_step_barrier (the DMA data is covered by the next hand-off poll's wait)
+  auto step_barrier = mx_step_barrier;
 
   for (int tt = 0; tt < T; ++tt) {
     const int t = P.reverse ? tt : T - 1 - tt;
@@ -266,9 +327,11 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_bwd_mx_kernel(LstmBwdArgs args)
         dhrec = s;
       }
       MRG_STAMP(1);
-      const int sl = tt & 1;
+      const int sl = tt % 3;
       const float ig = sv[sl][0][tid], fg = sv[sl][1][tid], gg = sv[sl][2][tid], og = sv[sl][3][tid];
-      const float cc = sv[sl][4][tid], cp = sv[sl][5][tid], dyv = sv[sl][6][tid];
+      const float cc = sv[sl][4][tid];
+      const float cp = tt + 1 < T ? sv[sl][5][tid] : c0v;
+      const float dyv = P.dy ? sv[sl][6][tid] : 0.0f;
       const float dh = dhrec + dyv;
       const float tc = tanhf_(cc);
       const float dc = dh * og * (1.0f - tc * tc) + dcn;
@@ -280,6 +343,12 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_bwd_mx_kernel(LstmBwdArgs args)
     } else {
 #pragma unroll
       for (int q = 0; q < 4; ++q) dgv[q] = 0.0f;
+    }
+    io_issue(tt + 2);   // into the slot step tt - 1 used (this wave's own reads of it are done)
+    if (cvalid) {   // dG of this step (fp32) before the product: the stores retire under it
+      float* dgo = P.dG + (long)bg * P.dG_bs + (long)t * P.dG_ts + hcol;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dgo[q * H] = dgv[q];
     }
 #pragma unroll
     for (int q = 0; q < 4; q += 2) {  // planes of (dG_q, dG_{q+1}): one split of the pair
@@ -293,7 +362,7 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_bwd_mx_kernel(LstmBwdArgs args)
       }
     }
     MRG_STAMP(2);
-    __syncthreads();
+    step_barrier();
     MRG_STAMP(3);
     // partial dh_{t-1}[b][n] = sum over this member's rows of dG[b][row] W[row][n], n in this wave's
     // two column tiles; lane holds rows 4 (lane >> 4) + i, column 16 ct' + (lane & 15)
@@ -304,7 +373,8 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_bwd_mx_kernel(LstmBwdArgs args)
       for (int s = 0; s < 4; ++s) {
         bf16x8 fa[3];
 #pragma unroll
-        for (int p = 0; p < 3; ++p) fa[p] = *reinterpret_cast<const bf16x8*>(&dgp[p][ar][32 * s + ak]);
+        for (int p = 0; p < 3; ++p) fa[p] = mx_lds_b128(&dgp[p][ar][32 * s + ak]);
+        mx_lds_wait3(fa);
         acc[0] = mx_mfma6(fa, wf[0][s], acc[0]);
         acc[1] = mx_mfma6(fa, wf[1][s], acc[1]);
       }
@@ -323,15 +393,8 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_bwd_mx_kernel(LstmBwdArgs args)
         }
       }
     }
-    if (cvalid) {  // dG of this step (fp32, from registers), stage step tt+1, prefetch tt+2
-      float* dgo = P.dG + (long)bg * P.dG_bs + (long)t * P.dG_ts + hcol;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) dgo[q * H] = dgv[q];
-      io_stage(tt + 1);
-      io_load(tt + 2);
-    }
     MRG_STAMP(5);
-    __syncthreads();
+    step_barrier();
     MRG_STAMP(6);
   }
   if (cvalid) {
