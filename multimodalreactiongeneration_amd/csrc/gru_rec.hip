@@ -276,6 +276,10 @@ __global__ __launch_bounds__((GruBwdCfg<H, G>::NT), (GruBwdCfg<H, G>::WPS)) void
   for (int tt = 0; tt < T; ++tt) {
     const int t = P.reverse ? tt : T - 1 - tt;
     const int r0 = cu, r1 = U + cu, r2 = 2 * U + cu;
+    if constexpr (!SELF_IO) {   // io waves stage / prefetch while the cells work (as lstm.hip's backward)
+      io_stage(tt + 1);
+      io_load(tt + 2);
+    }
     if (cvalid) {
       if (tt > 0) {
         float s;
@@ -355,8 +359,10 @@ __global__ __launch_bounds__((GruBwdCfg<H, G>::NT), (GruBwdCfg<H, G>::WPS)) void
       float* oh = P.dgh + (long)ibg * P.d_bs + (long)t * P.d_ts + iocol;
       ox[0] = gr; ox[H] = gz; ox[2 * H] = dxn[iot];
       oh[0] = gr; oh[H] = gz; oh[2 * H] = dgl[ib][ir2 / RL][ir2 % RL];
-      io_stage(tt + 1);
-      io_load(tt + 2);
+      if constexpr (SELF_IO) {
+        io_stage(tt + 1);
+        io_load(tt + 2);
+      }
     }
     __syncthreads();
   }
