@@ -345,11 +345,6 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_bwd_mx_kernel(LstmBwdArgs args)
       for (int q = 0; q < 4; ++q) dgv[q] = 0.0f;
     }
     io_issue(tt + 2);   // into the slot step tt - 1 used (this wave's own reads of it are done)
-    if (cvalid) {   // dG of this step (fp32) before the product: the stores retire under it
-      float* dgo = P.dG + (long)bg * P.dG_bs + (long)t * P.dG_ts + hcol;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) dgo[q * H] = dgv[q];
-    }
 #pragma unroll
     for (int q = 0; q < 4; q += 2) {  // planes of (dG_q, dG_{q+1}): one split of the pair
       unsigned p0, p1, p2;
@@ -392,6 +387,11 @@ __global__ __launch_bounds__(MX_NT, 1) void lstm_bwd_mx_kernel(LstmBwdArgs args)
                      (unsigned)(tt + 1) & 3u, acc[ct][i], vn, local);
         }
       }
+    }
+    if (cvalid) {   // dG of this step (fp32, from registers)
+      float* dgo = P.dG + (long)bg * P.dG_bs + (long)t * P.dG_ts + hcol;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dgo[q * H] = dgv[q];
     }
     MRG_STAMP(5);
     step_barrier();
