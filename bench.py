@@ -128,7 +128,17 @@ def parse(argv=None):
     ap.add_argument("--comm", default="torch", choices=["torch", "native"],
                     help="N>1 gradient all-reduce: torch.distributed (RCCL) or libmrg's mrg_comm_* RCCL communicator")
     ap.add_argument("--lstm-group", type=int, default=0, help="workgroups per LSTM row group at H=256 (8|16; 0 = library default)")
-    return ap.parse_args(argv)
+    ap.add_argument("--shared-device-gloo", type=int, default=0,
+                    help="TEST ONLY: run the N>1 branch with every rank on GPU 0 and gloo carrying the exchange "
+                         "(RCCL refuses two ranks on one device), so the multi-GPU timed path runs with real kernels "
+                         "on a 1-GPU box; the ranks' fwd+bwd replays take turns on the device (host lock)")
+    ap.add_argument("--ddp-check", type=int, default=0,
+                    help="N>1: before timing, check that one step's rank-averaged gradient equals a single-rank step "
+                         "on the concatenation of every rank's shard (reported as ddp_check)")
+    args = ap.parse_args(argv)
+    if args.shared_device_gloo and args.comm != "torch":
+        ap.error("--shared-device-gloo runs the exchange on torch.distributed gloo; --comm native needs RCCL")
+    return args
 
 
 def _free_port():
@@ -163,7 +173,7 @@ def launch_or_check(args, argv=None):
         return None
     if not args.dry_run:
         visible = torch.cuda.device_count()
-        if visible < args.gpus:
+        if visible < (1 if args.shared_device_gloo else args.gpus):
             print(f"bench.py: --gpus {args.gpus} asks for {args.gpus} ranks (one per GPU) but only {visible} "
                   "GPU(s) are visible; refusing to time fewer GPUs than asked", file=sys.stderr, flush=True)
             sys.exit(2)
@@ -180,9 +190,10 @@ def launch_or_check(args, argv=None):
     sys.exit(rc)
 
 
-def ranks_seen(rank, world, dev):
+def ranks_seen(rank, world, dev, shared=False):
     """Every rank's (rank, local rank, device) as RCCL / gloo initialised them, gathered to all ranks;
-    raises when two ranks share one GPU (the timing would then not be of N GPUs)."""
+    raises when two ranks share one GPU (the timing would then not be of N GPUs), unless ``shared``
+    (--shared-device-gloo, a test of the N>1 code path, never a measurement)."""
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if dev is not None and dev.type == "cuda":
         p = torch.cuda.get_device_properties(dev)
@@ -195,10 +206,95 @@ def ranks_seen(rank, world, dev):
     allr = [None] * world
     dist.all_gather_object(allr, mine)
     devs = {(r["host"], r["device"]) for r in allr}
-    if dev is not None and dev.type == "cuda" and len(devs) != world:
+    if dev is not None and dev.type == "cuda" and len(devs) != world and not shared:
         raise RuntimeError(f"bench.py: {world} ranks but only {len(devs)} distinct GPUs: {allr}")
     return {"world_size": dist.get_world_size(), "backend": dist.get_backend(), "distinct_devices": len(devs),
-            "ranks": allr}
+            "shared_device_test": bool(shared), "ranks": allr}
+
+
+class _DeviceTurns:
+    """--shared-device-gloo: the ranks' fwd+bwd work takes turns on the one GPU (an flock on a file
+    keyed by the rendezvous port).  Two processes' persistent recurrences are not guaranteed
+    co-resident on one device (each ring needs its members resident together), so the test mode
+    serialises them; collectives stay outside the lock (a rank holding it across an all-reduce
+    would wait for a rank that waits for the lock)."""
+
+    def __init__(self, on):
+        self.on = on
+        self.f = None
+        if on:
+            import tempfile
+            path = os.path.join(tempfile.gettempdir(), f"mrg_bench_dev0_{os.environ.get('MASTER_PORT', '0')}.lock")
+            self.f = open(path, "a+")
+
+    def __enter__(self):
+        if self.on:
+            import fcntl
+            fcntl.flock(self.f, fcntl.LOCK_EX)
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            import fcntl
+            torch.cuda.synchronize()
+            fcntl.flock(self.f, fcntl.LOCK_UN)
+        return False
+
+
+def _kink_layer(name):
+    """ReLU FeedForward input layers: a pre-activation within ~1e-7 of 0 may take the other side of the
+    kink under another fp32 summation order (tests/test_gpu_models.py RELU_KINK_TOL)."""
+    return ".feedforward.feed_forward.module.input." in name or ".output_feedforward.feed_forward.input." in name
+
+
+def ddp_grad_check(model, opt, reducer, batch, args, rank, world, dev, turns):
+    """One step's rank-averaged gradient (every rank on its own shard, then the exchange bench.py times)
+    vs a single-rank step on the concatenation of all ranks' shards (what Lightning DDP's mean
+    reproduces, config.yaml:127): the worst per-parameter max|a - b| / max|b| on rank 0."""
+    from multimodalreactiongeneration_amd.synthetic import make_batch, clone_batch
+    with turns:
+        opt.zero_grad()
+        model.training_step(clone_batch(batch, dev))["loss"].backward()
+    reducer.allreduce()
+    torch.cuda.synchronize()
+    g_avg = opt.flat_grad.clone()
+    res = None
+    if rank == 0:
+        shards = [make_batch(B=args.batch, T=args.seq, ratio=args.ratio, seed=1234 + r, device=dev)
+                  for r in range(world)]
+        full = [(torch.cat([s[i][0] for s in shards]), torch.cat([s[i][1] for s in shards])) for i in range(7)]
+        with turns:
+            opt.zero_grad()
+            model.training_step(full)["loss"].backward()
+        torch.cuda.synchronize()
+        base = opt.flat_grad.data_ptr()
+        worst, worst_kink = (0.0, None), (0.0, None)
+        names = {id(p): k for k, p in model.named_parameters()}
+        for p in opt.plist:
+            off = (p.grad.data_ptr() - base) // 4
+            a, b = g_avg[off:off + p.numel()], opt.flat_grad[off:off + p.numel()]
+            e = ((a - b).abs().max() / b.abs().max().clamp_min(1e-12)).item()
+            k = names.get(id(p), "?")
+            slot = worst_kink if _kink_layer(k) else worst
+            if e > slot[0]:
+                if _kink_layer(k):
+                    worst_kink = (e, k)
+                else:
+                    worst = (e, k)
+        res = {"grad_vs_concat_batch_worst_rel": worst[0], "worst_param": worst[1],
+               "relu_kink_layers_worst_rel": worst_kink[0], "relu_kink_worst_param": worst_kink[1],
+               "concat_batch": args.batch * world}
+    opt.zero_grad()
+    dist.barrier()
+    return res
+
+
+def params_agree(opt):
+    """Bitwise equality of every rank's flat parameter buffer (elementwise MAX == MIN over ranks)."""
+    hi, lo = opt.flat.clone(), opt.flat.clone()
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    return bool(torch.equal(hi, lo))
 
 
 def timed_region(run, steps, world, dev):
@@ -640,11 +736,13 @@ def main():
     from multimodalreactiongeneration_amd.model import Metaformer
     from multimodalreactiongeneration_amd.synthetic import make_batch
 
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    shared = bool(args.shared_device_gloo)
+    local = 0 if shared else int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)    # before the process group, so RCCL binds rank -> its own GPU
-    rank, world = init_from_env()
+    rank, world = init_from_env(backend="gloo" if shared else None)
     dev = torch.device("cuda", local)
-    seen = ranks_seen(rank, world, dev)
+    seen = ranks_seen(rank, world, dev, shared=shared)
+    turns = _DeviceTurns(shared and world > 1)
     if world != args.gpus:
         raise RuntimeError(f"bench.py: --gpus {args.gpus} but {world} ranks initialised")
     mc, oc, me = C.lstmformer_config(ratio=args.ratio)
@@ -675,16 +773,22 @@ def main():
         opt.step()
         return loss
 
+    check = None
+    if args.ddp_check and world > 1:
+        check = ddp_grad_check(model, opt, reducer, batch, args, rank, world, dev, turns)
+
     run = step
     if args.graph:
         # capture fwd+bwd(+AdamW at N=1) once; the RCCL all-reduce stays eager between replays at N>1
         captured = step if world == 1 else fwd_bwd
-        replay = capture(captured, max(2, args.warmup), preserve=opt.state_tensors())
+        with turns:
+            replay = capture(captured, max(2, args.warmup), preserve=opt.state_tensors())
         if world == 1:
             run = replay
         else:
             def run():
-                replay()
+                with turns:
+                    replay()
                 reducer.allreduce()
                 opt.step()
     else:
@@ -707,7 +811,9 @@ def main():
     # (the replay's stream schedule: weight gradients on the side stream, so a bracketed launch runs
     # beside the same work as in the graph; a weight-gradient bracket includes its split-K reduce)
     # (every rank steps, the all-reduce is collective; rank 0 records)
-    if rank == 0:
+    if shared:
+        kernels, roof = {}, None    # a test of the code path: ranks take turns, no kernel figures
+    elif rank == 0:
         kernels, roof = _probe_steps(step, 2)
         if roof is not None:
             roof["trace_check"] = trace_check(roof)
@@ -715,6 +821,8 @@ def main():
         for _ in range(2):
             step()
         kernels, roof = {}, None
+    agree = params_agree(opt) if world > 1 else None
+    Fn.check_errors()
     step_flop = (model_flops_per_frame(mc, args.ratio) + attn_flops_per_frame(mc, args.ratio, args.seq)) \
         * args.batch * args.seq
     out = {
@@ -738,6 +846,13 @@ def main():
         "cpu_baseline": None,
         "ranks_seen": {k: v for k, v in seen.items() if k != "ranks"} | {"devices": [r["device"] for r in seen["ranks"]]},
     }
+    if world > 1:
+        out["params_bitwise_equal_across_ranks"] = agree
+        if check is not None:
+            out["ddp_check"] = check
+    if shared:
+        out["value"] = None   # ranks shared one GPU and took turns: a test of the N>1 path, not a measurement
+        out["shared_device_test"] = True
     if rank == 0:
         progress(f"headline {ms:.3f} ms/step")
     if rank == 0 and world == 1 and args.secondary:

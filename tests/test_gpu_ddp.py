@@ -72,6 +72,39 @@ def test_two_ranks_overlapped_allreduce_equals_full_batch_gradient():
     assert worst < TOL, worst
 
 
+def test_bench_multi_rank_timed_branch_on_one_gpu():
+    """bench.py's N>1 timed branch (graph-replayed fwd+bwd, then the serial bucketed GradReducer
+    all-reduce, then the fused AdamW, max-over-ranks timing) with the real kernels: 2 ranks on the box's
+    one GPU (--shared-device-gloo: gloo carries the exchange, the ranks' replays take turns), the
+    pre-flight of the driver's 8-GPU SCALE run.  Asserts (a) one JSON line with a world of 2, (b) the
+    ranks' parameters bitwise equal after the timed steps, (c) one step's rank-averaged gradient equal
+    to a single-rank step on the concatenated 2 x B batch (1e-4; the ReLU-kink layers 2e-3, as in
+    test_gpu_models.RELU_KINK_TOL).  Reference: config.yaml:121,127 (Lightning DDP)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(OMP_NUM_THREADS="4", MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--shared-device-gloo", "1",
+                        "--ddp-check", "1", "--batch", "8", "--seq", "120", "--steps", "3", "--warmup", "1",
+                        "--secondary", "0", "--cpu-baseline", "0"],
+                       env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    print(json.dumps({k: out.get(k) for k in ("ms_per_step", "ranks_seen", "ddp_check",
+                                               "params_bitwise_equal_across_ranks")}))
+    assert out["n_gpus"] == 2 and out["ranks_seen"]["world_size"] == 2
+    assert out["ranks_seen"]["backend"] == "gloo" and out["shared_device_test"] is True
+    assert out["params_bitwise_equal_across_ranks"] is True
+    chk = out["ddp_check"]
+    assert chk["concat_batch"] == 16
+    assert chk["grad_vs_concat_batch_worst_rel"] < TOL, chk
+    assert chk["relu_kink_layers_worst_rel"] < 2e-3, chk
+
+
 def test_native_rccl_communicator_one_rank():
     """libmrg's own RCCL communicator (mrg_comm_* C-ABI) on the box's one GPU: a 1-rank group's mean
     and sum of bucketed spans leave the buffer bit-identical, spans outside the list untouched."""

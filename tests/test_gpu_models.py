@@ -626,13 +626,19 @@ def test_benchmark_schedule_b64_vs_oracle():
     replay()
     torch.cuda.synchronize()
     Fn.check_errors()
-    assert abs(loss_buf.item() - float(d["loss"])) / abs(float(d["loss"])) < TOL
+    _check_sampled_fixture(d, m, loss_buf, _b64_tol)
+
+
+def _check_sampled_fixture(d, m, loss, tol_of=lambda k: TOL):
+    """Loss, every parameter gradient (max|g|, L2 norm and the sampled entries incl. the argmax) and
+    the post-AdamW parameters at the sampled entries vs a make_b64_fixture.py float64 fixture."""
+    assert abs(loss.item() - float(d["loss"])) / abs(float(d["loss"])) < TOL, (loss.item(), float(d["loss"]))
     worst = []
     for k, p in m.named_parameters():
         g = p.grad.detach().reshape(-1).double().cpu()
         idx = torch.from_numpy(d[f"idx/{k}"])
         gmax, _, g2 = d[f"stat/{k}"]
-        tol = _b64_tol(k)
+        tol = tol_of(k)
         scale = max(gmax, 1e-30)
         e_pt = (g[idx] - torch.from_numpy(d[f"g/{k}"])).abs().max().item() / scale
         e_max = abs(g.abs().max().item() - gmax) / scale
@@ -646,6 +652,119 @@ def test_benchmark_schedule_b64_vs_oracle():
             assert rel_err(a, torch.from_numpy(d[f"after/{k}"])[sel]) < tol, k
     worst.sort()
     print("worst gradient errors vs float64:", [(f"{e:.2e}", k) for e, k in worst[-5:]])
+
+
+def _param_sum_matches(m, d):
+    assert abs(sum(v.double().sum().item() for v in m.state_dict().values()) - float(d["param_sum"])) < 1e-6, \
+        "torch.manual_seed(0) init differs from the fixture's"
+
+
+def test_c3_scheduled_sampling_b64_vs_oracle():
+    """BASELINE configs[2] exactly as bench.py's step_c3 times it: LSTMwithSample scheduled sampling,
+    B=64, T=300, lead 12, torch.manual_seed(0) weights, epoch 30, the device mask holding the first
+    RandomState(7) < 0.5 draw, fwd + loss + bwd + AdamW captured as ONE HIP graph (the fused per-frame
+    decode, 16-row x 4-unit tiles over 256 workgroups) and replayed, vs the oracle's float64 answer
+    (tests/golden/lstm_with_sample_ss_b64_f64.npz): loss, every gradient (max, L2, 257 samples),
+    the post-AdamW parameters, and the eager prediction.  Reference: lstm_with_sample.py:278-301,379-433."""
+    from multimodalreactiongeneration_amd import configs as C
+    from multimodalreactiongeneration_amd import functional as Fn
+    from multimodalreactiongeneration_amd.graphs import capture
+    from multimodalreactiongeneration_amd.model import LSTMwithSample
+    from multimodalreactiongeneration_amd.synthetic import make_batch, clone_batch
+    d = load("lstm_with_sample_ss_b64_f64")
+    mc, oc, me = C.lstm_with_sampling_config(use_scheduled_sampling=True)
+    torch.manual_seed(0)
+    m = LSTMwithSample(mc, oc, me)
+    _param_sum_matches(m, d)
+    m.current_epoch = 30
+    m = m.to(DEV)
+    T = 300
+    batch = make_batch(B=64, T=T, lead=12, seed=1234, device=DEV)
+    mask = torch.from_numpy(d["sampling_mask"]).to(DEV)
+    with torch.no_grad():
+        y, _ = m.prediction(clone_batch(batch, DEV), use_scheduled_sampling=True, sampling_mask=mask)
+    assert rel_err(y, d["y"]) < TOL
+    opt = m.configure_optimizers()["optimizer"]
+    loss_buf = torch.zeros((), device=DEV)
+
+    def step_c3():
+        opt.zero_grad()
+        loss = m.training_step(batch, sampling_mask=mask)["loss"]
+        loss.backward()
+        opt.step()
+        loss_buf.copy_(loss.detach())
+    replay = capture(step_c3, 2, preserve=opt.state_tensors())
+    replay()
+    torch.cuda.synchronize()
+    Fn.check_errors()
+    _check_sampled_fixture(d, m, loss_buf)
+
+
+def test_c2_simple_lstm_b64_vs_oracle():
+    """BASELINE configs[1]'s shape in fp32 exactly as bench.py's step_c2 times it: SimpleLSTM B=64,
+    T=300, torch.manual_seed(0) weights, paired encoder recurrences, HIP-graph replay of fwd + MSE +
+    bwd + AdamW, vs the oracle's float64 answer (tests/golden/simple_lstm_b64_f64.npz): output,
+    loss, every gradient (max, L2, 257 samples) and the post-AdamW parameters.
+    Reference: simple_lstm.py:146-269 (with the Q3 unwrap)."""
+    from multimodalreactiongeneration_amd import configs as C
+    from multimodalreactiongeneration_amd import functional as Fn
+    from multimodalreactiongeneration_amd.graphs import capture
+    from multimodalreactiongeneration_amd.model import SimpleLSTM
+    from multimodalreactiongeneration_amd.synthetic import make_simple_batch
+    d = load("simple_lstm_b64_f64")
+    cfg, oc, me = C.simple_lstm_config()
+    torch.manual_seed(0)
+    m = SimpleLSTM(cfg, oc, me).set_precision("32")
+    _param_sum_matches(m, d)
+    m = m.to(DEV)
+    batch = make_simple_batch(B=64, T=300, device=DEV)
+    with torch.no_grad():
+        assert rel_err(m.forward(batch[0], batch[1]), d["y"]) < TOL
+    opt = m.configure_optimizers()["optimizer"]
+    loss_buf = torch.zeros((), device=DEV)
+
+    def step_c2():
+        opt.zero_grad()
+        loss = m.training_step(batch)["loss"]
+        loss.backward()
+        opt.step()
+        loss_buf.copy_(loss.detach())
+    replay = capture(step_c2, 2, preserve=opt.state_tensors())
+    replay()
+    torch.cuda.synchronize()
+    Fn.check_errors()
+    _check_sampled_fixture(d, m, loss_buf)
+
+
+def test_generation_b64_vs_oracle():
+    """lstmformer generation (Metaformer.prediction) at the benchmarked batch B=64 with
+    bench.py's weights and inputs, 40 frames, captured as one HIP graph with the mask in a device buffer
+    and replayed for full generation and for the RandomState(7) < 0.5 scheduled-sampling mask, vs the
+    oracle's float64 predictions (tests/golden/metaformer_gen_b64_f64.npz).  Reference: lstmformer.py:426-547."""
+    from multimodalreactiongeneration_amd import configs as C
+    from multimodalreactiongeneration_amd.graphs import capture
+    from multimodalreactiongeneration_amd.model import Metaformer
+    from multimodalreactiongeneration_amd.synthetic import make_batch
+    d = load("metaformer_gen_b64_f64")
+    mc, oc, me = C.lstmformer_config(ratio=1)
+    torch.manual_seed(0)
+    m = Metaformer(mc, oc, me)
+    _param_sum_matches(m, d)
+    m = m.to(DEV).eval()
+    T = 40
+    batch = make_batch(B=64, T=T, lead=12, seed=1234, device=DEV)
+    mask = torch.ones(T, dtype=torch.bool, device=DEV)
+    out = torch.zeros(64, T, 6, device=DEV)
+
+    def gen():
+        with torch.no_grad():
+            out.copy_(m._generate(batch, sampling_mask=mask))
+    replay = capture(gen, 1)
+    for mode in ("ss", "full"):
+        mask.copy_(torch.from_numpy(d[f"mask/{mode}"]))
+        replay()
+        torch.cuda.synchronize()
+        assert rel_err(out, d[f"pred/{mode}"]) < TOL, mode
 
 
 def test_encoder_stack_mfma_matches_per_layer_valu():
