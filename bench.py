@@ -44,12 +44,16 @@ FAMILIES = {
                 "recurrence, 8H^2 FLOP per (b, t) per layer and direction",
     "attn_fwd": "attn_fwd_kernel<64>: block-causal flash attention, 4D FLOP per visible (q, k) pair per head",
     "attn_bwd": "attn_bwd_dq_kernel<64> + attn_bwd_dkv_kernel<64>: 10D FLOP per visible pair per head",
+    "gru_fwd": "gru_fwd_kernel<H,G> (gru_rec.hip, persistent GRU recurrence, config_gru.yaml): 6H^2 FLOP per (b, t) per layer",
+    "gru_bwd": "gru_bwd_kernel<H,G> (gru_rec.hip, persistent reverse GRU recurrence): 6H^2 FLOP per (b, t) per layer",
 }
 PEAK_NOTES = {
     "gemm": "peak = f32 dense matrix peak (the dtype's); the GEMMs compute fp32 as a three-plane bf16 split "
             "(6 bf16 MFMAs per product, fp32-class error), whose own MFMA ceiling is 2500/6 = 416.7 TFLOP/s",
     "lstm_fwd": "latency-bound (one cross-CU hand-off per time step); VALU v_pk_fma_f32 peak = 157.3",
     "lstm_bwd": "latency-bound (one cross-CU hand-off per time step); VALU v_pk_fma_f32 peak = 157.3",
+    "gru_fwd": "latency-bound (one cross-CU hand-off per time step); VALU v_pk_fma_f32 peak = 157.3",
+    "gru_bwd": "latency-bound (one cross-CU hand-off per time step); VALU v_pk_fma_f32 peak = 157.3",
 }
 # rocprofv3 kernel-name prefix of each family in the PMC summary (tools/tools_pmc_summary.py)
 PMC_KEYS = {"gemm": "gemm_all", "lstm_fwd": "lstm_fwd", "lstm_bwd": "lstm_bwd",
@@ -705,7 +709,9 @@ def secondary(args, dev):
     # lstmformer with config_gru.yaml's mixers (every recurrent layer a GRU)
     mc, oc, me = C.lstmformer_config(ratio=1, emb_mixers=("gru", "gru", "gru"))
     torch.manual_seed(0)
-    m = Metaformer(mc, oc, me).to(dev)
+    m = Metaformer(mc, oc, me)
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.to(dev)
     opt = m.configure_optimizers()["optimizer"]
     batch = make_batch(B=B, T=T, seed=1234, device=dev)
 
@@ -715,10 +721,53 @@ def secondary(args, dev):
         opt.step()
     replay = capture(step_gru, 2, preserve=opt.state_tensors())
     ms = _timed_replay(replay, K, W)
+    kern = _probe_steps(step_gru)
+    cpu = None
+    if cpu_on:
+        info = _cpu_setup(args)
+        cb = 8
+        cbatch = make_batch(B=cb, T=T, seed=1234)
+        t = _time_cpu(lambda: O.run_train_step(O.metaformer_training_loss, sd, oc, mc, list(cbatch)), 1, 1)
+        cpu = dict(value=round(cb * T / t, 2), unit="frames/s", kind="port", **info,
+                   sample=f"oracle lstmformer train step with GRU mixers (fwd+loss+bwd+AdamW, the fused ATen GRU "
+                          f"nn.GRU runs on CPU) on a bounded sample B={cb} T={T} r=1, 1 timed after 1 warm-up")
     out["lstmformer_gru_train"] = _secondary_entry(
         "lstmformer train step with config_gru.yaml's GRU mixers (persistent GRU recurrences), B=64 T=300 r=1, "
         "HIP graph", ms, B * T, model_flops_per_frame(mc, 1, gates=3) + attn_flops_per_frame(mc, 1, T), "fp32",
-        ({}, None), None)
+        kern, cpu)
+    del m, opt, replay
+
+    progress("lstmformer r=8")
+    # the reference-faithful audio rate (pred_fps 12.5: audio T = 8 x 300 = 2400, config.yaml:200; SURVEY §8
+    # conventions, secondary row): same step as the headline at ratio 8
+    mc, oc, me = C.lstmformer_config(ratio=8)
+    torch.manual_seed(0)
+    m = Metaformer(mc, oc, me)
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.to(dev)
+    opt = m.configure_optimizers()["optimizer"]
+    batch = make_batch(B=B, T=T, ratio=8, seed=1234, device=dev)
+    one = torch.ones((), device=dev)
+
+    def step_r8():
+        opt.zero_grad()
+        m.training_step(list(batch))["loss"].backward(one)
+        opt.step()
+    replay = capture(step_r8, 2, preserve=opt.state_tensors())
+    ms = _timed_replay(replay, K, W)
+    kern = _probe_steps(step_r8)
+    cpu = None
+    if cpu_on:
+        info = _cpu_setup(args)
+        cb = 4
+        cbatch = make_batch(B=cb, T=T, ratio=8, seed=1234)
+        t = _time_cpu(lambda: O.run_train_step(O.metaformer_training_loss, sd, oc, mc, list(cbatch)), 1, 1)
+        cpu = dict(value=round(cb * T / t, 2), unit="frames/s", kind="port", **info,
+                   sample=f"oracle lstmformer train step r=8 (audio T=2400; fwd+loss+bwd+AdamW, fused ATen LSTMs) "
+                          f"on a bounded sample B={cb} T={T}, 1 timed after 1 warm-up")
+    out["lstmformer_r8_train"] = _secondary_entry(
+        "lstmformer train step at the reference-faithful audio rate r=8 (pred_fps 12.5, audio T=2400), B=64 T=300, "
+        "HIP graph", ms, B * T, model_flops_per_frame(mc, 8) + attn_flops_per_frame(mc, 8, T), "fp32", kern, cpu)
     del m, opt, replay
     Fn.check_errors()
     return out

@@ -102,6 +102,25 @@ int mrg_gemm_x6g_batched(int n, int M, int N, int K, float alpha, const float* c
                          const float* const* B, long ldb, float beta, float* const* C, long ldc,
                          const float* const* bias, int epilogue, const float* const* aux, long ldaux,
                          int bf16, hipStream_t stream);
+/* Three bf16 planes (the x6 split: v ~ p0 + p1 + p2) of n row-major fp32 weights, once per optimizer
+ * step: dst_i [3][R'][C'] with (R', C') = (rows_i, cols_i), or (cols_i, rows_i) when transpose_i.   */
+int mrg_split_planes_batched(int n, const float* const* src, void* const* dst, const int* rows, const int* cols,
+                             const int* transpose, hipStream_t stream);
+/* C = epi(alpha A B^T + beta C + bias), B as three bf16 planes (row n of plane p at
+ * Bplanes + p * bplane + n * ldb, bf16 elements), A [M][K] through the RowMap; K % 32 == 0.  The
+ * forward products x W^T and the input-gradient products dY W (B = planes of W^T) of the nn.Linear /
+ * LSTM / MultiheadAttention layers (mixer_block.py:63-74,237-252, for_sequential.py:42-51).      */
+int mrg_gemm_x6_planes(int M, int N, int K, float alpha, const float* A, long lda, long lda_hi, int a_rdiv,
+                       const void* Bplanes, long ldb, long bplane, float beta, float* C, long ldc,
+                       const float* bias, int epilogue, const float* aux, long ldaux, hipStream_t stream);
+/* n same-shape products on pre-split weight planes (three bf16 planes per weight, as made by
+ * mrg_split_planes_batched; plane p row r at Bplanes[i] + p * bplane + r * ldb bf16): the batched
+ * activation-times-weight products of the encoder stack and the fused integrators, fp32-class x6
+ * arithmetic.  K % 32 == 0, 16-byte aligned rows, n <= 16.                                         */
+int mrg_gemm_x6_planes_batched(int n, int M, int N, int K, float alpha, const float* const* A, long lda,
+                               const void* const* Bplanes, long ldb, long bplane, float beta,
+                               float* const* C, long ldc, const float* const* bias, int epilogue,
+                               const float* const* aux, long ldaux, hipStream_t stream);
 
 /* out[n] = beta*out[n] + sum_rows X(row, n); out2 (nullable) receives the same
  * sum (b_ih and b_hh share one gradient).  Bias gradients of every Linear.  */
@@ -309,8 +328,11 @@ int mrg_residual_layernorm_bwd(int rows, int E, const float* dy, const float* a,
                                float* workspace, hipStream_t stream);
 /* dgamma = dbeta = NULL in mrg_residual_layernorm_bwd leaves the per-block partials in the
  * workspace; this reduces them (dgamma/dbeta += or = their sums) — e.g. on another stream, since
- * only the optimizer reads parameter gradients.                                              */
-int mrg_residual_layernorm_param_reduce(int rows, int E, const float* workspace, float* dgamma,
+ * only the optimizer reads parameter gradients.  The reduce CONSUMES the workspace: each row
+ * group's sum overwrites that group's first partial row, so a second reduce of the same partials
+ * gives wrong sums (re-run the backward first).  Any number of streams may reduce concurrently
+ * (each (device, stream) has its own completion tickets, up to 64 pairs per process).          */
+int mrg_residual_layernorm_param_reduce(int rows, int E, float* workspace, float* dgamma,
                                         float* dbeta, int accumulate, hipStream_t stream);
 /* Row-mapped forms (E % 4 == 0, 16-byte aligned rows) for the time-major encoder stack
  * (mixer_block.py:479-507 per layer, run as time chunks): the forward's output rows y and the

@@ -2,7 +2,7 @@
  * mrg_tuning.h — tuning, measurement and test hooks of libmrg.so (not part of the drop-in
  * boundary in mrg.h): knobs the measured A/Bs in DESIGN.md used, the kernel-bound probes
  * bench.py times the families with, fault injection / CU-occupying stand-ins for the tests, and
- * the structural-variant and pre-split-plane GEMM entry points that measured slower in the step.
+ * the structural-variant GEMM entry points.
  * Same conventions as mrg.h (0 = success, mrg_last_error()).
  */
 #ifndef MRG_TUNING_H_
@@ -21,22 +21,16 @@ int mrg_gemm_set_glds(int depth, int bn);
 /* Weight-gradient products (transA 1, transB 0) on the LDS-DMA kernel (1, default) or the
  * register-staged one (0); returns the previous setting.                                        */
 int mrg_gemm_set_glds_wg(int on);
-/* Warp-specialized x6 kernels (gemm_wsp.hip: splitter waves fill bf16 planes while MFMA waves
- * multiply; bitwise the LDS-DMA forms' results), a bit mask: 1 = weight-gradient products, 2 = the
- * k-contiguous products (forward / input gradients, batched too), 0 = the LDS-DMA kernels;
- * env MRG_GEMM_WSP; returns the previous mask.                                                    */
-int mrg_gemm_set_wgrad_kernel(int wsp);
-/* Three bf16 planes (the x6 split: v ~ p0 + p1 + p2) of n row-major fp32 weights, once per optimizer
- * step: dst_i [3][R'][C'] with (R', C') = (rows_i, cols_i), or (cols_i, rows_i) when transpose_i.   */
-int mrg_split_planes_batched(int n, const float* const* src, void* const* dst, const int* rows, const int* cols,
-                             const int* transpose, hipStream_t stream);
-/* C = epi(alpha A B^T + beta C + bias), B as three bf16 planes (row n of plane p at
- * Bplanes + p * bplane + n * ldb, bf16 elements), A [M][K] through the RowMap; K % 32 == 0.  The
- * forward products x W^T and the input-gradient products dY W (B = planes of W^T) of the nn.Linear /
- * LSTM / MultiheadAttention layers (mixer_block.py:63-74,237-252, for_sequential.py:42-51).      */
-int mrg_gemm_x6_planes(int M, int N, int K, float alpha, const float* A, long lda, long lda_hi, int a_rdiv,
-                       const void* Bplanes, long ldb, long bplane, float beta, float* C, long ldc,
-                       const float* bias, int epilogue, const float* aux, long ldaux, hipStream_t stream);
+/* Kernel of mrg_gemm_x6_planes: 0 = gemm_x6g_kernel (pre-split B, 32 x 32 blocks), 10 * (bn / 64) + ns =
+ * gemm_x6w_kernel (gemm_wide.hip: row-owning waves, bn columns per tile, ring depth ns); env
+ * MRG_GEMM_WIDE; returns the previous setting.                                                      */
+int mrg_gemm_set_wide(int cfg);
+/* Diagnostics: block 0 of gemm_x6r_kernel records per-wave s_memtime stamps into buf ([waves][16] u64: start,
+ * B slice resident, each row block's start, end); null disables.  Never in timed runs.              */
+int mrg_gemm_debug_stamps(void* buf);
+/* Timing only: gemm_x6r_kernel structural variants (1 no epilogue stores, 2 no split, 3 no B reads, 4 no
+ * MFMA; outputs meaningless); 0 = the real kernel.  Returns the previous setting.                   */
+int mrg_gemm_x6r_debug(int v);
 /* Tuning only: force the tile shape (0: 128x128, 1: 128x64, 2: 64x64), -1 = heuristic. */
 int mrg_gemm_force_tile(int tile);
 /* Tuning only: structural variants of the x6 kernel (0 product, 1 split + one MFMA, 2 plane-0 +

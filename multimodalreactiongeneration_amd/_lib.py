@@ -36,10 +36,14 @@ SIGNATURES = {
     "mrg_gemm_force_tile": (c_int, [c_int]),
     "mrg_gemm_set_blocks_per_cu": (c_int, [c_int]),
     "mrg_gemm_set_glds": (c_int, [c_int, c_int]),
-    "mrg_gemm_set_wgrad_kernel": (c_int, [c_int]),
     "mrg_gemm_set_glds_wg": (c_int, [c_int]),
     "mrg_transpose_batched": (c_int, [c_int, PP, PP, PI, PI, P]),
     "mrg_split_planes_batched": (c_int, [c_int, PP, PP, PI, PI, PI, P]),
+    "mrg_gemm_set_wide": (c_int, [c_int]),
+    "mrg_gemm_x6_planes_batched": (c_int, [c_int, c_int, c_int, c_int, c_float, P, c_long, P, c_long, c_long, c_float,
+                                           P, c_long, P, c_int, P, c_long, P]),
+    "mrg_gemm_debug_stamps": (c_int, [P]),
+    "mrg_gemm_x6r_debug": (c_int, [c_int]),
     "mrg_gemm_x6_planes": (c_int, [c_int, c_int, c_int, c_float, P, c_long, c_long, c_int, P, c_long, c_long,
                                    c_float, P, c_long, P, c_int, P, c_long, P]),
     "mrg_lstm_set_blocks_per_cu": (c_int, [c_int]),

@@ -885,10 +885,6 @@ static int g_glds_wg = [] {  // weight-gradient products on gemm_x6g_wgrad_kerne
   const char* e = getenv("MRG_GEMM_GLDS_WG");
   return e ? atoi(e) : 1;
 }();
-static int g_wsp = [] {  // weight gradients on the warp-specialized kernel (gemm_wsp.hip); MRG_GEMM_WSP
-  const char* e = getenv("MRG_GEMM_WSP");
-  return e ? (atoi(e) & 3) : 0;   // bit 0: weight gradients, bit 1: k-contiguous products
-}();
 static int g_glds_bn = [] {  // 64 forces 64-wide column tiles (tuning); 128 = by shape
   const char* e = getenv("MRG_GEMM_GLDS_BN");
   return e ? atoi(e) : 128;
@@ -944,13 +940,6 @@ MRG_API int mrg_gemm_set_mode(int mode) {
 MRG_API int mrg_gemm_get_mode(void) { return g_gemm_mode; }
 
 // Weight-gradient products on the LDS-DMA kernel (1) or the register-staged one (0); returns the old value.
-// Weight-gradient kernel: 1 = warp-specialized (gemm_wsp.hip), 0 = the LDS-DMA form; returns the old one.
-MRG_API int mrg_gemm_set_wgrad_kernel(int wsp) {
-  const int prev = g_wsp;
-  g_wsp = wsp & 3;
-  return prev;
-}
-
 MRG_API int mrg_gemm_set_glds_wg(int on) {
   const int prev = g_glds_wg;
   g_glds_wg = on ? 1 : 0;
@@ -1106,8 +1095,7 @@ static int gemm_ex(int mode, int M, int N, int K, float alpha,
     if (N >= 1024) bm = 128;
     else if (N == 256 && K <= 256) bn = 64;
     if (g_glds_bn == 64) bn = 64;
-    if ((g_wsp & 2) && mode != 2) launch_x6s(a, bm, bn, stream);
-    else launch_x6g(a, g_glds, bm, bn, stream, mode == 2 ? 1 : 3);
+    launch_x6g(a, g_glds, bm, bn, stream, mode == 2 ? 1 : 3);
     return check_launch("gemm_x6g_kernel");
   }
   int tile;  // 0: 128x128, 1: 128x64, 2: 64x64
@@ -1141,8 +1129,7 @@ static int gemm_ex(int mode, int M, int N, int K, float alpha,
   if (wg) {
     tile = 0;
     const int cap = g_blocks_per_cu > 0 ? g_blocks_per_cu * resident_cus() : 0;
-    if ((g_wsp & 1) && mode != 2) launch_x6s_wgrad(a, splits, stream, cap);
-    else launch_x6g_wgrad(a, splits, 128, 128, stream, mode == 2 ? 1 : 3, cap);
+    launch_x6g_wgrad(a, splits, 128, 128, stream, mode == 2 ? 1 : 3, cap);
   } else if (launch_gemm(mode, a, tile, bk, transA, transB, va, vb, splits, stream)) {
     return 2;
   }
@@ -1251,8 +1238,7 @@ MRG_API int mrg_gemm_x6g_batched(int n, int M, int N, int K, float alpha, const 
   if (N >= 1024) bm = 128;
   else if (N == 256 && K <= 256) bn = 64;
   if (g_glds_bn == 64) bn = 64;
-  if ((g_wsp & 2) && mode != 2) launch_x6s(a, bm, bn, stream, &gb);
-  else launch_x6g(a, g_glds, bm, bn, stream, mode == 2 ? 1 : 3, &gb);
+  launch_x6g(a, g_glds, bm, bn, stream, mode == 2 ? 1 : 3, &gb);
   return check_launch("gemm_x6g_kernel (batched)");
 }
 

@@ -145,11 +145,13 @@ void launch_x6g(GemmArgs a, int ns, int bm, int bn, hipStream_t s, int planes = 
 // max_grid > 0: at most that many workgroups (a multiple of 8), walking the items
 void launch_x6g_wgrad(GemmArgs a, int splits, int bm, int bn, hipStream_t s, int planes = 3, int max_grid = 0);
 
-// warp-specialized weight-gradient form (gemm_wsp.hip): same contract as launch_x6g_wgrad (x6 only),
-// 128 x 128 tiles, bitwise the same results
-void launch_x6s_wgrad(GemmArgs a, int splits, hipStream_t s, int max_grid = 0);
-// and of the k-contiguous products (launch_x6g's contract, x6 only; bm, bn in {64, 128})
-void launch_x6s(GemmArgs a, int bm, int bn, hipStream_t s, const GemmBatch* gb = nullptr);
+
+// row-owning x6 kernel on pre-split B planes (gemm_wide.hip): 64-row tiles, bn in {64, 128, 256},
+// ring depth ns in {2, 3}
+void launch_x6w(GemmArgs a, int bn, int ns, long bplane, hipStream_t s, const GemmBatch* gb = nullptr);
+// B-resident form (gemm_wide.hip) for K in {128, 256}: one workgroup of `waves` waves per CU; returns -1
+// when K is not supported
+int launch_x6r(GemmArgs a, long bplane, hipStream_t s, int waves);
 
 static constexpr int MRG_TP_MAX = 32;
 struct TransposeBatch {

@@ -589,6 +589,11 @@ __global__ __launch_bounds__(256) void split_planes_kernel(PlaneBatch pb) {
 
 using namespace mrg;
 
+static int g_wide_cfg = [] {
+  const char* e = getenv("MRG_GEMM_WIDE");
+  return e ? atoi(e) : 12;
+}();
+
 // planes of n weights (see split_planes_kernel): dst_i holds 3 x rows_i x cols_i bf16
 MRG_API int mrg_split_planes_batched(int n, const float* const* src, void* const* dst, const int* rows, const int* cols,
                                      const int* transpose, hipStream_t stream) {
@@ -637,6 +642,13 @@ MRG_API int mrg_gemm_x6_planes(int M, int N, int K, float alpha, const float* A,
   a.kchunk = K;
   a.vec = ((((uintptr_t)C | (uintptr_t)bias | (uintptr_t)aux) & 15) == 0 && (ldc & 3) == 0 &&
            (!aux || (ldaux & 3) == 0)) ? 1 : 0;
+  if ((g_wide_cfg == 4 || g_wide_cfg == 8) && launch_x6r(a, bplane, stream, g_wide_cfg) == 0)
+    return check_launch("gemm_x6r_kernel");
+  if (g_wide_cfg > 8) {   // row-owning kernel (gemm_wide.hip); cfg = 10 * bn / 64 + ns, 0 = the kernel below
+    const int bn = N <= 64 ? 64 : 64 * (g_wide_cfg / 10), ns = g_wide_cfg % 10;
+    launch_x6w(a, bn, ns, bplane, stream);
+    return check_launch("gemm_x6w_kernel");
+  }
   int bm = 64, bn = 128;  // the fp32-operand kernel's shape rule (gemm.hip)
   if (N >= 1024) bm = 128;
   else if (N <= 256 && K <= 256) bn = 64;
@@ -644,4 +656,58 @@ MRG_API int mrg_gemm_x6_planes(int M, int N, int K, float alpha, const float* A,
   none.n = 0;
   launch_shape<1>(a, 2, bm, bn, bplane, stream, none);
   return check_launch("gemm_x6g_kernel");
+}
+
+// n same-shape products C_p = epi(alpha A_p B_p^T + beta C_p + bias_p) in one launch, B_p as the three
+// bf16 planes of a weight (same ldb / plane stride for every p): the batched projections of the encoder
+// stack and of the fused integrators (encoder_stack.py, integrate.py) on the row-owning kernel.
+MRG_API int mrg_gemm_x6_planes_batched(int n, int M, int N, int K, float alpha, const float* const* A, long lda,
+                                       const void* const* Bplanes, long ldb, long bplane, float beta,
+                                       float* const* C, long ldc, const float* const* bias, int epilogue,
+                                       const float* const* aux, long ldaux, hipStream_t stream) {
+  MRG_REQUIRE(n >= 1 && n <= MRG_GB_MAX && M >= 0 && N >= 0 && K >= 0 && K % 32 == 0,
+              "mrg_gemm_x6_planes_batched: bad shape (n=%d, K=%d)", n, K);
+  MRG_REQUIRE(epilogue >= 0 && epilogue <= 3 && (epilogue < 2 || aux), "mrg_gemm_x6_planes_batched: bad epilogue");
+  MRG_REQUIRE((lda & 3) == 0 && (ldb & 7) == 0 && (bplane & 7) == 0, "mrg_gemm_x6_planes_batched: alignment");
+  if (M == 0 || N == 0) return 0;
+  GemmArgs a;
+  memset(&a, 0, sizeof(a));
+  a.M = M; a.N = N; a.K = K; a.alpha = alpha; a.beta = beta;
+  a.amap = RowMap{lda, 0, 0}; a.transA = 0;
+  a.bmap = RowMap{ldb, 0, 0}; a.transB = 1;
+  a.ldc = ldc; a.epi = epilogue; a.ldaux = ldaux;
+  a.kchunk = K;
+  GemmBatch gb;
+  memset(&gb, 0, sizeof(gb));
+  gb.n = n;
+  int vec = (ldc & 3) == 0 && (!aux || (ldaux & 3) == 0);
+  for (int p = 0; p < n; ++p) {
+    MRG_REQUIRE((((uintptr_t)A[p] | (uintptr_t)Bplanes[p]) & 15) == 0, "mrg_gemm_x6_planes_batched: unaligned operand");
+    gb.A[p] = A[p]; gb.B[p] = reinterpret_cast<const float*>(Bplanes[p]); gb.C[p] = C[p];
+    gb.bias[p] = bias ? bias[p] : nullptr;
+    gb.aux[p] = aux ? aux[p] : nullptr;
+    if ((((uintptr_t)C[p] | (uintptr_t)gb.bias[p] | (uintptr_t)gb.aux[p]) & 15) != 0) vec = 0;
+  }
+  a.A = gb.A[0]; a.B = gb.B[0]; a.C = gb.C[0]; a.bias = gb.bias[0]; a.aux = gb.aux[0];
+  a.vec = vec;
+  const int cfg = g_wide_cfg > 8 ? g_wide_cfg : 12;
+  launch_x6w(a, N <= 64 ? 64 : 64 * (cfg / 10), cfg % 10, bplane, stream, &gb);
+  return check_launch("gemm_x6w_kernel (batched)");
+}
+
+namespace mrg { int x6r_debug_stamps(void* buf); extern int g_x6r_dbg; }
+// Timing only: gemm_x6r_kernel structural variants (1 no epilogue stores, 2 no split, 3 no B reads,
+// 4 no MFMA; outputs meaningless), 0 = the real kernel.  Returns the previous setting.
+MRG_API int mrg_gemm_x6r_debug(int v) { const int p = mrg::g_x6r_dbg; mrg::g_x6r_dbg = v; return p; }
+// Diagnostics: gemm_x6r_kernel's block 0 records s_memtime stamps per wave into buf ([waves][16] u64:
+// start, B resident, each row block's start, end); null disables.  Never in timed runs.
+MRG_API int mrg_gemm_debug_stamps(void* buf) { return mrg::x6r_debug_stamps(buf); }
+
+// Tuning: which kernel mrg_gemm_x6_planes runs (0 = gemm_x6g_kernel with pre-split B; 10 * (bn / 64) + ns =
+// gemm_x6w_kernel with bn columns and ring depth ns); returns the previous setting.
+MRG_API int mrg_gemm_set_wide(int cfg) {
+  const int prev = g_wide_cfg;
+  if (cfg == 0 || cfg == 4 || cfg == 8 || cfg == 12 || cfg == 13 || cfg == 22 || cfg == 23 || cfg == 42)
+    g_wide_cfg = cfg;
+  return prev;
 }

@@ -4,6 +4,7 @@
 // wave shuffles (no LDS); parameter-gradient column sums go through per-block
 // fp32 partials reduced in a fixed order (deterministic).
 #include <atomic>
+#include <mutex>
 #include "mrg_common.h"
 
 namespace mrg {
@@ -304,7 +305,7 @@ __global__ __launch_bounds__(256) void resln_bwd_v4_batched_kernel(LnBatch lb, i
 // 8 workgroups that each walked all 600 partial rows of a 19,200-row LayerNorm: 13.3 us per call,
 // 1.2 % of HBM.  4-wave workgroups, so they still fit beside a persistent
 // recurrence as deferred parameter-gradient products.
-constexpr int RESLN_TSLOTS = 64;                 // ticket sets, rotated per launch (see launcher)
+constexpr int RESLN_TSLOTS = 64;                 // ticket sets: one per (device, stream) (see launcher)
 constexpr int RESLN_MAXCB = 32;                  // column blocks: 2E / 64 <= 32 (E <= 1024)
 __device__ unsigned g_resln_tickets[RESLN_TSLOTS * RESLN_MAXCB];
 
@@ -591,7 +592,7 @@ MRG_API size_t mrg_residual_layernorm_bwd_workspace_bytes(int rows, int E) {
   return (size_t)nblk * 2 * E * sizeof(float);
 }
 
-MRG_API int mrg_residual_layernorm_param_reduce(int rows, int E, const float* workspace, float* dgamma,
+MRG_API int mrg_residual_layernorm_param_reduce(int rows, int E, float* workspace, float* dgamma,
                                                 float* dbeta, int accumulate, hipStream_t stream);
 
 MRG_API int mrg_residual_layernorm_bwd(int rows, int E, const float* dy, const float* a,
@@ -720,7 +721,38 @@ MRG_API int mrg_residual_layernorm_bwd_batched(int n, int rows, int E, const flo
   return check_launch("resln_bwd_v4_batched_kernel");
 }
 
-MRG_API int mrg_residual_layernorm_param_reduce(int rows, int E, const float* workspace, float* dgamma,
+// The ticket set of a launch belongs to its (device, stream): launches on one stream run one after
+// the other (in a captured graph, nodes of one capture stream are chained), and every ticket is back
+// at 0 before a launch ends, so one set per stream is never shared by two launches in flight, however
+// far another stream lags (a rotation over a global pool could hand two overlapping
+// launches on different streams the same set).  The symbol is resolved per device.
+static std::mutex g_tick_mu;
+static struct { int dev; hipStream_t s; } g_tick_owner[RESLN_TSLOTS];
+static int g_tick_used = 0;
+static void* g_tick_base[64];
+
+static int resln_tickets(hipStream_t stream, unsigned** tick) {
+  int dev = 0;
+  MRG_HIP(hipGetDevice(&dev));
+  MRG_REQUIRE(dev >= 0 && dev < 64, "mrg_residual_layernorm_param_reduce: device %d", dev);
+  std::lock_guard<std::mutex> lk(g_tick_mu);
+  if (!g_tick_base[dev]) MRG_HIP(hipGetSymbolAddress(&g_tick_base[dev], HIP_SYMBOL(g_resln_tickets)));
+  int slot = -1;
+  for (int i = 0; i < g_tick_used; ++i)
+    if (g_tick_owner[i].dev == dev && g_tick_owner[i].s == stream) { slot = i; break; }
+  if (slot < 0) {
+    MRG_REQUIRE(g_tick_used < RESLN_TSLOTS,
+                "mrg_residual_layernorm_param_reduce: more than %d (device, stream) pairs issued reduces",
+                RESLN_TSLOTS);
+    slot = g_tick_used++;
+    g_tick_owner[slot].dev = dev;
+    g_tick_owner[slot].s = stream;
+  }
+  *tick = static_cast<unsigned*>(g_tick_base[dev]) + slot * RESLN_MAXCB;
+  return 0;
+}
+
+MRG_API int mrg_residual_layernorm_param_reduce(int rows, int E, float* workspace, float* dgamma,
                                                 float* dbeta, int accumulate, hipStream_t stream) {
   if (rows == 0) return 0;
   MRG_REQUIRE(E >= 1 && E <= 1024 && dgamma && dbeta && workspace,
@@ -728,20 +760,11 @@ MRG_API int mrg_residual_layernorm_param_reduce(int rows, int E, const float* wo
   const int nblk = (rows + RESLN_RPB - 1) / RESLN_RPB;
   // row groups of >= 16 partial rows (distinct first rows), at most 16
   const int R = nblk >= 32 ? (nblk / 16 < 16 ? nblk / 16 : 16) : 1;
-  // one ticket set per launch, rotated: two launches share a set only 64 launches apart, and at
-  // most one launch per stream is in flight (every ticket returns to 0 before its launch ends)
-  static std::atomic<unsigned> slot{0};
   unsigned* tick = nullptr;
-  if (R > 1) {
-    // resolved once (the first call is an eager warm-up step, never inside a stream capture); one
-    // process drives one device
-    static void* base = nullptr;
-    if (!base) MRG_HIP(hipGetSymbolAddress(&base, HIP_SYMBOL(g_resln_tickets)));
-    tick = static_cast<unsigned*>(base) + (slot.fetch_add(1) % RESLN_TSLOTS) * RESLN_MAXCB;
-  }
+  if (R > 1 && resln_tickets(stream, &tick)) return 1;
   // the partials are consumed in place (each row group's sum overwrites its first row)
-  resln_param_reduce_kernel<<<dim3((2 * E + 63) / 64, R), 256, 0, stream>>>(const_cast<float*>(workspace), nblk, E,
-                                                                            dgamma, dbeta, accumulate, R, tick);
+  resln_param_reduce_kernel<<<dim3((2 * E + 63) / 64, R), 256, 0, stream>>>(workspace, nblk, E, dgamma, dbeta,
+                                                                            accumulate, R, tick);
   return check_launch("resln_param_reduce_kernel");
 }
 

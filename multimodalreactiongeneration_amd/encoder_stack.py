@@ -177,6 +177,8 @@ def _bgemm(lib, M, N, K, items, lda, ldc, *, epi=0, ldaux=0, transposed=False, d
     dY (w^T)^T through the [in][out] copies (functional._wt); per product when a copy is missing."""
     if not items:
         return
+    if Fn.planes_batched(M, N, K, items, lda, ldc, epi=epi, ldaux=ldaux, transposed=transposed):
+        return
     bs = []
     for a_p, w, c_p, b_p, x_p in items:
         if transposed:

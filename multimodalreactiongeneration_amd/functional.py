@@ -408,9 +408,19 @@ def _capture_point(stream):
 def _fork(key, s, cur):
     """s.wait_stream(cur), skipped under capture when s already waited on cur's current point."""
     point = _capture_point(cur) if _FORK_GUARD[0] and torch.cuda.is_current_stream_capturing() else None
-    if point is None or _LAST_FORK.get(key) != point:
+    if point is None or _LAST_FORK.get(key) != (point, s.cuda_stream):
         s.wait_stream(cur)
-    _LAST_FORK[key] = point
+    _LAST_FORK[key] = None if point is None else (point, s.cuda_stream)
+
+
+def reset_fork_point(key=None):
+    """Forget the recorded fork point (all devices when key is None): called wherever the main and side
+    streams are joined or ordered outside _fork, and at the end of every capture (graphs.capture), so
+    the guard only ever skips a wait that an earlier _fork of the same capture really issued."""
+    if key is None:
+        _LAST_FORK.clear()
+    else:
+        _LAST_FORK.pop(key, None)
 
 
 def _ensure_join(key, cur, s, task):
@@ -418,6 +428,7 @@ def _ensure_join(key, cur, s, task):
         def join(cur=cur, s=s, key=key):
             _flush_deferred(key, cur.device)
             cur.wait_stream(s)
+            reset_fork_point(key)
             _JOIN_PENDING.pop(key, None)
             _SIDE_HOLD.pop(key, None)   # their blocks are reusable now: later work is ordered after the wait
         torch.autograd.Variable._execution_engine.queue_callback(join)
@@ -502,6 +513,7 @@ def _on_side(device, rows, keep, fn):
     if key in _JOIN_PENDING and _JOIN_PENDING[key] != task:
         _flush_deferred(key, dev)
         cur.wait_stream(_SIDE[key])
+        reset_fork_point(key)
         del _JOIN_PENDING[key]
     s = _SIDE.get(key)
     if s is None:
@@ -529,11 +541,13 @@ class _side:
             # left over from a backward that did not finish: order after its side-stream work
             _flush_deferred(key, dev)
             cur.wait_stream(s)
+            reset_fork_point(key)
             del _JOIN_PENDING[key]
         if self.rows < _SIDE_MIN_ROWS:
             if key in _JOIN_PENDING:  # order this write after the side stream's pending ones
                 _flush_deferred(key, dev)
                 cur.wait_stream(s)
+                reset_fork_point(key)
             return self
         if task < 0:  # not inside a backward pass: stay on the current stream
             return self
@@ -637,7 +651,7 @@ def _wt(w):
 # resolves to its parent's planes.  Opt-in (MRG_WEIGHT_PLANES=1 / set_weight_planes): 3-10 % faster
 # per product in isolation, but the step measured 0.9 ms SLOWER with it (every kernel of the step ran
 # ~3 % slower beside the extra plane traffic), so it is off by default.
-_PL_ON = [os.environ.get("MRG_WEIGHT_PLANES", "0") == "1"]
+_PL_ON = [os.environ.get("MRG_WEIGHT_PLANES", "1") == "1"]
 _PLANES = {}
 
 
@@ -714,6 +728,27 @@ def _planes_gemm(M, N, K, A, lda, planes, C, ldc, *, beta=0.0, bias=None, epi=0,
         rc = _lib.load().mrg_gemm_x6_planes(M, N, K, 1.0, A, lda, a_hi, a_div, bp, ldb, bplane, beta, C, ldc, bias,
                                            epi, aux, ldaux, _stream())
     _lib.check(rc, "gemm (weight planes)")
+
+
+def planes_batched(M, N, K, items, lda, ldc, *, epi=0, ldaux=0, beta=0.0, transposed=False):
+    """Same-shape products C_p = epi(A_p w_p^T ...) (transposed: dY_p w_p, on the planes of w_p^T) in ONE
+    launch on the weights' pre-split planes (mrg_gemm_x6_planes_batched); items = [(A ptr, w, C ptr,
+    bias ptr | None, aux ptr | None)].  Returns False (nothing launched) when a weight has no planes
+    or the planes' strides differ, so the caller takes its fp32-operand path."""
+    if not (M >= _WT_MIN_ROWS and K % 32 == 0 and _ARITH[0] is None and 0 < len(items) <= 16):
+        return False
+    pls = [_plane_operand(w, transposed) for _, w, _, _, _ in items]
+    if any(p is None for p in pls) or len({(p[1], p[2]) for p in pls}) != 1:
+        return False
+    n, VP = len(items), ctypes.c_void_p
+    arr = lambda xs: (VP * n)(*xs)  # noqa: E731
+    with _probe("gemm", 2.0 * M * N * K * n):
+        rc = _lib.load().mrg_gemm_x6_planes_batched(
+            n, M, N, K, 1.0, arr([it[0] for it in items]), lda, arr([p[0] for p in pls]), pls[0][1], pls[0][2], beta,
+            arr([it[2] for it in items]), ldc, None if all(it[3] is None for it in items) else arr([it[3] for it in items]),
+            epi, None if all(it[4] is None for it in items) else arr([it[4] for it in items]), ldaux, _stream())
+    _lib.check(rc, "batched gemm (weight planes)")
+    return True
 
 
 def _fwd_gemm(M, N, K, A, lda, w, C, ldc, **kw):

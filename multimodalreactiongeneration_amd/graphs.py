@@ -29,8 +29,13 @@ def capture(step: Callable[[], object], warmup: int = 2, preserve: Sequence[torc
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
     graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
-        step()
+    from . import functional as Fn
+    Fn.reset_fork_point()
+    try:
+        with torch.cuda.graph(graph):
+            step()
+    finally:
+        Fn.reset_fork_point()   # fork points are per capture (functional._fork's guard)
     with torch.no_grad():
         for t, v in zip(preserve, saved):
             t.copy_(v)

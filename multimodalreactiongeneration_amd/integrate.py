@@ -50,6 +50,8 @@ def _bgemm(M, N, K, items, lda, ldc, *, epi=0, ldaux=0, transposed=False, beta=0
     transposed: input-gradient products dY w through w's [in][out] copy (functional._wt), one by one
     when a copy is missing."""
     lib = _lib.load()
+    if Fn.planes_batched(M, N, K, items, lda, ldc, epi=epi, ldaux=ldaux, beta=beta, transposed=transposed):
+        return
     bs = []
     for a_p, w, c_p, b_p, x_p in items:
         wt = Fn._wt(w) if (transposed and M >= Fn._WT_MIN_ROWS) else (None if transposed else w)
@@ -78,15 +80,33 @@ class KVSink:
     that received a gradient has run its backward.  So the sum is never formed by autograd's separate
     adds, and it is right in any consumer order, for several forwards over one source, for a source
     passed twice to one op and when some consumers' backward never runs.  A source whose producer does
-    not drain (no ``_mrg_kv_sink`` attribute) gets per-consumer gradients that autograd sums."""
-    __slots__ = ("written", "buf")
+    not drain (no ``_mrg_kv_sink`` attribute) gets per-consumer gradients that autograd sums.
+
+    Limitation: the consumers return None for a sinked source, so the summed gradient
+    reaches the source tensor only inside its producer's backward.  ``torch.autograd.grad(...,
+    inputs=[encoder_output])``, tensor hooks and ``retain_grad()`` on an encoder output therefore see
+    a gradient without the integrators' share.  A backward pass that ends before the producer drains
+    (e.g. one stopped at the encoder outputs) would leave a stale sum behind: the next pass's first
+    write detects it (the autograd graph task that wrote it is recorded) and raises instead of adding
+    onto it."""
+    __slots__ = ("written", "buf", "task")
 
     def __init__(self):
-        self.written, self.buf = 0, None
+        self.written, self.buf, self.task = 0, None, None
+
+    def begin_write(self):
+        """Called by a consumer before it adds its share: True when it is the first write of this pass."""
+        task = torch._C._current_graph_task_id()
+        if self.written and self.task != task:
+            raise RuntimeError("integrate.KVSink: a key / value gradient sum from an earlier backward pass was "
+                               "never drained by its producer (a backward stopped at the encoder outputs?); "
+                               "refusing to add this pass's gradient onto it")
+        self.task = task
+        return self.written == 0
 
     def drain(self):
         buf = self.buf if self.written else None
-        self.written, self.buf = 0, None
+        self.written, self.buf, self.task = 0, None, None
         return buf
 
 
@@ -223,10 +243,11 @@ class _IntegrateFn(Function):
                 _dx_gemm(B * Tk, E, 2 * E, _ptr(dKV[i]), 2 * E, P[i][0][E:], _ptr(g), E, device=dev)
                 dkv.append(g)
                 continue
-            if sink.written == 0:
+            first = sink.begin_write()
+            if first:
                 sink.buf = torch.empty(B, Tk, E, **f32)
             _dx_gemm(B * Tk, E, 2 * E, _ptr(dKV[i]), 2 * E, P[i][0][E:], _ptr(sink.buf), E,
-                     beta=0.0 if sink.written == 0 else 1.0, device=dev)
+                     beta=0.0 if first else 1.0, device=dev)
             sink.written += 1
             dkv.append(None)   # the producer drains the sum (KVSink)
         _IntegrateFn._param_grads(lib, ctx, dev, do2, cat, G2, U, G1, O, dQ, q2, dKV, kv2, ws1, ws2, N, E, n)

@@ -105,7 +105,7 @@ class IntegrateModalBlock(nn.Module):
 
     def fused_args(self, main_modal, other_modals, attn_mask, hxs):
         """(per-integrator parameter tuples, cat_w, cat_b, heads, causal, eps, qpads, kpads) of the fused
-        form (integrate.py, block_stack.py), or None when the block is outside it."""
+        form (integrate.py), or None when the block is outside it."""
         from .masks import BlockCausalMask
         if not (self.use_fused and isinstance(main_modal, torch.Tensor) and main_modal.is_cuda
                 and main_modal.dim() == 3 and main_modal.shape[1] >= _FUSED_MIN_T and all(h is None for h in hxs)):
@@ -356,55 +356,6 @@ class MultiModalMetaformer(nn.Module):
             return None
         return encoder_stack([(f, e.weight, e.bias, l) for f, e, l in zip(feats, embs, layers)], eps)
 
-    # ---- MI355X schedule: blocks 1.. as one (block, time-chunk) wavefront (block_stack.py).  Opt-in
-    # (MRG_BLOCK_STACK=1): at B=64 T=300 it saves ~1 ms of recurrence time but its chunked GEMMs,
-    # attention and LayerNorms cost as much again, 21.6 vs 21.2 ms/step replayed
-    use_block_stack = os.environ.get("MRG_BLOCK_STACK", "0") == "1"
-
-    def _stack_blocks(self, x, other_modals, attn_mask):
-        """The output of blocks 1.. through block_stack.block_stack, or None when a block is outside its
-        form (LSTM block as in the encoder stack, fused-integrator form, Linear-ReLU-Linear residual-LN
-        FeedForward, one LayerNorm eps) or the input is not a CUDA fp32 [B, T, E] tensor."""
-        from ..block_stack import block_stack, CHUNK
-        blocks = list(self.metaformer_blocks)[1:]
-        if not (self.use_block_stack and CHUNK > 0 and blocks and isinstance(x, torch.Tensor) and x.is_cuda
-                and x.dim() == 3 and x.shape[1] >= 2 and Fn._ARITH[0] is None and x.shape[2] % 4 == 0):
-            return None
-        if any(b.encode_other_modal for b in blocks):
-            return None
-        flat, eps_all, fa0 = [], set(), None
-        for b in blocks:
-            got = self._stack_layers(b)
-            if got is None or len(got[0]) != 1 or len(got[0][0]) != 1:
-                return None
-            layer, eps = got[0][0][0], got[1]
-            om, am, hx = b.integrator.check_form_input(other_modals, attn_mask, None)
-            fa = b.integrator.fused_args(x, om, am, hx)
-            if fa is None:
-                return None
-            params, cw, cb, heads, causal, ieps, qpads, kpads = fa
-            ff = getattr(b.feedforward, "feed_forward", None)
-            if not (isinstance(ff, ResidualConnection) and ff.layer_norm is not None):
-                return None
-            mods = list(ff.module.children())
-            if not (len(mods) == 3 and isinstance(mods[0], nn.Linear) and isinstance(mods[1], nn.ReLU)
-                    and isinstance(mods[2], nn.Linear) and mods[0].bias is not None and mods[2].bias is not None):
-                return None
-            if fa0 is None:
-                fa0 = (heads, causal, qpads, kpads, om)
-            elif (heads, causal) != fa0[:2] or any(a is not b2 for a, b2 in zip(qpads + kpads, fa0[2] + fa0[3])):
-                return None
-            eps_all.update((eps, ieps, ff.layer_norm.eps))
-            flat.append([*layer, *[t for p in params for t in p], cw, cb, mods[0].weight, mods[0].bias,
-                         mods[2].weight, mods[2].bias, ff.layer_norm.weight, ff.layer_norm.bias])
-        heads, causal, qpads, kpads, om = fa0
-        if len(eps_all) != 1:
-            return None
-        if x.shape[2] // heads not in (8, 16, 32, 64):
-            return None
-        sinks = [getattr(kv, "_mrg_kv_sink", None) for kv in om]
-        return block_stack(x, list(om), qpads, kpads, flat, heads, causal, eps_all.pop(), sinks)
-
     def _fast_eligible(self) -> bool:
         if self.interlayer_residual:
             return False
@@ -436,13 +387,6 @@ class MultiModalMetaformer(nn.Module):
         if fast:
             record = []
             for bi, block in enumerate(self.metaformer_blocks):
-                if bi == 1:
-                    out = self._stack_blocks(main_modal, other_modals, integrate_attn_mask)
-                    if out is not None:
-                        main_modal = out
-                        record += [{"emb": [None] * b.emb_num_modal, "crm": [None] * (self.modal_num - 1)}
-                                   for b in list(self.metaformer_blocks)[1:]]
-                        break
                 mods = [main_modal] + (list(other_modals) if block.encode_other_modal else [])
                 enc = stacked if (bi == 0 and stacked is not None) else self._fast_first_embedding(block, mods)
                 main_modal = enc[0]

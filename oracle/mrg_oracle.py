@@ -81,6 +81,12 @@ def gru_layer(x: Tensor, w_ih: Tensor, w_hh: Tensor, b_ih: Tensor, b_hh: Tensor,
     calls (mixer_block.py:169-208).  n = tanh(W_in x + b_in + r * (W_hn h + b_hn))."""
     B, T, _ = x.shape
     H = w_hh.shape[1]
+    if ATEN_LSTM and T > 0:
+        # the fused ATen GRU op nn.GRU dispatches to on CPU (timing of the reference's own path only)
+        h = x.new_zeros(1, B, H) if h0 is None else h0.unsqueeze(0)
+        xi = x.flip(1) if reverse else x
+        y, hT = torch.gru(xi, h, [w_ih, w_hh, b_ih, b_hh], True, 1, 0.0, True, False, True)
+        return (y.flip(1) if reverse else y), hT[0]
     gx = F.linear(x, w_ih, b_ih)
     h = x.new_zeros(B, H) if h0 is None else h0
     ys: List[Optional[Tensor]] = [None] * T
@@ -218,10 +224,12 @@ def _cat_inputs(inputs):
     return torch.cat([la, a], 1), torch.cat([lmp, mp], 1), torch.cat([lms, ms], 1)
 
 
-def _lstm_mixer_block(x, sd, p):
-    """LSTMMixerBlock (mixer_block.py:479-507): LN(LSTM(x)+x) then LN(Linear(y)+y)."""
-    y, _, _ = lstm_layer(x, sd[p + "mixer.module.mixer.weight_ih_l0"], sd[p + "mixer.module.mixer.weight_hh_l0"],
-                         sd[p + "mixer.module.mixer.bias_ih_l0"], sd[p + "mixer.module.mixer.bias_hh_l0"])
+def _lstm_mixer_block(x, sd, p, kind="lstm"):
+    """LSTMMixerBlock (mixer_block.py:479-507): LN(LSTM(x)+x) then LN(Linear(y)+y); with kind "gru"
+    the GRUMixerBlock of config_gru.yaml (mixer_block.py:169-208,355-428: nn.GRU under the same
+    parameter names)."""
+    w = [sd[p + "mixer.module.mixer." + n] for n in ("weight_ih_l0", "weight_hh_l0", "bias_ih_l0", "bias_hh_l0")]
+    y = gru_layer(x, *w)[0] if kind == "gru" else lstm_layer(x, *w)[0]
     y = residual_ln(y, x, sd, p + "mixer.layer_norm.")
     z = linear(y, sd, p + "feed_forward.feed_forward.module.feedforward.")
     return residual_ln(z, y, sd, p + "feed_forward.feed_forward.layer_norm.")
@@ -241,6 +249,10 @@ def metaformer_forward(sd: SD, cfg, inputs) -> Tensor:
     Recurrent state is never carried: every LSTM starts from zero.
     """
     heads, nb, enc = cfg["num_heads"], cfg["num_block"], cfg["encoder_num_layer"]
+    kinds = set(cfg.get("emb_mixers", ["lstm"] * 3))
+    if len(kinds) != 1 or not kinds <= {"lstm", "gru"}:
+        raise ValueError(f"oracle: uniform lstm or gru emb_mixers only (config.yaml / config_gru.yaml), got {kinds}")
+    kind = kinds.pop()
     a, mp, ms = _cat_inputs(inputs)
     T = mp.shape[1]
     mm_mask = gen_attention_mask(ms, mp, heads).reshape(-1, T, T)
@@ -254,7 +266,7 @@ def metaformer_forward(sd: SD, cfg, inputs) -> Tensor:
         for mi in range(len(mods)):
             x = mods[mi]
             for layer in range(1 if mi == 0 else enc):
-                x = _lstm_mixer_block(x, sd, bp + f"embedding.modal_embeddings.{mi}.mixer.{layer}.")
+                x = _lstm_mixer_block(x, sd, bp + f"embedding.modal_embeddings.{mi}.mixer.{layer}.", kind)
             mods[mi] = x
         main = mods[0]
         if blk == 0:

@@ -28,13 +28,16 @@ def _header_functions(names=HEADERS):
 
 def test_boundary_header_holds_no_tuning_hooks():
     """include/mrg.h is the drop-in boundary only: the tuning knobs, probes, fault injection and the
-    measured-slower GEMM variants live in include/mrg_tuning.h."""
+    structural GEMM variants live in include/mrg_tuning.h; the pre-split weight
+    planes and their products are the step's path since round 5 (gemm_wide.hip), so they are boundary."""
     boundary = set(_header_functions(("mrg.h",)))
     tuning = set(_header_functions(("mrg_tuning.h",)))
     assert not boundary & tuning
-    for name in ("mrg_gemm_x6_variant", "mrg_gemm_force_tile", "mrg_ssd_gate_cell_fwd_dbg", "mrg_split_planes_batched",
-                 "mrg_gemm_x6_planes", "mrg_lstm_debug_inject", "mrg_lstm_debug_stamps", "mrg_probe_start"):
+    for name in ("mrg_gemm_x6_variant", "mrg_gemm_force_tile", "mrg_ssd_gate_cell_fwd_dbg", "mrg_gemm_set_wide",
+                 "mrg_gemm_x6r_debug", "mrg_lstm_debug_inject", "mrg_lstm_debug_stamps", "mrg_probe_start"):
         assert name in tuning and name not in boundary, name
+    for name in ("mrg_split_planes_batched", "mrg_gemm_x6_planes", "mrg_gemm_x6_planes_batched"):
+        assert name in boundary, name
 
 
 def test_library_exports_every_header_symbol():
@@ -209,3 +212,34 @@ def test_comm_entry_points_load_without_a_gpu():
     assert lib.mrg_comm_id_bytes() == 128
     assert lib.mrg_comm_available() in (0, 1)
     assert lib.mrg_comm_destroy(None) == 0
+
+
+def test_kv_sink_refuses_stale_sum_from_an_earlier_backward():
+    """integrate.KVSink: a sum left by a backward pass whose producer never drained it is
+    detected by the next pass's first write (the autograd graph task is recorded) instead of being added
+    onto; a drained sink starts over."""
+    import torch
+    from multimodalreactiongeneration_amd.integrate import KVSink
+    sink = KVSink()
+    firsts = []
+
+    class Consumer(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x):
+            return x.clone()
+
+        @staticmethod
+        def backward(ctx, g):
+            firsts.append(sink.begin_write())
+            sink.written += 1
+            return g
+
+    x = torch.ones(3, requires_grad=True)
+    (Consumer.apply(x) + Consumer.apply(x)).sum().backward()   # two consumers, one pass
+    assert firsts == [True, False]
+    with pytest.raises(RuntimeError, match="never drained"):
+        Consumer.apply(x).sum().backward()                     # the first pass never drained
+    sink.drain()
+    firsts.clear()
+    Consumer.apply(x).sum().backward()
+    assert firsts == [True]

@@ -238,11 +238,9 @@ def test_weight_grad_kernels_vs_fp64(rows, N, In, time_shift, wg):
 @pytest.mark.parametrize("rows,N,In,time_shift", [(19200, 1024, 256, False), (64 * 299, 1024, 256, True),
                                                   (19200, 256, 256, False), (19200, 256, 512, False),
                                                   (2048, 100, 36, False), (6400, 64, 256, False)])
-def test_weight_grad_specialized_kernel_bitwise(rows, N, In, time_shift):
-    """The warp-specialized weight-gradient kernel (gemm_wsp.hip: splitter waves fill bf16 planes while
-    MFMA waves multiply) gives bitwise the LDS-DMA kernel's dW and fused bias sums (same products and
-    sums in the same order), split-K slabs, ragged tiles and the time-shifted RowMap form included,
-    and matches fp64."""
+def test_weight_grad_kernel_vs_fp64(rows, N, In, time_shift):
+    """The weight-gradient product (gemm_x6g_wgrad_kernel: dW += dY^T X with the bias gradient fused)
+    vs fp64: split-K slabs, ragged tiles and the time-shifted RowMap form of dW_hh included."""
     from multimodalreactiongeneration_amd import functional as Fn
     from multimodalreactiongeneration_amd import _lib as L
     lib = L.load()
@@ -260,21 +258,16 @@ def test_weight_grad_specialized_kernel_bitwise(rows, N, In, time_shift):
         kw = {}
         dyp, xp = Fn._ptr(dyd), Fn._ptr(xd)
     gw0, gb0 = torch.randn(N, In, generator=g), torch.randn(N, generator=g)
-    out = []
     prev = Fn.set_wgrad_stream(False)
     try:
-        for wsp in (0, 1):
-            old = lib.mrg_gemm_set_wgrad_kernel(wsp)
-            gw, gb = gw0.to(DEV), gb0.to(DEV)
-            Fn._wgrad(dyp, N, xp, In, dy.shape[0], N, In, gw, DEV, gb=gb, keep=(dyd, xd), **kw)
-            torch.cuda.synchronize()
-            lib.mrg_gemm_set_wgrad_kernel(old)
-            out.append((gw.clone(), gb.clone()))
+        gw, gb = gw0.to(DEV), gb0.to(DEV)
+        Fn._wgrad(dyp, N, xp, In, dy.shape[0], N, In, gw, DEV, gb=gb, keep=(dyd, xd), **kw)
+        torch.cuda.synchronize()
     finally:
         Fn.set_wgrad_stream(prev)
-    assert torch.equal(out[1][0], out[0][0]) and torch.equal(out[1][1], out[0][1])
-    assert rel_err(out[1][0], gw0.double() + dy.double().t() @ x.double()) < 2e-6
-    assert rel_err(out[1][1], gb0.double() + dy.double().sum(0)) < 2e-6
+    del lib
+    assert rel_err(gw, gw0.double() + dy.double().t() @ x.double()) < 2e-6
+    assert rel_err(gb, gb0.double() + dy.double().sum(0)) < 2e-6
 
 
 def _bf16(t):
@@ -438,6 +431,49 @@ def test_layernorm_param_reduce_row_groups(rows, E):
         y.backward(dy.to(DEV))
         torch.cuda.synchronize()
         assert rel_err(gd.grad, gr.grad) < TOL and rel_err(btd.grad, btr.grad) < TOL
+
+
+def test_layernorm_param_reduce_concurrent_streams():
+    """mrg_residual_layernorm_param_reduce on four streams at once, 24 launches each, streams held back
+    by busy kernels so their launches overlap in any order (tickets are per (device, stream),
+    not rotated over a global pool): every launch's dgamma / dbeta bitwise equals a lone reduce of the
+    same partials (each launch consumes its own copy of the workspace)."""
+    import ctypes
+    from multimodalreactiongeneration_amd import _lib
+    from multimodalreactiongeneration_amd.functional import _ptr
+    lib = _lib.load()
+    rows, E = 19200, 256
+    g = torch.Generator().manual_seed(77)
+    a, b, dy = (torch.randn(rows, E, generator=g).to(DEV) for _ in range(3))
+    gam, bet = (1 + 0.1 * torch.randn(E, generator=g)).to(DEV), (0.1 * torch.randn(E, generator=g)).to(DEV)
+    y, dx = torch.empty_like(a), torch.empty_like(a)
+    mean, rstd = torch.empty(rows, device=DEV), torch.empty(rows, device=DEV)
+    ws = torch.empty(lib.mrg_residual_layernorm_bwd_workspace_bytes(rows, E) // 4, device=DEV)
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _lib.check(lib.mrg_residual_layernorm_fwd(rows, E, _ptr(a), _ptr(b), _ptr(gam), _ptr(bet), 1e-5, _ptr(y),
+                                              _ptr(mean), _ptr(rstd), st), "fwd")
+    _lib.check(lib.mrg_residual_layernorm_bwd(rows, E, _ptr(dy), _ptr(a), _ptr(b), _ptr(gam), _ptr(mean),
+                                              _ptr(rstd), _ptr(dx), None, None, 0, _ptr(ws), st), "bwd")
+    ref = torch.empty(2, E, device=DEV)
+    w0 = ws.clone()
+    _lib.check(lib.mrg_residual_layernorm_param_reduce(rows, E, _ptr(w0), _ptr(ref[0]), _ptr(ref[1]), 0, st), "ref")
+    n_str, per = 4, 24
+    copies = [ws.clone() for _ in range(n_str * per)]
+    outs = torch.full((n_str * per, 2, E), float("nan"), device=DEV)
+    streams = [torch.cuda.Stream(device=DEV) for _ in range(n_str)]
+    torch.cuda.synchronize()
+    for j in range(per):
+        for i, s in enumerate(streams):
+            with torch.cuda.stream(s):
+                if j % 6 == i:
+                    _lib.check(lib.mrg_debug_busy(1, 64, 256, 200.0, ctypes.c_void_p(s.cuda_stream)), "busy")
+                k = j * n_str + i
+                _lib.check(lib.mrg_residual_layernorm_param_reduce(rows, E, _ptr(copies[k]), _ptr(outs[k, 0]),
+                                                                   _ptr(outs[k, 1]), 0,
+                                                                   ctypes.c_void_p(s.cuda_stream)), "reduce")
+    torch.cuda.synchronize()
+    for k in range(n_str * per):
+        assert torch.equal(outs[k], ref), k
 
 
 @pytest.mark.parametrize("loss_type", ["huber", "mse", "mae", "smoothl1"])
@@ -1168,52 +1204,48 @@ def test_batched_gemm_matches_single_products(M, N, K, epi, n, gemm_mode):
         assert rel_err(Cs[i], exact) < TOL
 
 
-@pytest.mark.parametrize("M,N,K,epi,beta,n", [(19200, 1024, 256, 0, 0.0, 1), (19200, 256, 256, 3, 0.0, 1),
-                                              (19200, 512, 256, 1, 0.0, 1), (19200, 256, 1024, 3, 1.0, 1),
-                                              (2100, 256, 512, 2, 0.0, 1), (6400, 1024, 256, 0, 0.0, 3),
-                                              (6400, 256, 256, 3, 1.0, 4)])
-def test_specialized_products_bitwise(M, N, K, epi, beta, n):
-    """The warp-specialized k-contiguous product kernel (gemm_wsp.hip, mrg_gemm_set_wgrad_kernel bit 2)
-    gives bitwise the LDS-DMA kernel's C = epi(A W^T + beta C + bias) for every tile shape the
-    dispatcher picks (128x128 at N >= 1024, 64x64 at N = K = 256, else 64x128), ragged M, every
-    epilogue, accumulation into C, and the batched form."""
+@pytest.mark.parametrize("M,N,K,epi,beta", [(19200, 1024, 256, 0, 0.0), (19200, 256, 256, 3, 0.0),
+                                            (19200, 512, 256, 1, 0.0), (19200, 256, 1024, 3, 1.0),
+                                            (2100, 256, 512, 2, 0.0), (6400, 1024, 256, 0, 0.0),
+                                            (6400, 256, 128, 3, 1.0), (1000, 200, 256, 1, 0.0)])
+def test_weight_plane_products_every_kernel(M, N, K, epi, beta):
+    """C = epi(A W^T + beta C + bias) on W's pre-split bf16 planes (mrg_gemm_x6_planes) through each kernel
+    mrg_gemm_set_wide selects: the LDS-DMA tile kernel (0), the B-resident kernel (gemm_x6r_kernel, 4 / 8
+    waves, K in {128, 256}; other K fall through to the next form) and the row-owning ring kernel
+    (gemm_x6w_kernel, 64 / 128 columns), vs fp64: every epilogue, accumulation into C, ragged M and N."""
     import ctypes
     from multimodalreactiongeneration_amd import _lib as L
     from multimodalreactiongeneration_amd import functional as Fn
     lib = L.load()
-    g = torch.Generator().manual_seed(M + N + K + n + epi)
-    As = [torch.randn(M, K, generator=g).to(DEV) for _ in range(n)]
-    Ws = [(torch.randn(N, K, generator=g) / math.sqrt(K)).to(DEV) for _ in range(n)]
-    bs = [torch.randn(N, generator=g).to(DEV) for _ in range(n)]
-    aux = [torch.randn(M, N, generator=g).to(DEV) for _ in range(n)] if epi >= 2 else None
-    C0 = [torch.randn(M, N, generator=g).to(DEV) for _ in range(n)]
-    VP = ctypes.c_void_p
-    arr = lambda v: (VP * n)(*[VP(t.data_ptr()) for t in v])  # noqa: E731
-    out = []
-    for wsp in (0, 2):
-        old = lib.mrg_gemm_set_wgrad_kernel(wsp)
-        Cs = [c.clone() for c in C0]
-        if n == 1:
-            L.check(lib.mrg_gemm_f32_ex(M, N, K, 1.0, VP(As[0].data_ptr()), 0, K, 0, 0, VP(Ws[0].data_ptr()), 1, K, 0,
-                                        0, beta, VP(Cs[0].data_ptr()), N, VP(bs[0].data_ptr()), epi,
-                                        None if aux is None else VP(aux[0].data_ptr()), N, None, 1, None, None, 0.0,
-                                        None, Fn._stream()), "single")
-        else:
-            L.check(lib.mrg_gemm_x6g_batched(n, M, N, K, 1.0, arr(As), K, arr(Ws), K, beta, arr(Cs), N, arr(bs), epi,
-                                             None if aux is None else arr(aux), N, 0, Fn._stream()), "batched")
-        torch.cuda.synchronize()
-        lib.mrg_gemm_set_wgrad_kernel(old)
-        out.append(Cs)
-    for i in range(n):
-        assert torch.equal(out[1][i], out[0][i]), i
-        exact = As[i].double() @ Ws[i].double().T + bs[i].double() + beta * C0[i].double()
-        if epi == 1:
-            exact = exact.clamp_min(0)
-        elif epi == 2:
-            exact = exact * (aux[i].double() > 0)
-        elif epi == 3:
-            exact = exact + aux[i].double()
-        assert rel_err(out[1][i], exact) < TOL
+    g = torch.Generator().manual_seed(M + N + K + epi)
+    A = torch.randn(M, K, generator=g).to(DEV)
+    W = (torch.randn(N, K, generator=g) / math.sqrt(K)).to(DEV)
+    b = torch.randn(N, generator=g).to(DEV)
+    aux = torch.randn(M, N, generator=g).to(DEV) if epi >= 2 else None
+    C0 = torch.randn(M, N, generator=g).to(DEV)
+    VP, CI = ctypes.c_void_p, ctypes.c_int
+    planes = torch.empty(3, N, K, dtype=torch.int16, device=DEV)
+    L.check(lib.mrg_split_planes_batched(1, (VP * 1)(VP(W.data_ptr())), (VP * 1)(VP(planes.data_ptr())), (CI * 1)(N),
+                                         (CI * 1)(K), (CI * 1)(0), Fn._stream()), "split")
+    exact = A.double() @ W.double().T + b.double() + beta * C0.double()
+    if epi == 1:
+        exact = exact.clamp_min(0)
+    elif epi == 2:
+        exact = exact * (aux.double() > 0)
+    elif epi == 3:
+        exact = exact + aux.double()
+    prev = lib.mrg_gemm_set_wide(0)
+    try:
+        for cfg in (0, 4, 8, 12, 22):
+            lib.mrg_gemm_set_wide(cfg)
+            C = C0.clone()
+            L.check(lib.mrg_gemm_x6_planes(M, N, K, 1.0, VP(A.data_ptr()), K, 0, 0, VP(planes.data_ptr()), K, N * K,
+                                           beta, VP(C.data_ptr()), N, VP(b.data_ptr()), epi,
+                                           None if aux is None else VP(aux.data_ptr()), N, Fn._stream()), "planes")
+            torch.cuda.synchronize()
+            assert rel_err(C, exact) < TOL, cfg
+    finally:
+        lib.mrg_gemm_set_wide(prev)
 
 
 @pytest.mark.parametrize("n,rows,E", [(11, 3840, 256), (3, 70, 512), (16, 32, 36)])
