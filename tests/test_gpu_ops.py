@@ -1243,7 +1243,45 @@ def test_weight_plane_products_every_kernel(M, N, K, epi, beta):
                                            beta, VP(C.data_ptr()), N, VP(b.data_ptr()), epi,
                                            None if aux is None else VP(aux.data_ptr()), N, Fn._stream()), "planes")
             torch.cuda.synchronize()
-            assert rel_err(C, exact) < TOL, cfg
+            # x6 is fp32-class: ~6e-7 of the output's scale, so a dropped or mis-split product (~1e-5) fails
+            assert ((C.double() - exact).abs().max() / exact.abs().max()).item() < 3e-6, cfg
+    finally:
+        lib.mrg_gemm_set_wide(prev)
+
+
+@pytest.mark.parametrize("n,M,N,K,epi,beta", [(5, 19200, 256, 256, 3, 0.0), (3, 6400, 1024, 256, 1, 1.0),
+                                              (2, 2100, 64, 512, 2, 0.0)])
+def test_batched_plane_products_match_single(n, M, N, K, epi, beta):
+    """mrg_gemm_x6_planes_batched (the encoder stack's and fused integrators' projections): each problem
+    bitwise equal to its own mrg_gemm_x6_planes launch on the same row-owning kernel configuration."""
+    import ctypes
+    from multimodalreactiongeneration_amd import _lib as L
+    from multimodalreactiongeneration_amd import functional as Fn
+    lib = L.load()
+    g = torch.Generator().manual_seed(n * M + N + K)
+    VP, CI = ctypes.c_void_p, ctypes.c_int
+    As = [torch.randn(M, K, generator=g).to(DEV) for _ in range(n)]
+    Ws = [(torch.randn(N, K, generator=g) / math.sqrt(K)).to(DEV) for _ in range(n)]
+    bs = [torch.randn(N, generator=g).to(DEV) for _ in range(n)]
+    aux = [torch.randn(M, N, generator=g).to(DEV) for _ in range(n)] if epi >= 2 else None
+    C0 = [torch.randn(M, N, generator=g).to(DEV) for _ in range(n)]
+    planes = [torch.empty(3, N, K, dtype=torch.int16, device=DEV) for _ in range(n)]
+    arr = lambda xs: (VP * n)(*[VP(x.data_ptr()) for x in xs])  # noqa: E731
+    L.check(lib.mrg_split_planes_batched(n, arr(Ws), arr(planes), (CI * n)(*[N] * n), (CI * n)(*[K] * n),
+                                         (CI * n)(*[0] * n), Fn._stream()), "split")
+    Cb = [c.clone() for c in C0]
+    L.check(lib.mrg_gemm_x6_planes_batched(n, M, N, K, 1.0, arr(As), K, arr(planes), K, N * K, beta, arr(Cb), N,
+                                           arr(bs), epi, None if aux is None else arr(aux), N, Fn._stream()),
+            "batched")
+    prev = lib.mrg_gemm_set_wide(12)
+    try:
+        for i in range(n):
+            C = C0[i].clone()
+            L.check(lib.mrg_gemm_x6_planes(M, N, K, 1.0, VP(As[i].data_ptr()), K, 0, 0, VP(planes[i].data_ptr()), K,
+                                           N * K, beta, VP(C.data_ptr()), N, VP(bs[i].data_ptr()), epi,
+                                           None if aux is None else VP(aux[i].data_ptr()), N, Fn._stream()), "single")
+            torch.cuda.synchronize()
+            assert torch.equal(Cb[i], C), i
     finally:
         lib.mrg_gemm_set_wide(prev)
 
