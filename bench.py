@@ -32,12 +32,13 @@ METRIC = "training frames/sec/GPU, lstmformer T=300 B=64; 1→8 GPU scaling"
 FP32_MFMA_PEAK_TF = 157.3   # MI355X_MICROARCH.md chip table (f32 matrix, dense)
 BF16_MFMA_PEAK_TF = 2500.0  # MI355X_MICROARCH.md chip table (bf16 matrix, dense)
 HBM_PEAK_GBS = 8000.0
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r04_pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r05_pmc_summary.json")
 
 # probe name (functional._probe) -> kernels it brackets; FLOPs are algorithmic
 FAMILIES = {
-    "gemm": "gemm_x6g_kernel (LDS-DMA, activation and input-gradient products) + gemm_x6_kernel (weight gradients, "
-            "+ splitk_reduce4_kernel): every GEMM of the step, 2MNK FLOP per launch",
+    "gemm": "gemm_x6w_kernel (row-owning, on the weights' pre-split bf16 planes: activation and input-gradient "
+            "products) + gemm_x6g_kernel (LDS-DMA, the rest) + gemm_x6g_wgrad_kernel / gemm_x6_kernel (weight "
+            "gradients, + splitk_reduce4_kernel): every GEMM of the step, 2MNK FLOP per launch",
     "lstm_fwd": "lstm_fwd_kernel<H,G,BS> (VALU) + lstm_fwd_mx_kernel (MFMA, H=256): persistent recurrence, "
                 "8H^2 FLOP per (b, t) per layer and direction",
     "lstm_bwd": "lstm_bwd_kernel<H,G,BS> (VALU) + lstm_bwd_mx_kernel (MFMA, H=256): persistent reverse "
@@ -60,7 +61,7 @@ PMC_KEYS = {"gemm": "gemm_all", "lstm_fwd": "lstm_fwd", "lstm_bwd": "lstm_bwd",
             "attn_fwd": "attn_fwd_kernel", "attn_bwd": "attn_bwd"}
 
 
-TRACE_SUMMARY = os.path.join(ROOT, "profiles", "r04_trace_roofline.json")
+TRACE_SUMMARY = os.path.join(ROOT, "profiles", "r05_trace_roofline.json")
 
 
 def trace_check(roof):

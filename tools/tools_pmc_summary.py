@@ -66,7 +66,8 @@ doc = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes
                                                    "adamw_kernel")},
                         lstm_fwd=fam_total(("lstm_fwd_kernel", "lstm_fwd_mx_kernel")),
                         lstm_bwd=fam_total(("lstm_bwd_kernel", "lstm_bwd_mx_kernel")),
-                        gemm_all=fam_total(("gemm_x6_kernel", "gemm_x6g_kernel", "gemm_x6g_wgrad_kernel",
+                        gemm_all=fam_total(("gemm_x6_kernel", "gemm_x6g_kernel", "gemm_x6g_wgrad_kernel", "gemm_x6w_kernel",
+                                            "gemm_x6r_kernel",
                                             "gemm_rows_kernel", "gemm_f32_kernel", "gemm_bf16"),
                                            extra=("splitk_reduce",))),
        "kernels": summary}
