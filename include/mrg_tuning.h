@@ -45,6 +45,9 @@ int mrg_lstm_debug_inject(int mode);
  * microseconds on `stream` (a stand-in for a CU-occupying kernel, e.g. an RCCL collective, beside a
  * persistent recurrence, which must then wait for CUs without timing out its hand-offs).        */
 int mrg_debug_busy(int blocks, int threads, int lds, double usec, hipStream_t stream);
+/* Diagnostics: a 1-thread kernel writing the 100 MHz wall clock into ((uint64*)buf)[slot] in `stream`'s
+ * order (tools/side_timing.py: when a replayed graph reaches a point). */
+int mrg_debug_stamp(void* buf, int slot, hipStream_t stream);
 /* Measurement (bench.py): while on, every kernel launched for a tagged library call (tag >= 0) is
  * timed by start / stop events bound to that kernel (hipExtLaunchKernelGGL): its own execution,
  * as rocprofv3 reports it.  stop waits, writes (ms, tag) per launch and returns the count. */

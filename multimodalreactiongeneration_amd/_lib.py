@@ -124,6 +124,7 @@ SIGNATURES = {
     "mrg_residual_layernorm_bwd_batched": (c_int, [c_int, c_int, c_int, PP, PL, PL, PI, PP, PP, PP, PP, PP, PP,
                                                    PP, P]),
     "mrg_debug_busy": (c_int, [c_int, c_int, c_int, ctypes.c_double, P]),
+    "mrg_debug_stamp": (c_int, [P, c_int, P]),
     "mrg_padding_flags": (c_int, [c_int, c_int, P, c_long, c_long, c_float, P, P]),
     "mrg_zero_padding": (c_int, [c_long, P, c_float, P, P]),
     "mrg_swap01": (c_int, [c_int, c_int, c_int, P, P, c_float, P]),

@@ -40,7 +40,16 @@ __global__ void busy_kernel(unsigned long long ticks, float* sink) {
   __syncthreads();
   if (sink && threadIdx.x == 0 && scratch[0] < 0.0f) sink[blockIdx.x] = scratch[0];   // never taken
 }
+// one wall-clock stamp (100 MHz, the same clock on every XCD) into buf[slot], by a 1-thread kernel
+// placed in a stream's order: diagnostics of when a point of a replayed graph was reached
+__global__ void stamp_kernel(unsigned long long* buf, int slot) { buf[slot] = wall_clock64(); }
 }  // namespace mrg
+
+MRG_API int mrg_debug_stamp(void* buf, int slot, hipStream_t stream) {
+  MRG_REQUIRE(buf && slot >= 0, "mrg_debug_stamp: bad slot");
+  mrg::stamp_kernel<<<1, 1, 0, stream>>>(static_cast<unsigned long long*>(buf), slot);
+  return mrg::check_launch("stamp_kernel");
+}
 
 MRG_API int mrg_debug_busy(int blocks, int threads, int lds, double usec, hipStream_t stream) {
   MRG_REQUIRE(blocks > 0 && threads > 0 && threads <= 1024 && lds >= threads * 4 && lds <= 160 * 1024,

@@ -145,7 +145,8 @@ def _hold_if_side(t: torch.Tensor):
         return
     dev = t.device.index or 0
     s = _SIDE.get(dev)
-    if (s is not None and torch.cuda.current_stream(t.device) == s and dev in _JOIN_PENDING
+    cur = torch.cuda.current_stream(t.device)
+    if (s is not None and (cur == s or cur in _POOL.get(dev, ())) and dev in _JOIN_PENDING
             and torch.cuda.is_current_stream_capturing()):
         _SIDE_HOLD.setdefault(dev, []).append(t)
 
@@ -362,6 +363,13 @@ def set_wgrad_stream(on: bool) -> bool:
 # gradient-ready listener (DDP bucket overlap) needs each write issued when it is reported.
 _DEFER = [os.environ.get("MRG_WGRAD_DEFER", "1") == "1"]
 _PENDING = {}
+# MRG_SIDE_POOL=P (> 0): each flush of the deferred queue goes to the next of P side streams, forked
+# from its own mark only and joined at the end of the backward (experiment: the graph executor starts
+# a long side chain with several incoming edges late)
+_POOL_N = int(os.environ.get("MRG_SIDE_POOL", "0"))
+_POOL = {}       # device -> [P streams]
+_POOL_USED = {}  # device -> streams used since the last join
+_POOL_NEXT = {}
 
 
 def set_wgrad_defer(on: bool) -> bool:
@@ -428,6 +436,8 @@ def _ensure_join(key, cur, s, task):
         def join(cur=cur, s=s, key=key):
             _flush_deferred(key, cur.device)
             cur.wait_stream(s)
+            for ps in _POOL_USED.pop(key, []):
+                cur.wait_stream(ps)
             reset_fork_point(key)
             _JOIN_PENDING.pop(key, None)
             _SIDE_HOLD.pop(key, None)   # their blocks are reusable now: later work is ordered after the wait
@@ -450,7 +460,18 @@ def _flush_deferred(key, device, cap=0, after=None):
     dev = torch.device(device)
     cur = torch.cuda.current_stream(dev)
     s = _SIDE[key]
-    if after is None:
+    if _POOL_N > 0 and after is not None:
+        pool = _POOL.get(key)
+        if pool is None:
+            pool = _POOL[key] = [torch.cuda.Stream(device=dev) for _ in range(_POOL_N)]
+        n = _POOL_NEXT.get(key, 0)
+        _POOL_NEXT[key] = n + 1
+        s = pool[n % _POOL_N]
+        used = _POOL_USED.setdefault(key, [])
+        if s not in used:
+            used.append(s)
+        s.wait_event(after)
+    elif after is None:
         _fork(key, s, cur)
     else:
         s.wait_event(after)
