@@ -508,15 +508,16 @@ class _EncoderStackFn(Function):
         if l == 0:   # the embedding: dW_emb = sum dx0^T feat (features read time-major through a row map)
             parts.append(lambda: wg(_p(dx0, r0 * H), H, _p(ch.feat, t0 * ch.F), T * ch.F, rows, H, ch.F, emb[0],
                                     x_hi=ch.F, x_div=B, gb=emb[1]))
+        writes = (gw_ih, first, gbh, gw_hh, gw_ff, gb_ff, *emb, *[t for _, gg, gb in lns for t in (gg, gb)])
         if SPLIT_FORKS:   # one fork per product (the round-3 pattern, kept as a capture regression case)
             for f in parts:
-                _on_side(dev, rows, keep, f)
+                _on_side(dev, rows, keep, f, writes=writes)
             return
 
         def issue():
             for f in parts:
                 f()
-        _on_side(dev, rows, keep, issue)
+        _on_side(dev, rows, keep, issue, writes=writes)
 
     @staticmethod
     def _input_grads(chains, need):

@@ -146,7 +146,7 @@ def _hold_if_side(t: torch.Tensor):
     dev = t.device.index or 0
     s = _SIDE.get(dev)
     cur = torch.cuda.current_stream(t.device)
-    if (s is not None and (cur == s or cur in _POOL.get(dev, ())) and dev in _JOIN_PENDING
+    if (s is not None and (cur == s or cur == _REC.get(dev)) and dev in _JOIN_PENDING
             and torch.cuda.is_current_stream_capturing()):
         _SIDE_HOLD.setdefault(dev, []).append(t)
 
@@ -363,13 +363,18 @@ def set_wgrad_stream(on: bool) -> bool:
 # gradient-ready listener (DDP bucket overlap) needs each write issued when it is reported.
 _DEFER = [os.environ.get("MRG_WGRAD_DEFER", "1") == "1"]
 _PENDING = {}
-# MRG_SIDE_POOL=P (> 0): each flush of the deferred queue goes to the next of P side streams, forked
-# from its own mark only and joined at the end of the backward (experiment: the graph executor starts
-# a long side chain with several incoming edges late)
-_POOL_N = int(os.environ.get("MRG_SIDE_POOL", "0"))
-_POOL = {}       # device -> [P streams]
-_POOL_USED = {}  # device -> streams used since the last join
-_POOL_NEXT = {}
+# The queue flushed beside the recurrences runs on a stream of its own (_REC), the rest of the side
+# work (the end-of-backward flush: the products of the layers below the last recurrence) on _SIDE, so
+# that flush starts when its operands are ready instead of behind the recurrence stream's backlog
+# (in-graph wall-clock stamps, tools/side_timing.py: that backlog outlasts the main stream by ~1.7 ms;
+# headline 20.55 -> 20.23 ms, A/B on one box).  Writes into one gradient buffer stay ordered: every
+# queued item names the buffers it writes (_on_side(writes=...)), and a flush on _SIDE whose items
+# touch a buffer the recurrence stream has written in this backward, or name none, waits for it
+# first.  MRG_REC_STREAM=0 keeps everything on _SIDE.
+_REC_ON = [os.environ.get("MRG_REC_STREAM", "1") != "0"]
+_REC = {}          # device -> the recurrence-beside stream
+_REC_USED = {}     # device -> True once it has work in this backward
+_REC_WRITES = {}   # device -> {(ptr, nbytes)} written on it in this backward (None: unknown)
 
 
 def set_wgrad_defer(on: bool) -> bool:
@@ -436,8 +441,9 @@ def _ensure_join(key, cur, s, task):
         def join(cur=cur, s=s, key=key):
             _flush_deferred(key, cur.device)
             cur.wait_stream(s)
-            for ps in _POOL_USED.pop(key, []):
-                cur.wait_stream(ps)
+            if _REC_USED.pop(key, False):
+                cur.wait_stream(_REC[key])
+            _REC_WRITES.pop(key, None)
             reset_fork_point(key)
             _JOIN_PENDING.pop(key, None)
             _SIDE_HOLD.pop(key, None)   # their blocks are reusable now: later work is ordered after the wait
@@ -460,27 +466,31 @@ def _flush_deferred(key, device, cap=0, after=None):
     dev = torch.device(device)
     cur = torch.cuda.current_stream(dev)
     s = _SIDE[key]
-    if _POOL_N > 0 and after is not None:
-        pool = _POOL.get(key)
-        if pool is None:
-            pool = _POOL[key] = [torch.cuda.Stream(device=dev) for _ in range(_POOL_N)]
-        n = _POOL_NEXT.get(key, 0)
-        _POOL_NEXT[key] = n + 1
-        s = pool[n % _POOL_N]
-        used = _POOL_USED.setdefault(key, [])
-        if s not in used:
-            used.append(s)
+    if _REC_ON[0] and after is not None:
+        s = _REC.get(key)
+        if s is None:
+            s = _REC[key] = torch.cuda.Stream(device=dev)
+        _REC_USED[key] = True
+        w = _REC_WRITES.setdefault(key, set())
+        for _, _, _, writes in items:
+            if writes is None or w is None:
+                _REC_WRITES[key] = w = None
+            else:
+                w.update(writes)
         s.wait_event(after)
-    elif after is None:
-        _fork(key, s, cur)
     else:
-        s.wait_event(after)
-        _LAST_FORK[key] = None
+        if _REC_USED.get(key) and _conflicts(items, _REC_WRITES.get(key, set())):
+            s.wait_stream(_REC[key])   # same gradient buffers (or unknown): keep their write order
+        if after is None:
+            _fork(key, s, cur)
+        else:
+            s.wait_event(after)
+            _LAST_FORK[key] = None
     lib = _lib.load()
     prev = lib.mrg_gemm_set_blocks_per_cu(cap) if cap else None
     try:
         with torch.cuda.stream(s):
-            for fn, keep, arith in items:
+            for fn, keep, arith, _ in items:
                 for t in keep:
                     if t is not None:
                         t.record_stream(s)
@@ -521,8 +531,28 @@ def flush_beside_recurrence(device, mark) -> None:
     _flush_deferred(torch.device(device).index or 0, device, cap=1, after=mark)
 
 
-def _on_side(device, rows, keep, fn):
-    """Run fn() (weight-gradient launches) on the side stream now, or queue it (see _DEFER)."""
+def _writes(tensors):
+    """{(data_ptr, nbytes)} of the gradient buffers an item writes (None entries skipped)."""
+    return {(t.data_ptr(), t.numel() * t.element_size()) for t in tensors if t is not None}
+
+
+def _conflicts(items, rec_writes) -> bool:
+    """True when an item of a flush writes a buffer the recurrence stream wrote (or either is unknown)."""
+    if rec_writes is None:
+        return True
+    for _, _, _, writes in items:
+        if writes is None:
+            return True
+        for p, n in writes:
+            for q, m in rec_writes:
+                if p < q + m and q < p + n:
+                    return True
+    return False
+
+
+def _on_side(device, rows, keep, fn, writes=None):
+    """Run fn() (weight-gradient launches) on the side stream now, or queue it (see _DEFER).
+    writes: the gradient tensors fn writes (ordering across the two side streams), None = unknown."""
     if not _defers(device, rows):
         with _side(device, rows, keep):
             fn()
@@ -534,13 +564,16 @@ def _on_side(device, rows, keep, fn):
     if key in _JOIN_PENDING and _JOIN_PENDING[key] != task:
         _flush_deferred(key, dev)
         cur.wait_stream(_SIDE[key])
+        if _REC_USED.pop(key, False):
+            cur.wait_stream(_REC[key])
+        _REC_WRITES.pop(key, None)
         reset_fork_point(key)
         del _JOIN_PENDING[key]
     s = _SIDE.get(key)
     if s is None:
         s = _SIDE[key] = torch.cuda.Stream(device=dev)
     _ensure_join(key, cur, s, task)
-    _PENDING.setdefault(key, []).append((fn, tuple(keep), _ARITH[0]))
+    _PENDING.setdefault(key, []).append((fn, tuple(keep), _ARITH[0], None if writes is None else _writes(writes)))
 
 
 class _side:
@@ -562,12 +595,17 @@ class _side:
             # left over from a backward that did not finish: order after its side-stream work
             _flush_deferred(key, dev)
             cur.wait_stream(s)
+            if _REC_USED.pop(key, False):
+                cur.wait_stream(_REC[key])
+            _REC_WRITES.pop(key, None)
             reset_fork_point(key)
             del _JOIN_PENDING[key]
         if self.rows < _SIDE_MIN_ROWS:
-            if key in _JOIN_PENDING:  # order this write after the side stream's pending ones
+            if key in _JOIN_PENDING:  # order this write after the side streams' pending ones
                 _flush_deferred(key, dev)
                 cur.wait_stream(s)
+                if _REC_USED.get(key):
+                    cur.wait_stream(_REC[key])
                 reset_fork_point(key)
             return self
         if task < 0:  # not inside a backward pass: stay on the current stream
@@ -602,7 +640,7 @@ def _wgrad(dY, ldy, X, ldx, rows, Nout, Nin, gw, device, *, dy_hi=0, dy_div=0, x
         gemm(Nout, Nin, rows, dY, 1, ldy, X, 0, ldx, _ptr(gw), Nin, beta=1.0, a_hi=dy_hi, a_div=dy_div,
              b_hi=x_hi, b_div=x_div, splits=wgrad_splits(Nout, Nin, rows), device=device,
              asum_out=_ptr(gb), asum_out2=_ptr(gb2))
-    _on_side(device, rows, keep, issue)
+    _on_side(device, rows, keep, issue, writes=(gw, gb, gb2))
 
 
 # --- [in][out] weight copies for the input-gradient products.  dX = dY W reads W [out][in] along
@@ -948,7 +986,7 @@ def _resln_bwd(dy2, a2, b2, gamma, beta, mean, rstd):
             _lib.check(lib.mrg_residual_layernorm_param_reduce(
                 rows, E, _ptr(ws), _ptr(gg if gg is not None else scratch[0]),
                 _ptr(gb if gb is not None else scratch[1]), 1, _stream()), "layernorm param reduce")
-        _on_side(dev, rows, (ws,), reduce)
+        _on_side(dev, rows, (ws,), reduce, writes=(gg, gb))
     return g
 
 
@@ -1235,7 +1273,8 @@ class _LSTMFn(Function):
                 t0 = T - 1 if reverse[i] else 0
                 _on_side(dev, B * T, (g, h0),
                          lambda g=g, h0=h0, gw=gw, t0=t0: gemm(4 * H, H, B, _ptr(g, t0 * 4 * H), 1, T * 4 * H,
-                                                               _ptr(h0), 0, H, _ptr(gw), H, beta=1.0, device=dev))
+                                                               _ptr(h0), 0, H, _ptr(gw), H, beta=1.0, device=dev),
+                         writes=(gw,))
             gbi, gbh = _gbuf(b_ih), _gbuf(b_hh)
             first = gbi if gbi is not None else gbh
             second = gbh if gbi is not None else None
@@ -1508,10 +1547,11 @@ class _GRUFn(Function):
             t0 = T - 1 if reverse else 0
             _on_side(dev, B * T, (dGH, h0c),
                      lambda: gemm(H3, H, B, _ptr(dGH, t0 * H3), 1, T * H3, _ptr(h0c), 0, H, _ptr(gw), H, beta=1.0,
-                                  device=dev))
+                                  device=dev), writes=(gw,))
         gbh = _gbuf(b_hh)
         if gbh is not None:
-            _on_side(dev, B * T, (dGH,), lambda: colsum(B * T, H3, _ptr(dGH), H3, _ptr(gbh), device=dev))
+            _on_side(dev, B * T, (dGH,), lambda: colsum(B * T, H3, _ptr(dGH), H3, _ptr(gbh), device=dev),
+                     writes=(gbh,))
         dx = None
         if need[1]:
             dx = torch.empty(B, T, In, device=dev, dtype=torch.float32)

@@ -294,7 +294,7 @@ class _IntegrateFn(Function):
                 Nk = kv2[i].shape[0] * kv2[i].shape[1]
                 wg(_ptr(dKV[i]), 2 * E, _ptr(kv2[i]), E, Nk, 2 * E, E, None if g["in_w"] is None else g["in_w"][E:],
                    None if g["in_b"] is None else g["in_b"][E:])
-        _on_side(dev, N, keep, issue)
+        _on_side(dev, N, keep, issue, writes=(gcw, gcb, *[t for g in per for t in g.values()]))
 
 
 def _bln_fwd(rows, E, eps, items):

@@ -3,7 +3,7 @@ side stream in the replayed headline step, without a profiler attached?  Wall-cl
 (mrg_debug_stamp, 1-thread kernels captured INTO the graph) at the step's start, at each flush's
 fork point on the main stream, before and after every flush on its side stream, at the backward's
 end and the step's end; after a replay their times from the start are printed (ms).  Env as for
-bench.py (MRG_SIDE_POOL, ...).
+bench.py (MRG_REC_STREAM, ...).
 
     python tools/side_timing.py            (GPU box)
 """
@@ -44,9 +44,8 @@ def main():
             return orig_flush(key, device, cap, after)
         ev(f"fork point (main) of a flush of {n}", torch.cuda.current_stream(device))
         orig_flush(key, device, cap, after)
-        used = Fn._POOL_USED.get(key) or [Fn._SIDE[key]]
-        s = used[(Fn._POOL_NEXT.get(key, 1) - 1) % len(used)] if Fn._POOL_N > 0 and after is not None else Fn._SIDE[key]
-        ev(f"  side end of flush of {n}", s)
+        rec = Fn._REC_ON[0] and after is not None
+        ev(f"  {'recurrence' if rec else 'side'}-stream end of flush of {n}", Fn._REC[key] if rec else Fn._SIDE[key])
     Fn._flush_deferred = flush
     mc, oc, me = C.lstmformer_config(ratio=1)
     torch.manual_seed(0)
