@@ -231,121 +231,6 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
   }
 }
 
-// Solo forward with ONE workgroup barrier per step (H = 32 / 64 / 128): a group of KC = NT / H
-// lanes owns ONE hidden unit's four gate rows (i, f, g, o) over a k-slice of KL = H / KC, so after
-// the DPP reduce every lane of the group holds that unit's four pre-activations and lane kc = b runs
-// the cell of batch row b itself: no pre-activation round trip through LDS and no barrier before the
-// cell.  h_t goes to the other half of a double-buffered LDS h (the GEMV of step t reads h_{t-1}
-// from one half while the cells write h_t into the other), so the step's single barrier orders both.
-template <int H>
-struct SoloNT {
-  static constexpr int value = H == 128 ? 1024 : 256;
-  static constexpr int waves_per_simd = value / 256;
-};
-
-template <int H, int BS>
-__global__ __launch_bounds__((SoloNT<H>::value), (SoloNT<H>::waves_per_simd)) void lstm_fwd_solo_kernel(LstmFwdArgs args) {
-  constexpr int NT = SoloNT<H>::value;
-  constexpr int KC = NT / H;   // lanes per unit
-  constexpr int KL = H / KC;   // hidden inputs per lane
-  constexpr int KLP = ((KL / 4) % 2 == 0) ? KL + 4 : KL;  // odd 16-B chunk pitch: conflict-free b128
-  static_assert(KC >= 2 && KC <= 16 && (KL % 4) == 0 && BS <= KC, "bad solo LSTM tiling");
-  __shared__ __attribute__((aligned(16))) float hs[2][BS][KC][KLP];
-
-  const int ngroups = (args.B + BS - 1) / BS;
-  const int prob = blockIdx.x / ngroups, grp = blockIdx.x % ngroups;
-  const LstmFwdProblem& P = args.p[prob];
-  const int B = args.B, T = args.T;
-  const int tid = threadIdx.x;
-  const int u = tid / KC, kc = tid % KC;
-  const int b0 = grp * BS;
-
-  float w[4][KL];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-#pragma unroll
-    for (int i = 0; i < KL; i += 4) {
-      float4 v = *reinterpret_cast<const float4*>(P.w_hh + (long)(q * H + u) * H + kc * KL + i);
-      w[q][i] = v.x; w[q][i + 1] = v.y; w[q][i + 2] = v.z; w[q][i + 3] = v.w;
-    }
-  }
-  // the cell of (batch row kc, unit u)
-  const bool cell = kc < BS;
-  const int bg = b0 + kc;
-  const bool cvalid = cell && bg < B;
-  float c = 0.0f, h = 0.0f;
-  float bh[4] = {0.f, 0.f, 0.f, 0.f};
-  if (cvalid) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) bh[q] = P.b_hh[q * H + u];
-    if (P.c0) c = P.c0[(long)bg * P.c0_bs + u];
-  }
-  for (int e = tid; e < 2 * BS * H; e += NT) {   // h_{-1} into half 0; rows past B stay 0 in both halves
-    const int half = e / (BS * H), r = e % (BS * H), b = r / H, k = r % H;
-    float v = 0.0f;
-    if (half == 0 && P.h0 && b0 + b < B) v = P.h0[(long)(b0 + b) * P.h0_bs + k];
-    hs[half][b][k / KL][k % KL] = v;
-  }
-  float gxv[4] = {0.f, 0.f, 0.f, 0.f};
-  auto load_gx = [&](int t) {
-    if (cvalid) {
-      const float* g = P.gx + (long)bg * P.gx_bs + (long)t * P.gx_ts + u;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) gxv[q] = g[q * H];
-    }
-  };
-  load_gx(P.reverse ? T - 1 : 0);
-  __syncthreads();
-
-  for (int tt = 0; tt < T; ++tt) {
-    const int t = P.reverse ? T - 1 - tt : tt;
-    const int cur = tt & 1;
-    MRG_STAMP(0);
-    float z[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int b = 0; b < BS; ++b) {
-      float acc[4] = {0.f, 0.f, 0.f, 0.f};
-      const float* hp = &hs[cur][b][kc][0];
-#pragma unroll
-      for (int i = 0; i < KL; i += 4) {
-        float4 hv = *reinterpret_cast<const float4*>(hp + i);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          acc[q] = fmaf(w[q][i], hv.x, acc[q]);
-          acc[q] = fmaf(w[q][i + 1], hv.y, acc[q]);
-          acc[q] = fmaf(w[q][i + 2], hv.z, acc[q]);
-          acc[q] = fmaf(w[q][i + 3], hv.w, acc[q]);
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        acc[q] = group_sum<KC>(acc[q]);
-        z[q] = (kc == b) ? acc[q] : z[q];   // lane kc = b keeps batch row b's pre-activations
-      }
-    }
-    MRG_STAMP(2);
-    if (cvalid) {
-      const float ig = sigmoidf_(z[0] + gxv[0] + bh[0]), fg = sigmoidf_(z[1] + gxv[1] + bh[1]);
-      const float gg = tanhf_(z[2] + gxv[2] + bh[2]), og = sigmoidf_(z[3] + gxv[3] + bh[3]);
-      c = fg * c + ig * gg;
-      h = og * tanhf_(c);
-      hs[cur ^ 1][kc][u / KL][u % KL] = h;
-      P.y[(long)bg * P.y_bs + (long)t * P.y_ts + u] = h;
-      float* gs = P.gates + (long)bg * P.g_bs + (long)t * P.g_ts + u;
-      gs[0] = ig; gs[H] = fg; gs[2 * H] = gg; gs[3 * H] = og;
-      P.cs[(long)bg * P.cs_bs + (long)t * P.cs_ts + u] = c;
-      if (tt + 1 < T) load_gx(P.reverse ? t - 1 : t + 1);
-    }
-    MRG_STAMP(4);
-    __syncthreads();
-    MRG_STAMP(6);
-  }
-  if (cvalid) {
-    if (P.hT) P.hT[(long)bg * H + u] = h;
-    if (P.cT) P.cT[(long)bg * H + u] = c;
-  }
-}
-
 template <int H, int G, int BS>
 __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_simd)) void lstm_bwd_kernel(LstmBwdArgs args) {
   constexpr int NT = LstmNT<H, G>::value;
@@ -602,43 +487,10 @@ static bool try_tile(K kernel, int nt, long nblk, int cus, bool last_solo, hipSt
   return true;
 }
 
-// one-barrier solo forward (lstm_fwd_solo_kernel), opt-in MRG_LSTM_SOLO1=1.  Measured (r04,
-// profiles/r04_lstm_solo1.txt, B = 64, T = 300, ns per step at one problem): H = 128 1245 vs 1054 for
-// the two-barrier solo form, H = 64 775 vs 924, H = 32 823 vs 632; C2 12.35 vs 11.95 ms/step.  With
-// one lane in KC running each cell, the cell phase serialises within the wave.
-static int g_solo1 = [] {
-  const char* e = getenv("MRG_LSTM_SOLO1");
-  return (e && atoi(e) == 1) ? 1 : 0;
-}();
-
-template <int H>
-static int launch_fwd_solo1(const LstmFwdArgs& a, int force_bs, int cus, hipStream_t s) {
-  constexpr int NT = SoloNT<H>::value;
-  constexpr int BMAX = H == 128 ? 4 : (NT / H < 8 ? NT / H : 8);   // (H = 128, 8 rows: 51 VGPRs spilled)
-  for (int bs = 1; bs <= BMAX; bs *= 2) {
-    if (force_bs > 0 && bs != force_bs) continue;
-    const long nblk = (long)a.nprob * ((a.B + bs - 1) / bs);
-    const bool last = bs == BMAX || bs == force_bs;
-    bool ok = false;
-    switch (bs) {
-      case 1: ok = try_tile<1>(lstm_fwd_solo_kernel<H, 1>, NT, nblk, cus, last, s, a); break;
-      case 2: ok = try_tile<2>(lstm_fwd_solo_kernel<H, 2>, NT, nblk, cus, last, s, a); break;
-      case 4: if constexpr (NT / H >= 4) ok = try_tile<4>(lstm_fwd_solo_kernel<H, 4>, NT, nblk, cus, last, s, a); break;
-      default: if constexpr (BMAX >= 8) ok = try_tile<8>(lstm_fwd_solo_kernel<H, 8>, NT, nblk, cus, last, s, a); break;
-    }
-    if (ok) return check_launch("lstm_fwd_solo_kernel");
-  }
-  set_error("lstm fwd: no solo tile (nprob=%d B=%d H=%d force_bs=%d)", a.nprob, a.B, H, force_bs);
-  return 4;
-}
-
 template <int H, int G>
 static int launch_fwd(const LstmFwdArgs& a, int force_bs, int cus, hipStream_t s) {
   constexpr int NT = LstmNT<H, G>::value;
   const long groups1 = a.B;
-  if constexpr (G == 1 && H >= 32) {
-    if (g_solo1) return launch_fwd_solo1<H>(a, force_bs, cus, s);
-  }
   if constexpr (H == 256 && G == 8) {
     if (g_mx && force_bs <= 0 && (!a.stamps || g_mx == 2)) {
       const int bs = valu_bs(lstm_fwd_kernel<H, G, 1>, lstm_fwd_kernel<H, G, 2>, lstm_fwd_kernel<H, G, 4>,

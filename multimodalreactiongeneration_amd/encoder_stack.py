@@ -44,10 +44,9 @@ from .functional import _ptr, _stream, gemm, _dx_gemm, _wt_note, _gbuf, _on_side
 # time steps per chunk (the diagonal width); MRG_STACK_CHUNK overrides.  100 since the deferred weight
 # gradients run beside the backward recurrences (longer recurrences leave them more room): A/B on one
 # box 50 / 60 / 75 / 100 / 150 / 300 -> 21.80 / 21.68 / 21.53 / 21.29 / 21.55 / 23.05 ms/step (r03)
-# weight gradients per (layer, chunk) as each chunk's backward completes (1), or per layer once its
-# chunk 0 is done (0, default).  The per-chunk form starts the products diagonals earlier but issues
-# three times as many (smaller) products: measured 22.47 vs 21.15 ms/step (r04, A/B on one box)
-CHUNK_WGRAD = os.environ.get("MRG_STACK_CHUNK_WGRAD", "0") == "1"
+# Weight gradients are issued per layer once its chunk 0 is done.  Per (layer, chunk) as each chunk's
+# backward completed (three times as many, smaller products, starting diagonals earlier) measured
+# 22.47 vs 21.15 ms/step (r04) and 22.14 vs 20.38 (r05, with the recurrence stream): removed.
 # one side-stream fork per weight-gradient product instead of one per layer (a capture regression case:
 # tests/test_gpu_capture.py)
 SPLIT_FORKS = os.environ.get("MRG_STACK_SPLIT_FORKS", "0") == "1"
@@ -452,10 +451,7 @@ class _EncoderStackFn(Function):
                                   _p(gr["g1"], r0 * H)))
                 _bgemm(lib, tlen * B, H, 4 * H, items, 4 * H, H, epi=3, ldaux=H, transposed=True, dev=dev)
             for m, l, c, t0, t1 in probs:
-                if CHUNK_WGRAD:   # this chunk's share now: the products start diagonals earlier
-                    _EncoderStackFn._weight_grads(lib, chains[m], states[m][l], grads[m][l], l, B, H, dev,
-                                                  t0, t1, block_off(chains[m].T, c))
-                elif c == 0:
+                if c == 0:
                     _EncoderStackFn._weight_grads(lib, chains[m], states[m][l], grads[m][l], l, B, H, dev,
                                                   0, chains[m].T, 0)
         return (None,) + tuple(_EncoderStackFn._input_grads(chains, ctx.needs_input_grad))
