@@ -25,6 +25,10 @@ int mrg_gemm_set_glds_wg(int on);
  * gemm_x6w_kernel (gemm_wide.hip: row-owning waves, bn columns per tile, ring depth ns); env
  * MRG_GEMM_WIDE; returns the previous setting.                                                      */
 int mrg_gemm_set_wide(int cfg);
+/* Attention backward form: 1 (default, MRG_ATTN_FUSED) = the single-pass kernel (one workgroup per
+ * (sample, head); D = 64, Tq <= 320, 16-B rows) where it applies, 0 = always the two-pass dQ, dK / dV
+ * kernels; returns the previous setting.                                                           */
+int mrg_attention_set_fused(int on);
 /* Diagnostics: block 0 of gemm_x6r_kernel records per-wave s_memtime stamps into buf ([waves][16] u64: start,
  * B slice resident, each row block's start, end); null disables.  Never in timed runs.              */
 int mrg_gemm_debug_stamps(void* buf);

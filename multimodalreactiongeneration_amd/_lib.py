@@ -35,6 +35,7 @@ SIGNATURES = {
     "mrg_gemm_get_mode": (c_int, []),
     "mrg_gemm_force_tile": (c_int, [c_int]),
     "mrg_gemm_set_blocks_per_cu": (c_int, [c_int]),
+    "mrg_attention_set_fused": (c_int, [c_int]),
     "mrg_gemm_set_glds": (c_int, [c_int, c_int]),
     "mrg_gemm_set_glds_wg": (c_int, [c_int]),
     "mrg_transpose_batched": (c_int, [c_int, PP, PP, PI, PI, P]),

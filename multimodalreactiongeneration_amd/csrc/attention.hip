@@ -630,6 +630,217 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
   }
 }
 
+// Single-pass backward (D = 64, Tq <= 320 queries): ONE workgroup of 8 waves per (b, head) walks the
+// key blocks of 128 keys (wave w keeps keys 16w..16w+15 of the block and their dK / dV accumulators in
+// VGPRs, exactly as attn_bwd_dkv_kernel does) and, inside, the query tiles of 32 that see them; the
+// dS tile of a (key block, query tile) pair goes to LDS and the eight waves turn it into that tile's
+// dQ share at once (dQ += dS K over the block's keys), accumulated in LDS for all Tq queries and
+// written once at the end.  So Q, K, V, O and dO are read from HBM once and dQ, dK, dV written once
+// (the two-pass form reads Q, dO, K and V twice and recomputes S and dP), with no atomics: the dQ
+// shares add in key-block order, deterministic.  delta = rowsum(dO * O) and lse of every query are
+// formed in a prologue (LDS).  dK / dV sum the same products in the same order as the two-pass form
+// (bitwise equal); dQ sums over keys in another order.
+static constexpr int FKB = 128;          // keys per block (8 waves x 16)
+static constexpr int FQT = 32;           // queries per tile
+static constexpr int FTQ = 320;          // most queries per (b, head): the dQ accumulators live in LDS
+static constexpr int FSQ = FKB + 4;      // dS tile row stride
+template <int D>
+struct FusedLds {
+  static constexpr int SA = AttnCfg<D>::SA;
+  static constexpr int QS = 0, DS = QS + FQT * SA, KS = DS + FQT * SA, SS = KS + FKB * SA;
+  static constexpr int QA = SS + FQT * FSQ, LS = QA + FTQ * SA, DL = LS + FTQ;
+  static constexpr int FLOATS = DL + FTQ;
+};
+
+template <int D>
+__global__ __launch_bounds__(512) void attn_bwd_fused_kernel(AttnArgs a) {
+  static_assert(D == 64, "fused attention backward: D = 64 only");
+  using C = AttnCfg<D>;
+  using L = FusedLds<D>;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* Qs = lds + L::QS;    // query tile rows [FQT][SA]
+  float* Ds = lds + L::DS;    // dO tile rows
+  float* Ks = lds + L::KS;    // the key block's K rows [FKB][SA] (dQ product operand)
+  float* Ss = lds + L::SS;    // dS of the pair [FQT query][FSQ key]
+  float* Qa = lds + L::QA;    // dQ accumulators [FTQ][SA]
+  float* Ls = lds + L::LS;    // lse of every query
+  float* Dl = lds + L::DL;    // delta of every query
+  const int h = blockIdx.x, b = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lk = lane & 15, lg = lane >> 4;
+  const int hoff = h * D;
+  const int Tq = a.Tq, Tk = a.Tk;
+  const bool pad = a.qpad && a.kpad;
+  const float* qb_ = a.q + (long)b * a.q_bs + hoff;
+  const float* db_ = a.dout + (long)b * a.do_bs + hoff;
+  const unsigned char* qpb = pad ? a.qpad + (long)b * a.qp_bs : nullptr;
+
+  // prologue: 4 lanes per query (16 consecutive d each: the dQ kernel's lane-group split, so delta
+  // sums in its order), 128 queries per pass
+  for (int q0 = 0; q0 < Tq; q0 += 128) {
+    const int q = q0 + (tid >> 2), g = tid & 3;
+    float dsum = 0.0f;
+    if (q < Tq) {
+      const float* op = a.o + (long)b * a.o_bs + (long)q * a.o_ts + hoff + 16 * g;
+      const float* dp = db_ + (long)q * a.do_ts + 16 * g;
+#pragma unroll
+      for (int i = 0; i < 16; i += 4) {
+        const float4 o4 = *reinterpret_cast<const float4*>(op + i), d4 = *reinterpret_cast<const float4*>(dp + i);
+        dsum = fmaf(d4.x, o4.x, dsum);
+        dsum = fmaf(d4.y, o4.y, dsum);
+        dsum = fmaf(d4.z, o4.z, dsum);
+        dsum = fmaf(d4.w, o4.w, dsum);
+      }
+    }
+    dsum += __shfl_xor(dsum, 1, 64);
+    dsum += __shfl_xor(dsum, 2, 64);
+    if (q < Tq && g == 0) {
+      Dl[q] = dsum;
+      Ls[q] = a.lse[stat_row(a, b, h, q)];
+    }
+  }
+  for (int i = tid; i < FTQ * C::SA / 4; i += 512)
+    reinterpret_cast<float4*>(Qa)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+
+  const int trow = tid >> 4, tcol = (tid & 15) * 4;   // this thread's float4 of a query tile
+  for (int kb0 = 0; kb0 < Tk; kb0 += FKB) {
+    const int kj = kb0 + wave * 16 + lk;
+    const bool kv = kj < Tk;
+    const bool wact = kb0 + wave * 16 < Tk;            // the wave holds some key
+    const bool kp = pad && kv && a.kpad[(long)b * Tk + kj];
+    const int qmin = query_start(a, kj);
+    const int wq0 = query_start(a, min(kb0 + wave * 16, Tk - 1));
+    float kreg[C::KS], vreg[C::KS];
+    row_values<D>(a.k + (long)b * a.k_bs + (long)min(kj, Tk - 1) * a.k_ts + hoff, lg, kv, kreg);
+    row_values<D>(a.v + (long)b * a.v_bs + (long)min(kj, Tk - 1) * a.v_ts + hoff, lg, kv, vreg);
+    f32x4 dkT[C::DT], dvT[C::DT];
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt) {
+      dkT[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dvT[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    __syncthreads();   // the previous block's dQ products are done with Ks
+#pragma unroll
+    for (int i = 0; i < FKB * (D / 4) / 512; ++i) {
+      const int e = tid + i * 512, row = e >> 4, c = (e & 15) * 4;
+      float4 v4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (kb0 + row < Tk) v4 = *reinterpret_cast<const float4*>(a.k + (long)b * a.k_bs + (long)(kb0 + row) * a.k_ts + hoff + c);
+      *reinterpret_cast<float4*>(Ks + row * C::SA + c) = v4;
+    }
+    const int qs = (query_start(a, kb0) / 16) * 16;
+    float4 rq = make_float4(0.f, 0.f, 0.f, 0.f), rd = rq;
+    unsigned char qpn = 0;
+    if (qs < Tq) {
+      if (qs + trow < Tq) {
+        rq = *reinterpret_cast<const float4*>(qb_ + (long)(qs + trow) * a.q_ts + tcol);
+        rd = *reinterpret_cast<const float4*>(db_ + (long)(qs + trow) * a.do_ts + tcol);
+      }
+      qpn = (pad && lane < FQT && qs + lane < Tq) ? qpb[qs + lane] : 0;
+    }
+    for (int qt0 = qs; qt0 < Tq; qt0 += FQT) {
+      __syncthreads();   // the previous tile's dS / dQ product is done
+      *reinterpret_cast<float4*>(Qs + trow * C::SA + tcol) = rq;
+      *reinterpret_cast<float4*>(Ds + trow * C::SA + tcol) = rd;
+      const unsigned long long qbits = __ballot(qpn != 0);
+      const unsigned long long kmask = kp ? qbits : 0ull;   // queries of this tile padding hides from key kj
+      __syncthreads();
+      if (qt0 + FQT < Tq) {
+        const int nq = qt0 + FQT + trow;
+        rq = rd = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (nq < Tq) {
+          rq = *reinterpret_cast<const float4*>(qb_ + (long)nq * a.q_ts + tcol);
+          rd = *reinterpret_cast<const float4*>(db_ + (long)nq * a.do_ts + tcol);
+        }
+        qpn = (pad && lane < FQT && qt0 + FQT + lane < Tq) ? qpb[qt0 + FQT + lane] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < FQT / 16; ++u) {
+        const int qb = qt0 + u * 16;
+        float ds[4] = {0.f, 0.f, 0.f, 0.f};
+        if (wact && qb < Tq && qb + 16 > wq0) {   // wave-uniform: some query of the sub-tile sees a key of the wave
+          f32x4 s4 = f32x4{0.f, 0.f, 0.f, 0.f}, dp4 = s4;
+          {
+            float qq[C::KS], dd[C::KS];
+            row_operands<D, C::SA>(Qs, u * 16 + lk, lg, qq);
+            row_operands<D, C::SA>(Ds, u * 16 + lk, lg, dd);
+#pragma unroll
+            for (int s = 0; s < C::KS; ++s) {
+              s4 = __builtin_amdgcn_mfma_f32_16x16x4f32(qq[s], kreg[s], s4, 0, 0, 0);
+              dp4 = __builtin_amdgcn_mfma_f32_16x16x4f32(dd[s], vreg[s], dp4, 0, 0, 0);
+            }
+          }
+          const int ql = u * 16 + lg * 4;   // tile-local query of accumulator register 0
+          const float4 L4 = *reinterpret_cast<const float4*>(Ls + qt0 + ql);
+          const float4 D4 = *reinterpret_cast<const float4*>(Dl + qt0 + ql);
+          const float lv[4] = {L4.x, L4.y, L4.z, L4.w}, dv[4] = {D4.x, D4.y, D4.z, D4.w};
+          float p[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int qq = qt0 + ql + r;
+            const bool vis = kv && qq >= qmin && qq < Tq && !((kmask >> (ql + r)) & 1ull);
+            const float e = __expf(s4[r] * a.scale - lv[r]);
+            p[r] = vis ? e : 0.0f;
+            ds[r] = p[r] * (dp4[r] - dv[r]);
+          }
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            float dd[C::DT], qq[C::DT];
+            col_operands<D, C::SA>(Ds, u * 16 + 4 * lg + s, lk, dd);
+            col_operands<D, C::SA>(Qs, u * 16 + 4 * lg + s, lk, qq);
+#pragma unroll
+            for (int dt = 0; dt < C::DT; ++dt) {
+              dvT[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(dd[dt], p[s], dvT[dt], 0, 0, 0);
+              dkT[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(qq[dt], ds[s], dkT[dt], 0, 0, 0);
+            }
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Ss[(u * 16 + lg * 4 + r) * FSQ + wave * 16 + lk] = ds[r];
+      }
+      __syncthreads();
+      // dQ share of the tile: wave w -> queries 16 (w >> 2).., d tile (w & 3); C[d][q] = K^T dS^T over the
+      // keys any of those queries sees (k-step 4m + i of lane group lg: key 16m + 4lg + i)
+      {
+        const int qu = wave >> 2, dtl = wave & 3;
+        const int qr0 = qt0 + qu * 16;
+        if (qr0 < Tq) {
+          const int kend = min(key_bound(a, min(qr0 + 15, Tq - 1)) - kb0, FKB);
+          const int nm = (kend + 15) / 16;
+          f32x4 c0 = f32x4{0.f, 0.f, 0.f, 0.f}, c1 = c0;
+          const float* srow = Ss + (qu * 16 + lk) * FSQ + 4 * lg;
+          const float* kcol = Ks + 4 * lg * C::SA + dtl * 16 + lk;
+          for (int m = 0; m < nm; ++m) {
+            const float4 sv = *reinterpret_cast<const float4*>(srow + 16 * m);
+            const float* kc = kcol + 16 * m * C::SA;
+            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(kc[0], sv.x, c0, 0, 0, 0);
+            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(kc[C::SA], sv.y, c1, 0, 0, 0);
+            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(kc[2 * C::SA], sv.z, c0, 0, 0, 0);
+            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(kc[3 * C::SA], sv.w, c1, 0, 0, 0);
+          }
+          if (nm > 0) {
+            float4* qa = reinterpret_cast<float4*>(Qa + (qr0 + lk) * C::SA + dtl * 16 + 4 * lg);
+            const float4 o = *qa;
+            *qa = make_float4(o.x + (c0[0] + c1[0]), o.y + (c0[1] + c1[1]), o.z + (c0[2] + c1[2]),
+                              o.w + (c0[3] + c1[3]));
+          }
+        }
+      }
+    }
+    if (kv) {
+      store_row<D>(a.dk + (long)b * a.dk_bs + (long)kj * a.dk_ts + hoff, lg, 1, dkT, a.scale);
+      store_row<D>(a.dv + (long)b * a.dv_bs + (long)kj * a.dv_ts + hoff, lg, 1, dvT, 1.0f);
+    }
+  }
+  __syncthreads();
+  float* dqb = a.dq + (long)b * a.dq_bs + hoff;
+  for (int e = tid; e < Tq * (D / 4); e += 512) {
+    const int q = e >> 4, c = (e & 15) * 4;
+    const float4 v4 = *reinterpret_cast<const float4*>(Qa + q * C::SA + c);
+    *reinterpret_cast<float4*>(dqb + (long)q * a.dq_ts + c) =
+        make_float4(v4.x * a.scale, v4.y * a.scale, v4.z * a.scale, v4.w * a.scale);
+  }
+}
+
 }  // namespace mrg
 
 using namespace mrg;
@@ -646,6 +857,19 @@ static AttnArgs attn_base(int B, int Hh, int Tq, int Tk, const float* q, long q_
   a.causal = causal; a.scale = scale;
   a.q_off = 0; a.Tqf = Tq; a.qp_bs = Tq; a.kv_acc = 0; a.st_ld = Tq; a.st_off = 0;
   return a;
+}
+
+// single-pass backward (attn_bwd_fused_kernel) where it applies: 1 (default) or 0 (MRG_ATTN_FUSED,
+// mrg_attention_set_fused: the two-pass form always)
+static int g_attn_fused = [] {
+  const char* e = getenv("MRG_ATTN_FUSED");
+  return e ? atoi(e) : 1;
+}();
+
+MRG_API int mrg_attention_set_fused(int on) {
+  const int prev = g_attn_fused;
+  g_attn_fused = on ? 1 : 0;
+  return prev;
 }
 
 static bool rows16(const float* p, long bs, long ts) {
@@ -709,6 +933,17 @@ MRG_API int mrg_attention_bwd(int B, int Hh, int Tq, int Tk, int D,
   a.qvec = 1;  // required above
   a.ovec = rows16(o, o_bs, o_ts);
   a.dkvvec = rows16(dk, dk_bs, dk_ts) && rows16(dv, dv_bs, dv_ts);
+  if (g_attn_fused && D == 64 && Tq <= FTQ && rows16(o, o_bs, o_ts) && a.dkvvec && rows16(dq, dq_bs, dq_ts)) {
+    static bool attr = false;
+    constexpr int bytes = FusedLds<64>::FLOATS * (int)sizeof(float);
+    if (!attr) {
+      MRG_HIP(hipFuncSetAttribute((const void*)attn_bwd_fused_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  bytes));
+      attr = true;
+    }
+    klaunch(attn_bwd_fused_kernel<64>, dim3(Hh, B), 512, bytes, stream, a);
+    return check_launch("attn_bwd_fused_kernel");
+  }
   dim3 gq(Hh, B, (Tq + 63) / 64);
   MRG_ATTN_DISPATCH(attn_bwd_dq_kernel, gq, a);  // also writes delta = rowsum(dO * O) to the workspace
   if (check_launch("attn_bwd_dq_kernel")) return 1;

@@ -319,16 +319,20 @@ __global__ __launch_bounds__(256) void resln_param_reduce_kernel(float* part, in
   const int c = cb * 64 + lane;
   const int E2 = 2 * E;
   const int r0 = (int)((long)nblk * g / R), r1 = (int)((long)nblk * (g + 1) / R);
-  float s0 = 0.0f, s1 = 0.0f;
+  // wave w sums rows r0 + w + 4j: eight independent loads in flight per round of 32 rows
+  float s = 0.0f;
   if (c < E2) {
-    int i = r0 + wave;
-    for (; i + 4 < r1; i += 8) {
-      s0 += part[(long)i * E2 + c];
-      s1 += part[(long)(i + 4) * E2 + c];
+    for (int i0 = r0 + wave; i0 < r1; i0 += 32) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = i0 + 4 * j;
+        v[j] = i < r1 ? part[(long)i * E2 + c] : 0.0f;
+      }
+      s += ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
     }
-    if (i < r1) s0 += part[(long)i * E2 + c];
   }
-  red[wave][lane] = s0 + s1;
+  red[wave][lane] = s;
   __syncthreads();
   const float v = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
   if (R > 1) {
@@ -340,22 +344,31 @@ __global__ __launch_bounds__(256) void resln_param_reduce_kernel(float* part, in
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const unsigned old = __hip_atomic_fetch_add(tick + cb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int last = old == (unsigned)(R - 1);
-      if (last) {
-        __hip_atomic_store(tick + cb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
+      if (last) __hip_atomic_store(tick + cb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       last_flag = last;
     }
     __syncthreads();
     if (!last_flag) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // every wave reads the other groups' rows
+    // the group sums (each group's first row), wave w taking groups w + 4j, four loads in flight
+    float t = 0.0f;
+    if (c < E2) {
+      for (int q0 = wave; q0 < R; q0 += 16) {
+        float u[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int q = q0 + 4 * j;
+          u[j] = q < R ? part[(long)((long)nblk * q / R) * E2 + c] : 0.0f;
+        }
+        t += (u[0] + u[1]) + (u[2] + u[3]);
+      }
+    }
+    __syncthreads();   // every wave has read red[] above
+    red[wave][lane] = t;
+    __syncthreads();
   }
   if (wave == 0 && c < E2) {
-    float t = v;
-    if (R > 1) {
-      t = 0.0f;
-      for (int q = 0; q < R; ++q) t += part[(long)((long)nblk * q / R) * E2 + c];
-    }
+    const float t = R > 1 ? (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]) : v;
     float* out = c < E ? dgamma + c : dbeta + (c - E);
     *out = accumulate ? *out + t : t;
   }
@@ -758,8 +771,8 @@ MRG_API int mrg_residual_layernorm_param_reduce(int rows, int E, float* workspac
   MRG_REQUIRE(E >= 1 && E <= 1024 && dgamma && dbeta && workspace,
               "mrg_residual_layernorm_param_reduce: bad arguments (E=%d)", E);
   const int nblk = (rows + RESLN_RPB - 1) / RESLN_RPB;
-  // row groups of >= 16 partial rows (distinct first rows), at most 16
-  const int R = nblk >= 32 ? (nblk / 16 < 16 ? nblk / 16 : 16) : 1;
+  // row groups of ~32 partial rows (one round of loads per wave; distinct first rows), at most 64
+  const int R = nblk >= 64 ? ((nblk + 31) / 32 < 64 ? (nblk + 31) / 32 : 64) : 1;
   unsigned* tick = nullptr;
   if (R > 1 && resln_tickets(stream, &tick)) return 1;
   // the partials are consumed in place (each row group's sum overwrites its first row)

@@ -412,11 +412,12 @@ def test_residual_layernorm_vs_torch(E):
     assert rel_err(gd.grad, gr.grad) < TOL and rel_err(btd.grad, btr.grad) < TOL
 
 
-@pytest.mark.parametrize("rows,E", [(5000, 256), (19200, 256), (19200, 1000), (70, 256)])
+@pytest.mark.parametrize("rows,E", [(5000, 256), (19200, 256), (19200, 1000), (70, 256), (150000, 64)])
 def test_layernorm_param_reduce_row_groups(rows, E):
-    """dgamma / dbeta through the 2-D ticketed parameter reduce: ragged row groups (5000 rows: 157
-    partial blocks in 9 groups), the benchmark's 19,200 rows (16 groups), E = 1000 (16 column blocks,
-    partial last) and a single group; twice in a row (the tickets return to 0), vs torch float64."""
+    """dgamma / dbeta through the 2-D ticketed parameter reduce: ragged row groups (5000 rows), the
+    benchmark's 19,200 rows, E = 1000 (16 column blocks, partial last), a single group, and enough
+    partial blocks that the 64 groups take several rounds of loads each; twice in a row (the tickets
+    return to 0), vs torch float64."""
     from multimodalreactiongeneration_amd import functional as Fn
     g = torch.Generator().manual_seed(rows + E)
     a, b = torch.randn(rows, E, generator=g), torch.randn(rows, E, generator=g)
@@ -1443,7 +1444,11 @@ def test_attention_query_chunks_match_whole(Tq, Tk, causal, cuts):
                                  Tq * E, E, _ptr(lse), _ptr(qpad), _ptr(kpad), int(causal), sc, _stream()) == 0
     dq, dk, dv = torch.empty(B, Tq, E, **f), torch.empty(B, Tk, E, **f), torch.empty(B, Tk, E, **f)
     ws = torch.empty(B * Hh * Tq, **f)
-    assert lib.mrg_attention_bwd(B, Hh, Tq, Tk, D, *bwd_args(q, o, lse, do, dq, dk, dv), _ptr(ws), _stream()) == 0
+    prev = lib.mrg_attention_set_fused(0)   # the chunk forms are the two-pass kernels: compare like with like
+    try:
+        assert lib.mrg_attention_bwd(B, Hh, Tq, Tk, D, *bwd_args(q, o, lse, do, dq, dk, dv), _ptr(ws), _stream()) == 0
+    finally:
+        lib.mrg_attention_set_fused(prev)
     oc, dqc, dqs = torch.full_like(o, 7.0), torch.full_like(dq, 7.0), torch.full_like(dq, 7.0)
     dkc, dvc = torch.zeros_like(dk), torch.zeros_like(dv)
     dks, dvs = torch.full_like(dk, 7.0), torch.full_like(dv, 7.0)
@@ -1469,3 +1474,72 @@ def test_attention_query_chunks_match_whole(Tq, Tk, causal, cuts):
     assert torch.equal(oc, o) and torch.equal(dqc, dq) and torch.equal(dqs, dq)
     assert torch.equal(dks, dk) and torch.equal(dvs, dv)
     assert rel_err(dkc, dk) < 1e-5 and rel_err(dvc, dv) < 1e-5
+
+
+@pytest.mark.parametrize("B,Tq,Tk,causal,ragged", [(64, 300, 300, True, True), (3, 300, 2400, True, True),
+                                                   (3, 37, 74, True, False), (2, 320, 320, False, True),
+                                                   (3, 40, 20, True, True), (3, 100, 100, False, False),
+                                                   (2, 321, 321, True, True)])
+def test_attention_single_pass_backward_matches_two_pass(B, Tq, Tk, causal, ragged):
+    """attn_bwd_fused_kernel (one workgroup per (sample, head), dQ shares accumulated in LDS) against the
+    two-pass dQ, dK / dV kernels on the same forward: dK and dV bitwise (same products, same order,
+    same delta), dQ within fp32 reordering, and dQ against a float64 reference on two samples.
+    Tq = 321 is past the single-pass limit (the two-pass form runs: bitwise)."""
+    from multimodalreactiongeneration_amd import _lib
+    from multimodalreactiongeneration_amd.functional import _ptr, _stream
+    lib = _lib.load()
+    Hh, D = 4, 64
+    E = Hh * D
+    g = torch.Generator().manual_seed(Tq * 5 + Tk)
+    q, do = torch.randn(B, Tq, E, generator=g), torch.randn(B, Tq, E, generator=g)
+    kv = torch.randn(B, Tk, 2 * E, generator=g)
+    qpad = torch.zeros(B, Tq, dtype=torch.uint8)
+    kpad = torch.zeros(B, Tk, dtype=torch.uint8)
+    if ragged:
+        for b in range(1, B):
+            qpad[b, Tq - (b * 37) % (Tq // 2 + 1) - 1:] = 1
+            kpad[b, Tk - (b * 53) % (Tk // 2 + 1) - 1:] = 1
+    q, do, kv, qpad, kpad = (t.to(DEV) for t in (q, do, kv, qpad, kpad))
+    f = dict(device=DEV, dtype=torch.float32)
+    sc = 1.0 / math.sqrt(D)
+    o, lse = torch.empty(B, Tq, E, **f), torch.empty(B, Hh, Tq, **f)
+    assert lib.mrg_attention_fwd(B, Hh, Tq, Tk, D, _ptr(q), Tq * E, E, _ptr(kv), Tk * 2 * E, 2 * E, _ptr(kv, E),
+                                 Tk * 2 * E, 2 * E, _ptr(o), Tq * E, E, _ptr(lse), _ptr(qpad), _ptr(kpad), int(causal),
+                                 sc, _stream()) == 0
+    outs = {}
+    for fused in (1, 0):
+        dq, dkv = torch.full((B, Tq, E), 7.0, **f), torch.full((B, Tk, 2 * E), 7.0, **f)
+        ws = torch.empty(B * Hh * Tq, **f)
+        prev = lib.mrg_attention_set_fused(fused)
+        try:
+            assert lib.mrg_attention_bwd(
+                B, Hh, Tq, Tk, D, _ptr(q), Tq * E, E, _ptr(kv), Tk * 2 * E, 2 * E, _ptr(kv, E), Tk * 2 * E, 2 * E,
+                _ptr(o), Tq * E, E, _ptr(lse), _ptr(qpad), _ptr(kpad), int(causal), sc, _ptr(do), Tq * E, E,
+                _ptr(dq), Tq * E, E, _ptr(dkv), Tk * 2 * E, 2 * E, _ptr(dkv, E), Tk * 2 * E, 2 * E, _ptr(ws),
+                _stream()) == 0
+        finally:
+            lib.mrg_attention_set_fused(prev)
+        torch.cuda.synchronize()
+        outs[fused] = (dq, dkv)
+    (dq1, dkv1), (dq0, dkv0) = outs[1], outs[0]
+    assert torch.equal(dkv1, dkv0)
+    if Tq > 320:
+        assert torch.equal(dq1, dq0)
+    else:
+        assert rel_err(dq1, dq0) < 1e-5
+    # float64 reference of dQ on two samples (the reference's mask rules: block-causal, AND padding)
+    for b in (0, B - 1):
+        qq = q[b].double().view(Tq, Hh, D).transpose(0, 1).requires_grad_(True)
+        kk = kv[b, :, :E].double().view(Tk, Hh, D).transpose(0, 1)
+        vv = kv[b, :, E:].double().view(Tk, Hh, D).transpose(0, 1)
+        i, j = torch.arange(Tq, device=DEV)[:, None], torch.arange(Tk, device=DEV)[None, :]
+        vis = torch.ones(Tq, Tk, dtype=torch.bool, device=DEV)
+        if causal:
+            vis = (j < (i + 1) * (Tk // Tq)) if Tk >= Tq else (j <= i // (Tq // Tk))
+        vis = vis & ~(qpad[b].bool()[:, None] & kpad[b].bool()[None, :])
+        s = (qq @ kk.transpose(1, 2)) * sc
+        s = s.masked_fill(~vis, float("-inf"))
+        oo = torch.softmax(s, -1) @ vv
+        oo.backward(do[b].double().view(Tq, Hh, D).transpose(0, 1))
+        ref = qq.grad.transpose(0, 1).reshape(Tq, E)
+        assert rel_err(dq1[b], ref) < 1e-4
