@@ -694,9 +694,9 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(AttnArgs a) {
     }
     dsum += __shfl_xor(dsum, 1, 64);
     dsum += __shfl_xor(dsum, 2, 64);
-    if (q < Tq && g == 0) {
-      Dl[q] = dsum;
-      Ls[q] = a.lse[stat_row(a, b, h, q)];
+    if (q < FTQ && g == 0) {   // zeros past Tq: the last sub-tile's rows beyond it read them (p = 0 there)
+      Dl[q] = q < Tq ? dsum : 0.0f;
+      Ls[q] = q < Tq ? a.lse[stat_row(a, b, h, q)] : 0.0f;
     }
   }
   for (int i = tid; i < FTQ * C::SA / 4; i += 512)
