@@ -372,7 +372,6 @@ _PENDING = {}
 # touch a buffer the recurrence stream has written in this backward, or name none, waits for it
 # first.  MRG_REC_STREAM=0 keeps everything on _SIDE.
 _REC_ON = [os.environ.get("MRG_REC_STREAM", "1") != "0"]
-_REC_CAP = [int(os.environ.get("MRG_REC_CAP", "1"))]   # GEMM workgroups per CU beside a recurrence (0: no cap)
 _REC = {}          # device -> the recurrence-beside stream
 _REC_USED = {}     # device -> True once it has work in this backward
 _REC_WRITES = {}   # device -> {(ptr, nbytes)} written on it in this backward (None: unknown)
@@ -529,7 +528,7 @@ def flush_beside_recurrence(device, mark, rec=True) -> None:
     the backward and the executor places them where the main stream leaves room."""
     if mark is None:
         return
-    _flush_deferred(torch.device(device).index or 0, device, cap=_REC_CAP[0] if rec else 0, after=mark, rec=rec)
+    _flush_deferred(torch.device(device).index or 0, device, cap=1 if rec else 0, after=mark, rec=rec)
 
 
 def _writes(tensors):
