@@ -75,35 +75,6 @@ struct SsdPersistArgs {
     if (a.stamps && blockIdx.x == 0 && threadIdx.x == 0) a.stamps[(long)t * 8 + (ph)] = wall_clock64(); \
   } while (0)
 
-// Wave roles (one vmcnt per wave counts loads and stores in issue order, so a wave's own memory traffic
-// sits in front of its next hand-off poll): waves 2-3 poll the gathers and issue nothing else to
-// memory before them (their next frame's P rows are loaded right after the frame's last gather); waves
-// 0-1 run the cells (publish first), the sampling select and every saved output (member 0's X / U /
-// statistics copied out of LDS by wave 1).
-// rows x n granules of a tile (row r at ring + r * ld) -> dst[r * LDK + k], by waves 2-3 in rounds of 16
-template <int LDK>
-__device__ __forceinline__ void ssdp_gather(unsigned long long* ring, int ld, int rows, int n, unsigned tag,
-                                            float* dst, int* err, bool& dead) {
-  const int gt = threadIdx.x - 128;
-  if (gt < 0 || dead) return;
-  const int total = rows * n;
-  for (int base = 0; base < total; base += 128 * 16) {
-    int idx[16];
-    float gv[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int e = min(base + gt + i * 128, total - 1);
-      idx[i] = (e / n) * ld + e % n;
-    }
-    get_granules_idx<16>(ring, idx, tag, gv, err, dead);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int e = base + gt + i * 128;
-      if (e < total) dst[(e / n) * LDK + e % n] = gv[i];
-    }
-  }
-}
-
 __device__ __forceinline__ float4 ssdp_ld4(const float* p, long idx, bool ok) {
   return ok ? *reinterpret_cast<const float4*>(p + idx) : make_float4(0.f, 0.f, 0.f, 0.f);
 }
@@ -132,7 +103,6 @@ __global__ __launch_bounds__(256, 2) void ssd_fwd_persist_kernel(SsdPersistArgs 
   __shared__ __attribute__((aligned(16))) float w1s[4][HMAX];        // this member's FFN rows (<= 4)
   __shared__ float4 wms[8][GL];                                      // W_ms^T (LDS: registers are short)
   __shared__ float4 lnp[MAXL][2][GL];                                // every LayerNorm's gamma / beta
-  __shared__ float stt[2][SSDP_R];                                   // a stage's LayerNorm statistics
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int H = a.H, H4 = H / 4, B = a.B, T = a.T, nl = a.nl, HB = a.HB, FO = a.FO;
   const int G = H / 4;                                     // members per row tile
@@ -225,13 +195,28 @@ __global__ __launch_bounds__(256, 2) void ssd_fwd_persist_kernel(SsdPersistArgs 
     {
       const bool fed = t > 0;
       const int tm = t > 0 ? t - 1 : 0;
-      if (fed)   // z(t-1) of the tile's rows from every member's FFN columns
-        ssdp_gather<65>(a.ring_z + ((long)(tm & 1) * B + r0) * HB, HB, min(SSDP_R, B - r0), HB, (unsigned)t,
-                        &zs[0][0], a.err, dead);
+      if (fed && !dead) {   // z(t-1) of the tile's rows from every member's FFN columns
+        constexpr int NZ = (SSDP_R * 64 + 255) / 256;
+        int idx[NZ];
+        float gv[NZ];
+        const int nvalid = min(SSDP_R, B - r0) * HB;
+#pragma unroll
+        for (int i = 0; i < NZ; ++i) idx[i] = min(tid + i * 256, nvalid - 1);
+        unsigned long long* rz = a.ring_z + ((long)(tm & 1) * B + r0) * HB;
+        get_granules_idx<NZ>(rz, idx, (unsigned)t, gv, a.err, dead);
+#pragma unroll
+        for (int i = 0; i < NZ; ++i) {
+          const int e = tid + i * 256;
+          if (e < SSDP_R * 64) {
+            const int r = e / HB, jj = e % HB;
+            if (e < nvalid) zs[r][jj] = gv[i];
+          }
+        }
+      }
       SSDP_STAMP(1);
       const float msv = msv_next;
       const bool sel = fed && sel_next;
-      if (t + 1 < T && tid < 128) {   // for frame t + 1: ms[.][t] and mask[t] (waves 0-1)
+      if (t + 1 < T) {   // for frame t + 1: ms[.][t] and mask[t]
         msv_next = svalid ? a.ms[(long)bs_ * a.ms_bs + (long)t * a.ms_ts + os_] : 0.0f;
         sel_next = a.mask[t] != 0;
       }
@@ -264,13 +249,34 @@ __global__ __launch_bounds__(256, 2) void ssd_fwd_persist_kernel(SsdPersistArgs 
           xv[i].z = fmaf(mo, w.z, xv[i].z); xv[i].w = fmaf(mo, w.w, xv[i].w);
         }
       }
+      if (t + 1 < T) {   // next frame's P rows, off the chain
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+          const int rr = (tid + i * 256) / GL, b = r0 + rr;
+          pv[i] = ssdp_ld4(a.p, (long)(t + 1) * B * H + (long)b * H + 4 * c4, rr < SSDP_R && b < B && cv);
+        }
+      }
     }
     for (int l = 0; l < nl; ++l) {
       const SsdPersistLayer& L = a.L[l];
       if (l > 0) {
         // gather h of layer l-1 (all H units of the tile's rows), then X = LayerNorm(h + x)
-        ssdp_gather<LDK>(a.ring_h + (((long)(l - 1) * 2 + par) * B + r0) * H, H, min(SSDP_R, B - r0), H,
-                         (unsigned)(t + 1), Xs, a.err, dead);
+        const SsdPersistLayer& P = a.L[l - 1];
+        if (!dead) {
+          constexpr int NGH = SSDP_R * HMAX / 256;
+          int idx[NGH];
+          float gv[NGH];
+          const int nvalid = min(SSDP_R, B - r0) * H;
+#pragma unroll
+          for (int i = 0; i < NGH; ++i) idx[i] = min(tid + i * 256, nvalid - 1);
+          unsigned long long* rh = a.ring_h + (((long)(l - 1) * 2 + par) * B + r0) * H;
+          get_granules_idx<NGH>(rh, idx, (unsigned)(t + 1), gv, a.err, dead);
+#pragma unroll
+          for (int i = 0; i < NGH; ++i) {
+            const int e = tid + i * 256;
+            if (e < nvalid) Xs[(e / H) * LDK + e % H] = gv[i];
+          }
+        }
         SSDP_STAMP(3);
         __syncthreads();
         const float4 g = lnp[l - 1][0][c4], bt = lnp[l - 1][1][c4];
@@ -306,37 +312,24 @@ __global__ __launch_bounds__(256, 2) void ssd_fwd_persist_kernel(SsdPersistArgs 
           const float rs = rsqrtf(qv[i] / (float)H + a.eps);
           xv[i].x = (xv[i].x - s[i]) * rs * g.x + bt.x; xv[i].y = (xv[i].y - s[i]) * rs * g.y + bt.y;
           xv[i].z = (xv[i].z - s[i]) * rs * g.z + bt.z; xv[i].w = (xv[i].w - s[i]) * rs * g.w + bt.w;
-          const int rr = (tid + i * 256) / GL;
-          if (c4 == 0 && rr < SSDP_R) {
-            stt[0][rr] = s[i];
-            stt[1][rr] = rs;
+          const int rr = (tid + i * 256) / GL, b = r0 + rr;
+          if (j == 0 && c4 == 0 && rr < SSDP_R && b < B) {
+            P.mean[(long)t * B + b] = s[i];
+            P.rstd[(long)t * B + b] = rs;
           }
         }
       }
       // ---- the layer input tile -> LDS (member 0 saves it)
 #pragma unroll
       for (int i = 0; i < NX; ++i) {
-        const int rr = (tid + i * 256) / GL;
+        const int rr = (tid + i * 256) / GL, b = r0 + rr;
         if (rr >= SSDP_R) continue;
         float2* xd = reinterpret_cast<float2*>(&Xs[rr * LDK + 4 * c4]);
         xd[0] = make_float2(xv[i].x, xv[i].y);
         xd[1] = make_float2(xv[i].z, xv[i].w);
+        if (j == 0 && b < B && cv) *reinterpret_cast<float4*>(L.x + (long)t * B * H + (long)b * H + 4 * c4) = xv[i];
       }
       __syncthreads();
-      if (j == 0 && wave == 1) {   // member 0 saves the layer input (and the statistics of the layer below)
-        for (int e = lane; e < SSDP_R * H4; e += 64) {
-          const int rr = e / H4, cc = e % H4, b = r0 + rr;
-          if (b < B) {
-            const float2* xp = reinterpret_cast<const float2*>(&Xs[rr * LDK + 4 * cc]);
-            const float2 x0 = xp[0], x1 = xp[1];
-            *reinterpret_cast<float4*>(L.x + (long)t * B * H + (long)b * H + 4 * cc) = make_float4(x0.x, x0.y, x1.x, x1.y);
-          }
-        }
-        if (l > 0 && lane < SSDP_R && r0 + lane < B) {
-          a.L[l - 1].mean[(long)t * B + r0 + lane] = stt[0][lane];
-          a.L[l - 1].rstd[(long)t * B + r0 + lane] = stt[1][lane];
-        }
-      }
       if (l == 0) SSDP_STAMP(2);
       // ---- 16 x 16 gate tile over this wave's quarter of K (decode.hip's order)
       const int l16 = lane & 15, kg = lane >> 4;
@@ -375,13 +368,19 @@ __global__ __launch_bounds__(256, 2) void ssd_fwd_persist_kernel(SsdPersistArgs 
     // ================= last LayerNorm + the FFN's first Linear and ReLU: z columns of this member
     {
       const SsdPersistLayer& P = a.L[nl - 1];
-      ssdp_gather<LDK>(a.ring_h + (((long)(nl - 1) * 2 + par) * B + r0) * H, H, min(SSDP_R, B - r0), H,
-                       (unsigned)(t + 1), Xs, a.err, dead);
-      if (t + 1 < T) {   // next frame's P rows (waves 2-3: after their last gather of this frame)
+      if (!dead) {
+        constexpr int NGH = SSDP_R * HMAX / 256;
+        int idx[NGH];
+        float gv[NGH];
+        const int nvalid = min(SSDP_R, B - r0) * H;
 #pragma unroll
-        for (int i = 0; i < NX; ++i) {
-          const int rr = (tid + i * 256) / GL, b = r0 + rr;
-          pv[i] = ssdp_ld4(a.p, (long)(t + 1) * B * H + (long)b * H + 4 * c4, rr < SSDP_R && b < B && cv);
+        for (int i = 0; i < NGH; ++i) idx[i] = min(tid + i * 256, nvalid - 1);
+        unsigned long long* rh = a.ring_h + (((long)(nl - 1) * 2 + par) * B + r0) * H;
+        get_granules_idx<NGH>(rh, idx, (unsigned)(t + 1), gv, a.err, dead);
+#pragma unroll
+        for (int i = 0; i < NGH; ++i) {
+          const int e = tid + i * 256;
+          if (e < nvalid) Xs[(e / H) * LDK + e % H] = gv[i];
         }
       }
       SSDP_STAMP(4);
@@ -418,7 +417,7 @@ __global__ __launch_bounds__(256, 2) void ssd_fwd_persist_kernel(SsdPersistArgs 
       __syncthreads();   // every wave is done reading the gathered h in Xs
 #pragma unroll
       for (int i = 0; i < NX; ++i) {
-        const int rr = (tid + i * 256) / GL;
+        const int rr = (tid + i * 256) / GL, b = r0 + rr;
         if (rr >= SSDP_R) continue;
         const float rs = rsqrtf(qv[i] / (float)H + a.eps);
         float4 uv;
@@ -427,26 +426,15 @@ __global__ __launch_bounds__(256, 2) void ssd_fwd_persist_kernel(SsdPersistArgs 
         float2* ud = reinterpret_cast<float2*>(&Xs[rr * LDK + 4 * c4]);
         ud[0] = make_float2(uv.x, uv.y);
         ud[1] = make_float2(uv.z, uv.w);
-        if (c4 == 0) {
-          stt[0][rr] = s[i];
-          stt[1][rr] = rs;
+        if (j == 0 && b < B) {
+          if (cv) *reinterpret_cast<float4*>(a.u + (long)t * B * H + (long)b * H + 4 * c4) = uv;
+          if (c4 == 0) {
+            P.mean[(long)t * B + b] = s[i];
+            P.rstd[(long)t * B + b] = rs;
+          }
         }
       }
       __syncthreads();
-      if (j == 0 && wave == 1) {   // member 0 saves u and the last LayerNorm's statistics
-        for (int e = lane; e < SSDP_R * H4; e += 64) {
-          const int rr = e / H4, cc = e % H4, b = r0 + rr;
-          if (b < B) {
-            const float2* xp = reinterpret_cast<const float2*>(&Xs[rr * LDK + 4 * cc]);
-            const float2 x0 = xp[0], x1 = xp[1];
-            *reinterpret_cast<float4*>(a.u + (long)t * B * H + (long)b * H + 4 * cc) = make_float4(x0.x, x0.y, x1.x, x1.y);
-          }
-        }
-        if (lane < SSDP_R && r0 + lane < B) {
-          P.mean[(long)t * B + r0 + lane] = stt[0][lane];
-          P.rstd[(long)t * B + r0 + lane] = stt[1][lane];
-        }
-      }
       // z[r][jj] = relu(u[r] . W1[jj] + b1[jj]): 4 lanes (k phases) per (output, row), decode.hip's order
       if (fzi < nz) {
         float acc = 0.0f;

@@ -55,9 +55,6 @@ CHUNK = int(os.environ.get("MRG_STACK_CHUNK", "100"))
 # (8 workgroups of 16 rows per problem, one per CU: 8 problems at B = 64 on 256 CUs; a wider launch
 # falls back to the VALU form at batch tiles of 16, measured 3x slower per step)
 MAXP = int(os.environ.get("MRG_STACK_MAXP", "0"))
-# the last TAIL_SIDE diagonals of the backward flush their queued weight gradients onto the side stream
-# (uncapped, beside the recurrence stream's backlog) instead of the recurrence stream
-TAIL_SIDE = int(os.environ.get("MRG_TAIL_SIDE", "0"))
 
 
 def _maxp(B, dev):
@@ -136,10 +133,8 @@ def _launch_fwd(lib, items, B, Tc, H, dev, pool=None):
     _lib.check(rc, "lstm fwd (encoder stack)")
 
 
-def _launch_bwd(lib, items, B, Tc, H, dev, pool=None, rec=True):
-    """One persistent backward launch over `items` = [(chain, state, grads, t0, dhT, dcT, dh0, dc0)];
-    rec=False: the weight-gradient products queued before it go to the side stream, not the
-    recurrence stream (TAIL_SIDE)."""
+def _launch_bwd(lib, items, B, Tc, H, dev, pool=None):
+    """One persistent backward launch over `items` = [(chain, state, grads, t0, dhT, dcT, dh0, dc0)]."""
     n = len(items)
     xb = pool.take(n) if pool is not None else \
         Fn.zeros(n, lib.mrg_lstm_bwd_xbuf_bytes(B, H) // 8, dtype=torch.int64, device=dev)
@@ -164,7 +159,7 @@ def _launch_bwd(lib, items, B, Tc, H, dev, pool=None, rec=True):
                               A(CI, rev), A(VP, [_p(xb[i]) for i in range(n)]), (CL * (8 * n))(*lay),
                               _ptr(Fn._err_flag(dev)), _lib.cu_count(dev.index or 0), 0, _stream())
     _lib.check(rc, "lstm bwd (encoder stack)")
-    Fn.flush_beside_recurrence(dev, mark, rec=rec)
+    Fn.flush_beside_recurrence(dev, mark)
 
 
 _BMAX = 16   # problems per batched GEMM / LayerNorm launch (mrg_gemm_x6g_batched, mrg_residual_layernorm_*_batched)
@@ -412,7 +407,7 @@ class _EncoderStackFn(Function):
         del diags
 
         pool = _RingPool(sum(len(p) for p in rdiag), lib.mrg_lstm_bwd_xbuf_bytes(B, H) // 8, dev)
-        for ri, probs in enumerate(rdiag):
+        for probs in rdiag:
             bg = _bgroups(probs)
             for tlen, grp in bg:   # LN2, FeedForward, LN1 backward of the chunks (batched launches)
                 n = tlen * B
@@ -447,7 +442,7 @@ class _EncoderStackFn(Function):
                     (ch, states[m][l], grads[m][l], t0, dh_in, dc_in, dh_out, dc_out))
             for tlen, grp in items.items():
                 for part in _split(grp, _maxp(B, dev)):
-                    _launch_bwd(lib, part, B, tlen, H, dev, pool, rec=ri < len(rdiag) - TAIL_SIDE)
+                    _launch_bwd(lib, part, B, tlen, H, dev, pool)
             for tlen, grp in bg:   # input gradients of the chunks: dG W_ih + g1 (residual), batched
                 items = []
                 for m, l, c, t0, t1 in grp:

@@ -456,7 +456,7 @@ def _defers(device, rows) -> bool:
             and torch._C._current_graph_task_id() >= 0)
 
 
-def _flush_deferred(key, device, cap=0, after=None, rec=True):
+def _flush_deferred(key, device, cap=0, after=None):
     """Issue the queued weight-gradient products on the side stream (GEMM grids capped at `cap`
     blocks per CU while they run beside a recurrence), ordered after event `after` when given, else
     after the current stream's work so far."""
@@ -466,7 +466,7 @@ def _flush_deferred(key, device, cap=0, after=None, rec=True):
     dev = torch.device(device)
     cur = torch.cuda.current_stream(dev)
     s = _SIDE[key]
-    if _REC_ON[0] and rec and after is not None:
+    if _REC_ON[0] and after is not None:
         s = _REC.get(key)
         if s is None:
             s = _REC[key] = torch.cuda.Stream(device=dev)
@@ -518,7 +518,7 @@ def fork_beside_recurrence(device):
     return 1, mark
 
 
-def flush_beside_recurrence(device, mark, rec=True) -> None:
+def flush_beside_recurrence(device, mark) -> None:
     """Called right after the recurrence launch: issues the queued weight-gradient products on the side
     stream, ordered after `mark` (the work before the recurrence) but not after the recurrence.
     Measured (r03, headline step, graph replay): issued BEFORE the recurrence launch the products were
@@ -528,7 +528,7 @@ def flush_beside_recurrence(device, mark, rec=True) -> None:
     the backward and the executor places them where the main stream leaves room."""
     if mark is None:
         return
-    _flush_deferred(torch.device(device).index or 0, device, cap=1 if rec else 0, after=mark, rec=rec)
+    _flush_deferred(torch.device(device).index or 0, device, cap=1, after=mark)
 
 
 def _writes(tensors):

@@ -38,13 +38,13 @@ def main():
     BUF.append(torch.zeros(4096, dtype=torch.int64, device=dev))
     orig_flush = Fn._flush_deferred
 
-    def flush(key, device, cap=0, after=None, rec=True):
+    def flush(key, device, cap=0, after=None):
         n = len(Fn._PENDING.get(key, []))
         if n == 0:
-            return orig_flush(key, device, cap, after, rec)
+            return orig_flush(key, device, cap, after)
         ev(f"fork point (main) of a flush of {n}", torch.cuda.current_stream(device))
-        orig_flush(key, device, cap, after, rec)
-        rec = Fn._REC_ON[0] and rec and after is not None
+        orig_flush(key, device, cap, after)
+        rec = Fn._REC_ON[0] and after is not None
         ev(f"  {'recurrence' if rec else 'side'}-stream end of flush of {n}", Fn._REC[key] if rec else Fn._SIDE[key])
     Fn._flush_deferred = flush
     mc, oc, me = C.lstmformer_config(ratio=1)
