@@ -632,22 +632,22 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
 
 // Single-pass backward (D = 64, Tq <= 320 queries): ONE workgroup of 8 waves per (b, head) walks the
 // key blocks of 128 keys (wave w keeps keys 16w..16w+15 of the block and their dK / dV accumulators in
-// VGPRs, exactly as attn_bwd_dkv_kernel does) and, inside, the query tiles of 32 that see them; the
+// VGPRs, exactly as attn_bwd_dkv_kernel does) and, inside, the query tiles of 64 that see them; the
 // dS tile of a (key block, query tile) pair goes to LDS and the eight waves turn it into that tile's
-// dQ share at once (dQ += dS K over the block's keys), accumulated in LDS for all Tq queries and
-// written once at the end.  So Q, K, V, O and dO are read from HBM once and dQ, dK, dV written once
-// (the two-pass form reads Q, dO, K and V twice and recomputes S and dP), with no atomics: the dQ
-// shares add in key-block order, deterministic.  delta = rowsum(dO * O) and lse of every query are
-// formed in a prologue (LDS).  dK / dV sum the same products in the same order as the two-pass form
-// (bitwise equal); dQ sums over keys in another order.
+// dQ share at once (dQ += dS K over the block's keys; wave w holds the block's K columns of its d tile
+// in VGPRs), accumulated in LDS for all Tq queries and written once at the end.  So Q, K, V, O and dO
+// are read from HBM once and dQ, dK, dV written once (the two-pass form reads Q, dO, K and V twice and
+// recomputes S and dP), with no atomics: the dQ shares add in key-block order, deterministic.
+// delta = rowsum(dO * O) and lse of every query are formed in a prologue (LDS).  dK / dV sum the same
+// products in the same order as the two-pass form (bitwise equal); dQ sums over keys in another order.
 static constexpr int FKB = 128;          // keys per block (8 waves x 16)
-static constexpr int FQT = 32;           // queries per tile
+static constexpr int FQT = 64;           // queries per tile
 static constexpr int FTQ = 320;          // most queries per (b, head): the dQ accumulators live in LDS
 static constexpr int FSQ = FKB + 4;      // dS tile row stride
 template <int D>
 struct FusedLds {
   static constexpr int SA = AttnCfg<D>::SA;
-  static constexpr int QS = 0, DS = QS + FQT * SA, KS = DS + FQT * SA, SS = KS + FKB * SA;
+  static constexpr int QS = 0, DS = QS + FQT * SA, SS = DS + FQT * SA;
   static constexpr int QA = SS + FQT * FSQ, LS = QA + FTQ * SA, DL = LS + FTQ;
   static constexpr int FLOATS = DL + FTQ;
 };
@@ -657,10 +657,10 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(AttnArgs a) {
   static_assert(D == 64, "fused attention backward: D = 64 only");
   using C = AttnCfg<D>;
   using L = FusedLds<D>;
+  constexpr int NT = FQT * (D / 4) / 512;   // float4 of a query tile per thread
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* Qs = lds + L::QS;    // query tile rows [FQT][SA]
   float* Ds = lds + L::DS;    // dO tile rows
-  float* Ks = lds + L::KS;    // the key block's K rows [FKB][SA] (dQ product operand)
   float* Ss = lds + L::SS;    // dS of the pair [FQT query][FSQ key]
   float* Qa = lds + L::QA;    // dQ accumulators [FTQ][SA]
   float* Ls = lds + L::LS;    // lse of every query
@@ -673,6 +673,7 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(AttnArgs a) {
   const bool pad = a.qpad && a.kpad;
   const float* qb_ = a.q + (long)b * a.q_bs + hoff;
   const float* db_ = a.dout + (long)b * a.do_bs + hoff;
+  const float* kb_ = a.k + (long)b * a.k_bs + hoff;
   const unsigned char* qpb = pad ? a.qpad + (long)b * a.qp_bs : nullptr;
 
   // prologue: 4 lanes per query (16 consecutive d each: the dQ kernel's lane-group split, so delta
@@ -702,7 +703,7 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(AttnArgs a) {
   for (int i = tid; i < FTQ * C::SA / 4; i += 512)
     reinterpret_cast<float4*>(Qa)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
 
-  const int trow = tid >> 4, tcol = (tid & 15) * 4;   // this thread's float4 of a query tile
+  const int dtl = wave & 3;   // this wave's d tile of the dQ products
   for (int kb0 = 0; kb0 < Tk; kb0 += FKB) {
     const int kj = kb0 + wave * 16 + lk;
     const bool kv = kj < Tk;
@@ -711,47 +712,58 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(AttnArgs a) {
     const int qmin = query_start(a, kj);
     const int wq0 = query_start(a, min(kb0 + wave * 16, Tk - 1));
     float kreg[C::KS], vreg[C::KS];
-    row_values<D>(a.k + (long)b * a.k_bs + (long)min(kj, Tk - 1) * a.k_ts + hoff, lg, kv, kreg);
+    row_values<D>(kb_ + (long)min(kj, Tk - 1) * a.k_ts, lg, kv, kreg);
     row_values<D>(a.v + (long)b * a.v_bs + (long)min(kj, Tk - 1) * a.v_ts + hoff, lg, kv, vreg);
+    // the dQ products' K operand: K[kb0 + 16m + 4lg + i][16 dtl + lk], m < 8, i < 4
+    float kd[FKB / 4];
+#pragma unroll
+    for (int m = 0; m < FKB / 16; ++m)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = kb0 + 16 * m + 4 * lg + i;
+        kd[4 * m + i] = key < Tk ? kb_[(long)key * a.k_ts + 16 * dtl + lk] : 0.0f;
+      }
     f32x4 dkT[C::DT], dvT[C::DT];
 #pragma unroll
     for (int dt = 0; dt < C::DT; ++dt) {
       dkT[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
       dvT[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    __syncthreads();   // the previous block's dQ products are done with Ks
-#pragma unroll
-    for (int i = 0; i < FKB * (D / 4) / 512; ++i) {
-      const int e = tid + i * 512, row = e >> 4, c = (e & 15) * 4;
-      float4 v4 = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (kb0 + row < Tk) v4 = *reinterpret_cast<const float4*>(a.k + (long)b * a.k_bs + (long)(kb0 + row) * a.k_ts + hoff + c);
-      *reinterpret_cast<float4*>(Ks + row * C::SA + c) = v4;
-    }
     const int qs = (query_start(a, kb0) / 16) * 16;
-    float4 rq = make_float4(0.f, 0.f, 0.f, 0.f), rd = rq;
+    float4 rq[NT], rd[NT];
     unsigned char qpn = 0;
-    if (qs < Tq) {
-      if (qs + trow < Tq) {
-        rq = *reinterpret_cast<const float4*>(qb_ + (long)(qs + trow) * a.q_ts + tcol);
-        rd = *reinterpret_cast<const float4*>(db_ + (long)(qs + trow) * a.do_ts + tcol);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int e = tid + 512 * j, q = qs + (e >> 4), c = (e & 15) * 4;
+      rq[j] = rd[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (q < Tq) {
+        rq[j] = *reinterpret_cast<const float4*>(qb_ + (long)q * a.q_ts + c);
+        rd[j] = *reinterpret_cast<const float4*>(db_ + (long)q * a.do_ts + c);
       }
-      qpn = (pad && lane < FQT && qs + lane < Tq) ? qpb[qs + lane] : 0;
     }
+    qpn = (pad && qs + lane < Tq) ? qpb[qs + lane] : 0;
     for (int qt0 = qs; qt0 < Tq; qt0 += FQT) {
-      __syncthreads();   // the previous tile's dS / dQ product is done
-      *reinterpret_cast<float4*>(Qs + trow * C::SA + tcol) = rq;
-      *reinterpret_cast<float4*>(Ds + trow * C::SA + tcol) = rd;
+      __syncthreads();   // the previous tile's dS / dQ products are done
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int e = tid + 512 * j, row = e >> 4, c = (e & 15) * 4;
+        *reinterpret_cast<float4*>(Qs + row * C::SA + c) = rq[j];
+        *reinterpret_cast<float4*>(Ds + row * C::SA + c) = rd[j];
+      }
       const unsigned long long qbits = __ballot(qpn != 0);
       const unsigned long long kmask = kp ? qbits : 0ull;   // queries of this tile padding hides from key kj
       __syncthreads();
       if (qt0 + FQT < Tq) {
-        const int nq = qt0 + FQT + trow;
-        rq = rd = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (nq < Tq) {
-          rq = *reinterpret_cast<const float4*>(qb_ + (long)nq * a.q_ts + tcol);
-          rd = *reinterpret_cast<const float4*>(db_ + (long)nq * a.do_ts + tcol);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const int e = tid + 512 * j, q = qt0 + FQT + (e >> 4), c = (e & 15) * 4;
+          rq[j] = rd[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (q < Tq) {
+            rq[j] = *reinterpret_cast<const float4*>(qb_ + (long)q * a.q_ts + c);
+            rd[j] = *reinterpret_cast<const float4*>(db_ + (long)q * a.do_ts + c);
+          }
         }
-        qpn = (pad && lane < FQT && qt0 + FQT + lane < Tq) ? qpb[qt0 + FQT + lane] : 0;
+        qpn = (pad && qt0 + FQT + lane < Tq) ? qpb[qt0 + FQT + lane] : 0;
       }
 #pragma unroll
       for (int u = 0; u < FQT / 16; ++u) {
@@ -798,24 +810,27 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(AttnArgs a) {
         for (int r = 0; r < 4; ++r) Ss[(u * 16 + lg * 4 + r) * FSQ + wave * 16 + lk] = ds[r];
       }
       __syncthreads();
-      // dQ share of the tile: wave w -> queries 16 (w >> 2).., d tile (w & 3); C[d][q] = K^T dS^T over the
-      // keys any of those queries sees (k-step 4m + i of lane group lg: key 16m + 4lg + i)
-      {
-        const int qu = wave >> 2, dtl = wave & 3;
+      // dQ shares of the tile: wave w -> d tile w & 3 of query sub-tiles (w >> 2) and (w >> 2) + 2;
+      // C[d][q] = K^T dS^T over the keys any of the sub-tile's queries sees (k-step 4m + i of lane
+      // group lg: key 16m + 4lg + i)
+#pragma unroll
+      for (int hq = 0; hq < 2; ++hq) {
+        const int qu = (wave >> 2) + 2 * hq;
         const int qr0 = qt0 + qu * 16;
         if (qr0 < Tq) {
           const int kend = min(key_bound(a, min(qr0 + 15, Tq - 1)) - kb0, FKB);
           const int nm = (kend + 15) / 16;
           f32x4 c0 = f32x4{0.f, 0.f, 0.f, 0.f}, c1 = c0;
           const float* srow = Ss + (qu * 16 + lk) * FSQ + 4 * lg;
-          const float* kcol = Ks + 4 * lg * C::SA + dtl * 16 + lk;
-          for (int m = 0; m < nm; ++m) {
-            const float4 sv = *reinterpret_cast<const float4*>(srow + 16 * m);
-            const float* kc = kcol + 16 * m * C::SA;
-            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(kc[0], sv.x, c0, 0, 0, 0);
-            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(kc[C::SA], sv.y, c1, 0, 0, 0);
-            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(kc[2 * C::SA], sv.z, c0, 0, 0, 0);
-            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(kc[3 * C::SA], sv.w, c1, 0, 0, 0);
+#pragma unroll
+          for (int m = 0; m < FKB / 16; ++m) {
+            if (m < nm) {
+              const float4 sv = *reinterpret_cast<const float4*>(srow + 16 * m);
+              c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(kd[4 * m], sv.x, c0, 0, 0, 0);
+              c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(kd[4 * m + 1], sv.y, c1, 0, 0, 0);
+              c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(kd[4 * m + 2], sv.z, c0, 0, 0, 0);
+              c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(kd[4 * m + 3], sv.w, c1, 0, 0, 0);
+            }
           }
           if (nm > 0) {
             float4* qa = reinterpret_cast<float4*>(Qa + (qr0 + lk) * C::SA + dtl * 16 + 4 * lg);

@@ -18,6 +18,7 @@ from multimodalreactiongeneration_amd import _lib  # noqa: E402
 from multimodalreactiongeneration_amd.functional import visible_pairs  # noqa: E402
 
 B, H, T, D = 64, 4, 300, 64
+TK = int(os.environ.get("TK", str(T)))   # keys (TK = 8 T: the reference-rate audio; no float64 check then)
 E = H * D
 PEAK = 157.3
 
@@ -31,49 +32,52 @@ def main():
     dev = "cuda:0"
     g = torch.Generator(device="cpu").manual_seed(0)
     Q = torch.randn(B, T, E, generator=g).to(dev)
-    KV = torch.randn(B, T, 2 * E, generator=g).to(dev)
+    KV = torch.randn(B, TK, 2 * E, generator=g).to(dev)
     dO = torch.randn(B, T, E, generator=g).to(dev)
     lens = torch.randint(T // 2, T + 1, (B,), generator=g)
     lens[0] = T
     pad = (torch.arange(T)[None, :] >= lens[:, None]).to(torch.uint8).to(dev)
+    kpad = (torch.arange(TK)[None, :] >= (lens * (TK // T))[:, None]).to(torch.uint8).to(dev)
     O = torch.empty(B, T, E, device=dev)
     lse = torch.empty(B, H, T, device=dev)
     dQ = torch.empty(B, T, E, device=dev)
-    dKV = torch.empty(B, T, 2 * E, device=dev)
+    dKV = torch.empty(B, TK, 2 * E, device=dev)
     ws = torch.empty(B * H * T, device=dev)
     scale = D ** -0.5
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
     def fwd():
-        rc = lib.mrg_attention_fwd(B, H, T, T, D, ptr(Q), T * E, E, ptr(KV), T * 2 * E, 2 * E, ptr(KV, E),
-                                   T * 2 * E, 2 * E, ptr(O), T * E, E, ptr(lse), ptr(pad), ptr(pad), 1,
+        rc = lib.mrg_attention_fwd(B, H, T, TK, D, ptr(Q), T * E, E, ptr(KV), TK * 2 * E, 2 * E, ptr(KV, E),
+                                   TK * 2 * E, 2 * E, ptr(O), T * E, E, ptr(lse), ptr(pad), ptr(kpad), 1,
                                    ctypes.c_float(scale), stream)
         assert rc == 0
 
     def bwd():
-        rc = lib.mrg_attention_bwd(B, H, T, T, D, ptr(Q), T * E, E, ptr(KV), T * 2 * E, 2 * E, ptr(KV, E),
-                                   T * 2 * E, 2 * E, ptr(O), T * E, E, ptr(lse), ptr(pad), ptr(pad), 1,
+        rc = lib.mrg_attention_bwd(B, H, T, TK, D, ptr(Q), T * E, E, ptr(KV), TK * 2 * E, 2 * E, ptr(KV, E),
+                                   TK * 2 * E, 2 * E, ptr(O), T * E, E, ptr(lse), ptr(pad), ptr(kpad), 1,
                                    ctypes.c_float(scale), ptr(dO), T * E, E, ptr(dQ), T * E, E, ptr(dKV),
-                                   T * 2 * E, 2 * E, ptr(dKV, E), T * 2 * E, 2 * E, ptr(ws), stream)
+                                   TK * 2 * E, 2 * E, ptr(dKV, E), TK * 2 * E, 2 * E, ptr(ws), stream)
         assert rc == 0
 
     # float64 reference on the first 4 samples (the reference's mask: causal, AND-padding)
     nb = 4
-    q = Q[:nb].double().view(nb, T, H, D).transpose(1, 2).requires_grad_()
-    k = KV[:nb, :, :E].double().reshape(nb, T, H, D).transpose(1, 2).requires_grad_()
-    v = KV[:nb, :, E:].double().reshape(nb, T, H, D).transpose(1, 2).requires_grad_()
-    causal = torch.arange(T, device=dev)[None, :] > torch.arange(T, device=dev)[:, None]
-    pm = pad[:nb].bool()
-    mask = causal[None] | (pm[:, :, None] & pm[:, None, :])
-    s = (q @ k.transpose(-1, -2)) * scale
-    s = s.masked_fill(mask[:, None], float("-inf"))
-    o = torch.softmax(s, -1) @ v
-    o.backward(dO[:nb].double().view(nb, T, H, D).transpose(1, 2))
-    ref = [q.grad.transpose(1, 2).reshape(nb, T, E), k.grad.transpose(1, 2).reshape(nb, T, E),
-           v.grad.transpose(1, 2).reshape(nb, T, E)]
-    ok_rows = ~torch.isnan(o.detach().transpose(1, 2).reshape(nb, T, E)).any(-1)
+    ref, ok_rows = [], None
+    if TK == T:
+        q = Q[:nb].double().view(nb, T, H, D).transpose(1, 2).requires_grad_()
+        k = KV[:nb, :, :E].double().reshape(nb, T, H, D).transpose(1, 2).requires_grad_()
+        v = KV[:nb, :, E:].double().reshape(nb, T, H, D).transpose(1, 2).requires_grad_()
+        causal = torch.arange(T, device=dev)[None, :] > torch.arange(T, device=dev)[:, None]
+        pm = pad[:nb].bool()
+        mask = causal[None] | (pm[:, :, None] & pm[:, None, :])
+        s = (q @ k.transpose(-1, -2)) * scale
+        s = s.masked_fill(mask[:, None], float("-inf"))
+        o = torch.softmax(s, -1) @ v
+        o.backward(dO[:nb].double().view(nb, T, H, D).transpose(1, 2))
+        ref = [q.grad.transpose(1, 2).reshape(nb, T, E), k.grad.transpose(1, 2).reshape(nb, T, E),
+               v.grad.transpose(1, 2).reshape(nb, T, E)]
+        ok_rows = ~torch.isnan(o.detach().transpose(1, 2).reshape(nb, T, E)).any(-1)
 
-    pairs = B * H * visible_pairs(T, T, True)
+    pairs = B * H * visible_pairs(T, TK, True)
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 1
     for var in range(reps):
         fwd()
@@ -83,8 +87,8 @@ def main():
         if var == 0:
             first = (dQ.clone(), dKV.clone())
         same = torch.equal(first[0], dQ) and torch.equal(first[1], dKV)
-        errs = []
-        for gt, rt in zip(got, ref):
+        errs = [float("nan")] * 3 if TK != T else []
+        for gt, rt in zip(got, ref if TK == T else []):
             m = ok_rows[..., None].expand_as(rt)
             errs.append(((gt - rt).abs()[m].max() / rt.abs()[m].max()).item())
         res = {}
