@@ -44,7 +44,7 @@ FAMILIES = {
     "lstm_bwd": "lstm_bwd_kernel<H,G,BS> (VALU) + lstm_bwd_mx_kernel (MFMA, H=256): persistent reverse "
                 "recurrence, 8H^2 FLOP per (b, t) per layer and direction",
     "attn_fwd": "attn_fwd_kernel<64>: block-causal flash attention, 4D FLOP per visible (q, k) pair per head",
-    "attn_bwd": "attn_bwd_dq_kernel<64> + attn_bwd_dkv_kernel<64>: 10D FLOP per visible pair per head",
+    "attn_bwd": "attn_bwd_fused_kernel<64> (single pass; two-pass dq + dkv where it does not apply): 10D FLOP per visible pair per head",
     "gru_fwd": "gru_fwd_kernel<H,G> (gru_rec.hip, persistent GRU recurrence, config_gru.yaml): 6H^2 FLOP per (b, t) per layer",
     "gru_bwd": "gru_bwd_kernel<H,G> (gru_rec.hip, persistent reverse GRU recurrence): 6H^2 FLOP per (b, t) per layer",
 }
