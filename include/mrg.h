@@ -296,7 +296,10 @@ int mrg_lstm_step_fwd(int B, int H, int In, const float* x, const float* h0, con
  * from indices: causal != 0 selects the block-causal rectangular mask;
  * qpad/kpad (uint8 [B,Tq]/[B,Tk], nullable) give the padding AND rule.
  * Element (b, t, head, d) lives at base + b*bs + t*ts + head*D + d.
- * lse: [B, heads, Tq] log-sum-exp saved for the backward.  D in {8,16,32,64}. */
+ * lse: [B, heads, Tq] log-sum-exp saved for the backward.  D in {8,16,32,64}.
+ * Backward: deterministic (no atomics).  D = 64 with Tq <= 320 and 16-B rows everywhere runs a single
+ * pass (one workgroup per (sample, head); the workspace is then unused); other shapes run a dQ pass
+ * (delta = rowsum(dO * O) into the workspace) and a dK / dV pass. */
 int mrg_attention_fwd(int B, int heads, int Tq, int Tk, int D,
                       const float* q, long q_bs, long q_ts, const float* k, long k_bs, long k_ts,
                       const float* v, long v_bs, long v_ts, float* o, long o_bs, long o_ts,
