@@ -949,12 +949,14 @@ MRG_API int mrg_attention_bwd(int B, int Hh, int Tq, int Tk, int D,
   a.ovec = rows16(o, o_bs, o_ts);
   a.dkvvec = rows16(dk, dk_bs, dk_ts) && rows16(dv, dv_bs, dv_ts);
   if (g_attn_fused && D == 64 && Tq <= FTQ && rows16(o, o_bs, o_ts) && a.dkvvec && rows16(dq, dq_bs, dq_ts)) {
-    static bool attr = false;
+    static bool attr[64] = {};   // the LDS size attribute, set once per device
     constexpr int bytes = FusedLds<64>::FLOATS * (int)sizeof(float);
-    if (!attr) {
+    int dev = 0;
+    MRG_HIP(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64 || !attr[dev]) {
       MRG_HIP(hipFuncSetAttribute((const void*)attn_bwd_fused_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   bytes));
-      attr = true;
+      if (dev >= 0 && dev < 64) attr[dev] = true;
     }
     klaunch(attn_bwd_fused_kernel<64>, dim3(Hh, B), 512, bytes, stream, a);
     return check_launch("attn_bwd_fused_kernel");
