@@ -261,25 +261,6 @@ int mrg_ssd_ln_cell_bwd(int B, int H, const float* du, const float* h, const flo
                         const float* mean, const float* rstd, float* g, const float* gates, const float* c,
                         float* dG, int FM, const float* vt, const float* wms_t, float* dyx, hipStream_t stream);
 int mrg_ssd_dx(int B, int H, const float* dG, const float* w_t, const float* g, float* dx, hipStream_t stream);
-/* The forward's whole frame loop in ONE persistent launch (decode_persist.hip; opt-in in decode.py,
- * MRG_SSD_PERSIST=1): per frame every layer of mrg_ssd_feat_gate_cell_fwd / mrg_ssd_gate_cell_fwd and
- * mrg_ssd_ffn_z_fwd, with the same outputs over all T frames, time-major ([T][B][...]; y[b * y_bs + t *
- * FO + o] for t < T - 1 and xf_ms[t * B * F + b * F + o]; the last frame's y by mrg_ssd_y_fwd).  Layer
- * arrays of nl <= 4 (nl <= 2 at H > 128): w_ih [4H, H], b_ih, b_hh, the layer's LayerNorm ln_w / ln_b,
- * outputs x, gates, c, h, and mean / rstd of that LayerNorm.  rings: mrg_ssd_persist_ring_bytes of
- * zeroed device memory per launch; err: the recurrences' error flag (a hand-off spin that times out
- * sets it).  mrg_ssd_persist_fits: 1 when every workgroup of the launch can be resident on `cus` CUs
- * (a persistent launch must not be started otherwise).                                             */
-long mrg_ssd_persist_ring_bytes(int B, int H, int HB, int nl);
-int mrg_ssd_persist_fits(int B, int H, int cus);
-int mrg_ssd_fwd_persist(int B, int H, int HB, int FO, int F, int T, int nl, float eps, const float* p,
-                        const float* ms, long ms_bs, long ms_ts, const unsigned char* mask, const float* wms_t,
-                        const float* w1, const float* b1, const float* w2, const float* b2,
-                        const float* const* w_ih, const float* const* b_ih, const float* const* b_hh,
-                        const float* const* ln_w, const float* const* ln_b, float* const* x, float* const* gates,
-                        float* const* c, float* const* h, float* const* mean, float* const* rstd, float* u,
-                        float* z, float* y, long y_bs, float* xf_ms, void* rings, int* err, hipStream_t stream);
-
 /* One step (T = 1) of an LSTM direction with a carried state (the generation loops' mixers,
  * lstmformer.py:466-521): gates = [x | h0] [W_ih | W_hh]^T + b_ih + b_hh (i, f, g, o) -> gates
  * [B, 4H], c = f c0 + i g [B, H], h -> y[b * ldy + u] and hT [B, H] (nullable); h0 / c0 nullable

@@ -52,8 +52,6 @@ int mrg_debug_busy(int blocks, int threads, int lds, double usec, hipStream_t st
 /* Diagnostics: a 1-thread kernel writing the 100 MHz wall clock into ((uint64*)buf)[slot] in `stream`'s
  * order (tools/side_timing.py: when a replayed graph reaches a point). */
 int mrg_debug_stamp(void* buf, int slot, hipStream_t stream);
-/* Diagnostics: per-frame phase wall clocks of the persistent decode forward's block 0 ([T][8] u64). */
-int mrg_ssd_persist_debug_stamps(void* buf);
 /* Measurement (bench.py): while on, every kernel launched for a tagged library call (tag >= 0) is
  * timed by start / stop events bound to that kernel (hipExtLaunchKernelGGL): its own execution,
  * as rocprofv3 reports it.  stop waits, writes (ms, tag) per launch and returns the count. */

@@ -126,7 +126,6 @@ SIGNATURES = {
                                                    PP, P]),
     "mrg_debug_busy": (c_int, [c_int, c_int, c_int, ctypes.c_double, P]),
     "mrg_debug_stamp": (c_int, [P, c_int, P]),
-    "mrg_ssd_persist_debug_stamps": (c_int, [P]),
     "mrg_padding_flags": (c_int, [c_int, c_int, P, c_long, c_long, c_float, P, P]),
     "mrg_zero_padding": (c_int, [c_long, P, c_float, P, P]),
     "mrg_swap01": (c_int, [c_int, c_int, c_int, P, P, c_float, P]),
@@ -153,11 +152,6 @@ SIGNATURES = {
     "mrg_lstm_step_fwd": (c_int, [c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, c_long, P, P]),
     "mrg_ssd_ffn_z_fwd": (c_int, [c_int, c_int, c_int, P, P, P, P, c_float, P, P, P, P, P, P, P]),
     "mrg_ssd_y_fwd": (c_int, [c_int, c_int, c_int, P, P, P, P, c_long, P]),
-    "mrg_ssd_persist_ring_bytes": (c_long, [c_int, c_int, c_int, c_int]),
-    "mrg_ssd_persist_fits": (c_int, [c_int, c_int, c_int]),
-    "mrg_ssd_fwd_persist": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, ctypes.c_float, P, P, c_long,
-                                    c_long, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, c_long, P,
-                                    P, P, P]),
     "mrg_ssd_ffn_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_long, P, P, P, P, P, P, P, P, P, P, P,
                                 P, P, P, P, P, P, P, P, P, P, P]),
     "mrg_ssd_ln_cell_bwd": (c_int, [c_int, c_int, P, P, P, P, P, P, P, P, P, P, c_int, P, P, P, P]),

@@ -648,8 +648,10 @@ template <int D>
 struct FusedLds {
   static constexpr int SA = AttnCfg<D>::SA;
   static constexpr int QS = 0, DS = QS + FQT * SA, SS = DS + FQT * SA;
-  static constexpr int QA = SS + FQT * FSQ, LS = QA + FTQ * SA, DL = LS + FTQ;
-  static constexpr int FLOATS = DL + FTQ;
+  // lse / delta rows: FTQ + FQT, so a tile's reads stay inside the arrays for any tile start
+  // (they reach ceil16(Tq) - 1 < FTQ today, through the wave-uniform qb < Tq guard)
+  static constexpr int QA = SS + FQT * FSQ, LS = QA + FTQ * SA, DL = LS + FTQ + FQT;
+  static constexpr int FLOATS = DL + FTQ + FQT;
 };
 
 template <int D>
@@ -695,10 +697,14 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(AttnArgs a) {
     }
     dsum += __shfl_xor(dsum, 1, 64);
     dsum += __shfl_xor(dsum, 2, 64);
-    if (q < FTQ && g == 0) {   // zeros past Tq: the last sub-tile's rows beyond it read them (p = 0 there)
-      Dl[q] = q < Tq ? dsum : 0.0f;
-      Ls[q] = q < Tq ? a.lse[stat_row(a, b, h, q)] : 0.0f;
+    if (q < Tq && g == 0) {
+      Dl[q] = dsum;
+      Ls[q] = a.lse[stat_row(a, b, h, q)];
     }
+  }
+  for (int q = Tq + tid; q < FTQ + FQT; q += 512) {   // zeros past Tq: a sub-tile's rows beyond it read them (p = 0)
+    Dl[q] = 0.0f;
+    Ls[q] = 0.0f;
   }
   for (int i = tid; i < FTQ * C::SA / 4; i += 512)
     reinterpret_cast<float4*>(Qa)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -951,6 +957,7 @@ MRG_API int mrg_attention_bwd(int B, int Hh, int Tq, int Tk, int D,
   if (g_attn_fused && D == 64 && Tq <= FTQ && rows16(o, o_bs, o_ts) && a.dkvvec && rows16(dq, dq_bs, dq_ts)) {
     static bool attr[64] = {};   // the LDS size attribute, set once per device
     constexpr int bytes = FusedLds<64>::FLOATS * (int)sizeof(float);
+    static_assert(bytes <= 160 * 1024, "fused attention backward: LDS layout exceeds a CU's 160 KB");
     int dev = 0;
     MRG_HIP(hipGetDevice(&dev));
     if (dev < 0 || dev >= 64 || !attr[dev]) {

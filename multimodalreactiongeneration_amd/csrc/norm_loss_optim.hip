@@ -305,7 +305,7 @@ __global__ __launch_bounds__(256) void resln_bwd_v4_batched_kernel(LnBatch lb, i
 // 8 workgroups that each walked all 600 partial rows of a 19,200-row LayerNorm: 13.3 us per call,
 // 1.2 % of HBM.  4-wave workgroups, so they still fit beside a persistent
 // recurrence as deferred parameter-gradient products.
-constexpr int RESLN_TSLOTS = 64;                 // ticket sets: one per (device, stream) (see launcher)
+constexpr int RESLN_TSLOTS = 256;                // ticket sets: one per (device, stream, capture) (see launcher)
 constexpr int RESLN_MAXCB = 32;                  // column blocks: 2E / 64 <= 32 (E <= 1024)
 __device__ unsigned g_resln_tickets[RESLN_TSLOTS * RESLN_MAXCB];
 
@@ -734,32 +734,48 @@ MRG_API int mrg_residual_layernorm_bwd_batched(int n, int rows, int E, const flo
   return check_launch("resln_bwd_v4_batched_kernel");
 }
 
-// The ticket set of a launch belongs to its (device, stream): launches on one stream run one after
-// the other (in a captured graph, nodes of one capture stream are chained), and every ticket is back
-// at 0 before a launch ends, so one set per stream is never shared by two launches in flight, however
-// far another stream lags (a rotation over a global pool could hand two overlapping
-// launches on different streams the same set).  The symbol is resolved per device.
+// The ticket set of a launch belongs to its (device, stream, capture id): launches on one stream run
+// one after the other (in a captured graph, nodes of one capture stream are chained), and every ticket
+// is back at 0 before a launch ends, so one set per stream is never shared by two launches in flight,
+// however far another stream lags (a rotation over a global pool could hand two
+// overlapping launches on different streams the same set).  Under capture the capture id is part of
+// the key: two graphs captured on the same capture stream (torch.cuda.graph's shared
+// default one) hold different sets, so they may also be replayed concurrently.  Slots are never
+// recycled (a graph's nodes keep their pointer for its lifetime); when the table is full the reduce
+// runs ticket-free (R = 1: one workgroup per column block walks every partial row, slower, and its
+// summation order differs from R > 1 in the last bits).
+// The symbol is resolved per device.
 static std::mutex g_tick_mu;
-static struct { int dev; hipStream_t s; } g_tick_owner[RESLN_TSLOTS];
+static struct { int dev; hipStream_t s; unsigned long long cap; } g_tick_owner[RESLN_TSLOTS];
 static int g_tick_used = 0;
 static void* g_tick_base[64];
 
+// *tick = nullptr (and return 0) when the table is full: the caller then runs the ticket-free form.
 static int resln_tickets(hipStream_t stream, unsigned** tick) {
   int dev = 0;
   MRG_HIP(hipGetDevice(&dev));
   MRG_REQUIRE(dev >= 0 && dev < 64, "mrg_residual_layernorm_param_reduce: device %d", dev);
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  unsigned long long cap = 0;
+  MRG_HIP(hipStreamGetCaptureInfo(stream, &st, &cap));
+  if (st != hipStreamCaptureStatusActive) cap = 0;
   std::lock_guard<std::mutex> lk(g_tick_mu);
   if (!g_tick_base[dev]) MRG_HIP(hipGetSymbolAddress(&g_tick_base[dev], HIP_SYMBOL(g_resln_tickets)));
   int slot = -1;
   for (int i = 0; i < g_tick_used; ++i)
-    if (g_tick_owner[i].dev == dev && g_tick_owner[i].s == stream) { slot = i; break; }
+    if (g_tick_owner[i].dev == dev && g_tick_owner[i].s == stream && g_tick_owner[i].cap == cap) {
+      slot = i;
+      break;
+    }
   if (slot < 0) {
-    MRG_REQUIRE(g_tick_used < RESLN_TSLOTS,
-                "mrg_residual_layernorm_param_reduce: more than %d (device, stream) pairs issued reduces",
-                RESLN_TSLOTS);
+    if (g_tick_used >= RESLN_TSLOTS) {
+      *tick = nullptr;
+      return 0;
+    }
     slot = g_tick_used++;
     g_tick_owner[slot].dev = dev;
     g_tick_owner[slot].s = stream;
+    g_tick_owner[slot].cap = cap;
   }
   *tick = static_cast<unsigned*>(g_tick_base[dev]) + slot * RESLN_MAXCB;
   return 0;
@@ -772,9 +788,10 @@ MRG_API int mrg_residual_layernorm_param_reduce(int rows, int E, float* workspac
               "mrg_residual_layernorm_param_reduce: bad arguments (E=%d)", E);
   const int nblk = (rows + RESLN_RPB - 1) / RESLN_RPB;
   // row groups of ~32 partial rows (one round of loads per wave; distinct first rows), at most 64
-  const int R = nblk >= 64 ? ((nblk + 31) / 32 < 64 ? (nblk + 31) / 32 : 64) : 1;
+  int R = nblk >= 64 ? ((nblk + 31) / 32 < 64 ? (nblk + 31) / 32 : 64) : 1;
   unsigned* tick = nullptr;
   if (R > 1 && resln_tickets(stream, &tick)) return 1;
+  if (!tick) R = 1;   // ticket table full: one group per column block
   // the partials are consumed in place (each row group's sum overwrites its first row)
   resln_param_reduce_kernel<<<dim3((2 * E + 63) / 64, R), 256, 0, stream>>>(workspace, nblk, E, dgamma, dbeta,
                                                                             accumulate, R, tick);

@@ -23,8 +23,6 @@ reference's golden and to the oracle at benchmark width).
 """
 from __future__ import annotations
 
-import ctypes
-import os
 
 import torch
 from torch.autograd import Function
@@ -33,11 +31,6 @@ from . import _lib
 from .functional import _err_flag, _gbuf, _keeps_precision, _ptr, _resln_bwd, _stream, _wgrad, _side, gemm
 
 F32 = torch.float32
-# the frame loop of the forward as one persistent launch (decode_persist.hip, MRG_SSD_PERSIST=1): bitwise
-# the per-frame launches' result, but not faster yet (17 us per frame vs ~16: every global load or store
-# of a member's poller waves sits in front of its next hand-off poll, one in-order vmcnt; DESIGN.md
-# round 5), so the per-frame launches stay the default
-_PERSIST = [os.environ.get("MRG_SSD_PERSIST", "0") == "1"]
 
 
 class _SSDecodeFn(Function):
@@ -84,23 +77,7 @@ class _SSDecodeFn(Function):
         msc = ms.contiguous()
         slab, gslab, zslab = B * H, B * 4 * H, B * HB
         lw, lb = layers[-1][4], layers[-1][5]
-        persist = (_PERSIST[0] and nl <= 4 and HB <= H
-                   and lib.mrg_ssd_persist_fits(B, H, _lib.cu_count(dev.index or 0)) == 1)
-        if persist:
-            # the whole frame loop in one launch (decode_persist.hip)
-            rings = torch.zeros(max(1, lib.mrg_ssd_persist_ring_bytes(B, H, HB, nl) // 8), dtype=torch.int64,
-                                device=dev)
-
-            def arr(ts):
-                return (ctypes.c_void_p * nl)(*[_ptr(t_) for t_ in ts])
-            _lib.check(lib.mrg_ssd_fwd_persist(
-                B, H, HB, FO, F, T, nl, eps, _ptr(P), _ptr(msc), msc.stride(0), msc.stride(1), _ptr(mask),
-                _ptr(wms_t), _ptr(w1), _ptr(b1), _ptr(w2), _ptr(b2), arr([lay[0] for lay in layers]),
-                arr([lay[2] for lay in layers]), arr([lay[3] for lay in layers]), arr([lay[4] for lay in layers]),
-                arr([lay[5] for lay in layers]), arr(X), arr(G), arr(C), arr(Hs), arr([st[0] for st in stats]),
-                arr([st[1] for st in stats]), _ptr(U), _ptr(Z), _ptr(y), T * FO, _ptr(xf, SA + FMp), _ptr(rings),
-                _ptr(_err_flag(dev)), _stream()), "ssd persistent fwd")
-        for t in range(T) if not persist else ():
+        for t in range(T):
             for i, (w_ih, _w_hh, b_ih, b_hh, _g, _b) in enumerate(layers):
                 cell = (_ptr(w_ih), _ptr(b_ih), _ptr(b_hh), _ptr(G[i], t * gslab), _ptr(C[i], t * slab),
                         _ptr(Hs[i], t * slab), _stream())

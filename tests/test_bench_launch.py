@@ -36,13 +36,35 @@ def test_dry_run_launches_two_gloo_ranks():
     assert sorted(r_["rank"] for r_ in out["ranks_seen"]["ranks"]) == [0, 1]
     assert out["allreduce_mean_ok"] is True
     assert out["ms_per_step"] > 0
+    assert out["exchange"]["allreduce_ms"] > 0 and out["exchange"]["allreduce_bytes"] == 13_052_678 * 4
 
 
 def test_dry_run_single_rank_needs_no_launcher():
     r = _run(["--dry-run", "1", "--steps", "1", "--warmup", "0"], _env())
     assert r.returncode == 0, r.stderr[-2000:]
-    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert out["n_gpus"] == 1 and out["ranks_seen"]["world_size"] == 1
+
+
+def test_headline_is_the_last_line_and_small():
+    """a 20.7 KB line holding the secondary block was not parsed by the driver.  The
+    secondary configs print as their own lines first; the headline, with full-size synthetic kernels,
+    roofline (traffic included), CPU baseline and secondary summary, is the LAST stdout line, parses,
+    and fits HEADLINE_MAX_BYTES (8,000) with room to spare."""
+    r = _run(["--dry-run", "1", "--steps", "1", "--warmup", "0"], _env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = r.stdout.rstrip("\n").split("\n")
+    assert all(ln.startswith("{") for ln in lines), r.stdout[:500]
+    *sec, last = lines
+    assert len(last.encode()) <= 6000, len(last)
+    out = json.loads(last)
+    assert "secondary" not in out or all(isinstance(v, dict) and "ms_per_step" in v for v in out["secondary"].values())
+    assert out["roofline"]["family"] == "gemm" and "traffic" in out["roofline"]
+    assert out["roofline"]["frac"] > 0 and out["cpu_baseline"]["cores"] == 16
+    assert len(sec) == 6 and len(out["secondary"]) == 6
+    for ln in sec:
+        s = json.loads(ln)
+        assert s["secondary"] in out["secondary"] and "cpu_baseline" in s and "whole_step_roofline" in s
 
 
 def test_more_gpus_than_visible_fails_loudly():

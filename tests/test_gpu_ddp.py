@@ -99,6 +99,8 @@ def test_bench_multi_rank_timed_branch_on_one_gpu():
     assert out["n_gpus"] == 2 and out["ranks_seen"]["world_size"] == 2
     assert out["ranks_seen"]["backend"] == "gloo" and out["shared_device_test"] is True
     assert out["params_bitwise_equal_across_ranks"] is True
+    ex = out["exchange"]          # replay and exchange timed apart at N > 1
+    assert ex["replay_ms"] > 0 and ex["allreduce_ms"] > 0 and ex["allreduce_bytes"] == 13_052_678 * 4, ex
     chk = out["ddp_check"]
     assert chk["concat_batch"] == 16
     assert chk["grad_vs_concat_batch_worst_rel"] < TOL, chk

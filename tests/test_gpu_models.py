@@ -895,44 +895,3 @@ def test_feature_input_gradient_vs_oracle():
     for i in (0, 1):
         assert gb[i][0].grad is not None
         assert rel_err(gb[i][0].grad, cb[i][0].grad) < TOL, i
-
-
-@pytest.mark.parametrize("B,T", [(64, 300), (3, 40), (37, 25)])
-def test_ssd_persistent_forward_matches_per_frame(B, T):
-    """The scheduled-sampling decode forward as ONE persistent launch (decode_persist.hip: 16-row tiles x
-    H/4 members, granule hand-offs between the layers and frames; opt-in) vs decode.hip's per-frame launches on
-    the same inputs: prediction, loss and every gradient bitwise equal (the same per-element operation
-    order), ragged last row tile included.  Reference: lstm_with_sample.py:379-433."""
-    from multimodalreactiongeneration_amd import configs as C
-    from multimodalreactiongeneration_amd import decode as D
-    from multimodalreactiongeneration_amd import functional as Fn
-    from multimodalreactiongeneration_amd.model import LSTMwithSample
-    from multimodalreactiongeneration_amd.synthetic import make_batch, clone_batch
-    mc, oc, me = C.lstm_with_sampling_config(use_scheduled_sampling=True)
-    torch.manual_seed(0)
-    m = LSTMwithSample(mc, oc, me)
-    m.current_epoch = 30
-    m = m.to(DEV)
-    batch = make_batch(B=B, T=T, lead=12, seed=99, device=DEV)
-    mask = torch.from_numpy(np.random.RandomState(3).rand(T) < 0.5).to(DEV)
-    out = []
-    prev = D._PERSIST[0]
-    try:
-        for persist in (False, True):
-            D._PERSIST[0] = persist
-            for p in m.parameters():
-                p.grad = None
-            with torch.no_grad():
-                y, _ = m.prediction(clone_batch(batch, DEV), use_scheduled_sampling=True, sampling_mask=mask)
-            loss = m.training_step(clone_batch(batch, DEV), sampling_mask=mask)["loss"]
-            loss.backward()
-            torch.cuda.synchronize()
-            Fn.check_errors()
-            out.append((y.clone(), loss.detach().clone(), {k: p.grad.detach().clone() for k, p in m.named_parameters()}))
-    finally:
-        D._PERSIST[0] = prev
-    (y0, l0, g0), (y1, l1, g1) = out
-    assert torch.equal(y0, y1), rel_err(y1, y0)
-    assert torch.equal(l0, l1)
-    for k in g0:
-        assert torch.equal(g0[k], g1[k]), (k, rel_err(g1[k], g0[k]))
