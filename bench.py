@@ -242,12 +242,6 @@ class _DeviceTurns:
         return False
 
 
-def _kink_layer(name):
-    """ReLU FeedForward input layers: a pre-activation within ~1e-7 of 0 may take the other side of the
-    kink under another fp32 summation order (tests/test_gpu_models.py RELU_KINK_TOL)."""
-    return ".feedforward.feed_forward.module.input." in name or ".output_feedforward.feed_forward.input." in name
-
-
 def ddp_grad_check(model, opt, reducer, batch, args, rank, world, dev, turns):
     """One step's rank-averaged gradient (every rank on its own shard, then the exchange bench.py times)
     vs a single-rank step on the concatenation of all ranks' shards (what Lightning DDP's mean
@@ -269,21 +263,15 @@ def ddp_grad_check(model, opt, reducer, batch, args, rank, world, dev, turns):
             model.training_step(full)["loss"].backward()
         torch.cuda.synchronize()
         base = opt.flat_grad.data_ptr()
-        worst, worst_kink = (0.0, None), (0.0, None)
+        worst = (0.0, None)
         names = {id(p): k for k, p in model.named_parameters()}
         for p in opt.plist:
             off = (p.grad.data_ptr() - base) // 4
             a, b = g_avg[off:off + p.numel()], opt.flat_grad[off:off + p.numel()]
             e = ((a - b).abs().max() / b.abs().max().clamp_min(1e-12)).item()
-            k = names.get(id(p), "?")
-            slot = worst_kink if _kink_layer(k) else worst
-            if e > slot[0]:
-                if _kink_layer(k):
-                    worst_kink = (e, k)
-                else:
-                    worst = (e, k)
+            if e > worst[0]:
+                worst = (e, names.get(id(p), "?"))
         res = {"grad_vs_concat_batch_worst_rel": worst[0], "worst_param": worst[1],
-               "relu_kink_layers_worst_rel": worst_kink[0], "relu_kink_worst_param": worst_kink[1],
                "concat_batch": args.batch * world}
     opt.zero_grad()
     dist.barrier()

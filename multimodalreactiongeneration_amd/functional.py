@@ -874,6 +874,17 @@ def linear(x, weight, bias=None):
 
 
 # ------------------------------------------------------------------ FFN (Linear -> ReLU -> Linear)
+# Test hook (None in the product path): when a dict, every FFN forward stores the ReLU's side per
+# element, {w1.data_ptr(): bool [..., Hb] (pre-activation > 0)}, so a test can evaluate the float64
+# oracle at exactly this forward's kinks (oracle.RELU_MASKS; tests/test_gpu_models.py).
+RELU_TAP = None
+
+
+def _tap_relu(w1, h, lead_shape):
+    if RELU_TAP is not None:
+        RELU_TAP[w1.data_ptr()] = (h > 0).view(*lead_shape, h.shape[-1])
+
+
 class _FFNFn(Function):
     @staticmethod
     @_keeps_precision
@@ -888,6 +899,7 @@ class _FFNFn(Function):
         z = torch.empty(M, N, device=dev, dtype=torch.float32)
         _fwd_gemm(M, N, Hb, _ptr(h), Hb, w2, _ptr(z), N, bias=_ptr(b2), device=dev)
         _wt_note(w1, M, ctx.needs_input_grad[0])
+        _tap_relu(w1, h, x.shape[:-1])
         ctx.save_for_backward(x2, h, w1, b1, w2, b2)
         ctx.xshape = x.shape
         return z.view(*x.shape[:-1], N)
@@ -1047,6 +1059,7 @@ class _FFNResLNFn(Function):
         z = torch.empty(M, E, device=dev, dtype=torch.float32)
         _fwd_gemm(M, E, Hb, _ptr(h), Hb, w2, _ptr(z), E, bias=_ptr(b2), device=dev)
         _wt_note(w1, M, ctx.needs_input_grad[0])
+        _tap_relu(w1, h, x.shape[:-1])
         y, mean, rstd = _resln_fwd(z, x2, gamma, beta, eps)
         ctx.save_for_backward(x2, h, z, w1, b1, w2, b2, gamma, beta, mean, rstd)
         ctx.xshape = x.shape

@@ -28,12 +28,28 @@ PADDING_VALUE = -100.0
 ATEN_LSTM = False
 Tensor = torch.Tensor
 SD = Dict[str, Tensor]
+# ReLU masks of a GPU forward to evaluate the restatement AT (tests only): {weight prefix of the
+# Linear before the ReLU: bool tensor of its output's shape (True = the GPU's pre-activation > 0)}.
+# A pre-activation within fp32 rounding of 0 can take either side of the kink under a different
+# summation order; with the GPU's side injected the float64 answer is the GPU's own function of
+# its inputs, so the comparison holds 1e-4 everywhere (tests/test_gpu_models.py).
+RELU_MASKS: Optional[Dict[str, Tensor]] = None
 
 
 # --------------------------------------------------------------------------- ops
 def linear(x: Tensor, sd: SD, prefix: str) -> Tensor:
     """nn.Linear: y = x W^T + b."""
     return F.linear(x, sd[prefix + "weight"], sd.get(prefix + "bias"))
+
+
+def relu(x: Tensor, prefix: str) -> Tensor:
+    """torch.relu (mixer_block.py:37-87 FeedForward), or x * mask when RELU_MASKS holds this layer."""
+    m = None if RELU_MASKS is None else RELU_MASKS.get(prefix)
+    if m is None:
+        return torch.relu(x)
+    if m.shape != x.shape:
+        raise ValueError(f"oracle.relu: mask {tuple(m.shape)} for {prefix} but pre-activation {tuple(x.shape)}")
+    return x * m.to(x.dtype)
 
 
 def residual_ln(y: Tensor, x: Tensor, sd: SD, prefix: str) -> Tensor:
@@ -275,10 +291,11 @@ def metaformer_forward(sd: SD, cfg, inputs) -> Tensor:
               for ii, (kv, mk) in enumerate(zip(others, [ma_mask, mm_mask]))]
         main = linear(torch.cat(ys, -1), sd, bp + "integrator.cat_linear.")
         fp = bp + "feedforward.feed_forward."
-        z = linear(torch.relu(linear(main, sd, fp + "module.input.")), sd, fp + "module.output.")
+        u = relu(linear(main, sd, fp + "module.input."), fp + "module.input.")
+        z = linear(u, sd, fp + "module.output.")
         main = residual_ln(z, main, sd, fp + "layer_norm.")
     op = P + "output_feedforward.feed_forward."
-    return linear(torch.relu(linear(main, sd, op + "input.")), sd, op + "output.")
+    return linear(relu(linear(main, sd, op + "input."), op + "input."), sd, op + "output.")
 
 
 def metaformer_training_loss(sd: SD, cfg, batch) -> Tuple[Tensor, Tensor]:
@@ -394,7 +411,7 @@ def lstm_with_sample_forward(sd: SD, cfg, inputs, hx_sampler=None):
         p = f"layerd_lstm.lstm_layered.{layer}.lstm_module."
         y, _ = lstm_stack(f, sd, p + "module.lstm_module.", 1, False)
         f = residual_ln(y, f, sd, p + "layer_norm.")
-    y = linear(torch.relu(linear(f, sd, "feed_forward.input.")), sd, "feed_forward.mapping.")
+    y = linear(relu(linear(f, sd, "feed_forward.input."), "feed_forward.input."), sd, "feed_forward.mapping.")
     return y, hx_sampler
 
 
@@ -447,7 +464,8 @@ def _lstm_layerd(x, sd, p, num_layers, use_ff=True, use_mixing=True, bidirection
         y = residual_ln(y, x, sd, bp + "lstm_module.layer_norm.")
         if use_ff:
             fp = bp + "feed_forward_module."
-            z = linear(torch.relu(linear(y, sd, fp + "module.input.")), sd, fp + "module.mapping.")
+            u = relu(linear(y, sd, fp + "module.input."), fp + "module.input.")
+            z = linear(u, sd, fp + "module.mapping.")
             y = residual_ln(z, y, sd, fp + "layer_norm.")
         x = y
     return x
@@ -467,7 +485,7 @@ def simple_lstm_forward(sd: SD, cfg, audio: Tensor, motion: Tensor) -> Tensor:
         x = residual_ln(o, x, sd, p + "layer_norm.")
     d = _lstm_layerd(x, sd, "motion_decoder.decoder_lstm.", cfg["decoder_num_layers"])
     d = d[:, -1:, :]
-    return linear(torch.relu(linear(d, sd, "motion_decoder.mapping.input.")), sd,
+    return linear(relu(linear(d, sd, "motion_decoder.mapping.input."), "motion_decoder.mapping.input."), sd,
                   "motion_decoder.mapping.output.")
 
 

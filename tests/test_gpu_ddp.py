@@ -78,8 +78,8 @@ def test_bench_multi_rank_timed_branch_on_one_gpu():
     one GPU (--shared-device-gloo: gloo carries the exchange, the ranks' replays take turns), the
     pre-flight of the driver's 8-GPU SCALE run.  Asserts (a) one JSON line with a world of 2, (b) the
     ranks' parameters bitwise equal after the timed steps, (c) one step's rank-averaged gradient equal
-    to a single-rank step on the concatenated 2 x B batch (1e-4; the ReLU-kink layers 2e-3, as in
-    test_gpu_models.RELU_KINK_TOL).  Reference: config.yaml:121,127 (Lightning DDP)."""
+    to a single-rank step on the concatenated 2 x B batch (1e-4 on every parameter).
+    Reference: config.yaml:121,127 (Lightning DDP)."""
     import json
     import subprocess
     import sys
@@ -103,8 +103,7 @@ def test_bench_multi_rank_timed_branch_on_one_gpu():
     assert ex["replay_ms"] > 0 and ex["allreduce_ms"] > 0 and ex["allreduce_bytes"] == 13_052_678 * 4, ex
     chk = out["ddp_check"]
     assert chk["concat_batch"] == 16
-    assert chk["grad_vs_concat_batch_worst_rel"] < TOL, chk
-    assert chk["relu_kink_layers_worst_rel"] < 2e-3, chk
+    assert chk["grad_vs_concat_batch_worst_rel"] < TOL, chk     # every parameter, ReLU layers included
 
 
 def test_native_rccl_communicator_one_rank():

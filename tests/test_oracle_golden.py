@@ -411,3 +411,43 @@ def test_aten_gru_timing_path_equals_restatement(reverse):
     finally:
         O.ATEN_LSTM = prev
     assert rel_err(y1, y0) < 1e-5 and rel_err(h1, h0_) < 1e-5
+
+
+def test_relu_mask_injection_is_the_identity_at_the_own_kinks():
+    """oracle.RELU_MASKS (the GPU B=64 checks evaluate the float64 oracle at the GPU forward's ReLU
+    sides): injecting the masks the oracle's own forward decides gives bitwise its own loss and
+    gradients; flipping the sides of one sample's rows changes the result (the masks are really used); a mask of
+    the wrong shape is refused."""
+    d = load("metaformer_small_r2_pad")
+    cfg = config(d)
+    sd = prefixed(d, "param/")
+    batch = batch_from(d)
+    seen = {}
+    real = O.relu
+
+    def record(x, prefix):
+        seen[prefix] = x > 0
+        return real(x, prefix)
+    O.relu = record
+    try:
+        base = O.run_train_step(O.metaformer_training_loss, sd, cfg["optim"], cfg["model"], batch)
+    finally:
+        O.relu = real
+    assert sorted(seen) == sorted({k[:-len("weight")] for k in sd if k.endswith("input.weight")})
+    try:
+        O.RELU_MASKS = seen
+        inj = O.run_train_step(O.metaformer_training_loss, sd, cfg["optim"], cfg["model"], batch)
+        assert torch.equal(inj[0], base[0])
+        for k in base[2]:
+            assert torch.equal(inj[2][k], base[2][k]), k
+        key = sorted(seen)[-1]
+        flipped = seen[key].clone()
+        flipped[0] = ~flipped[0]
+        O.RELU_MASKS = dict(seen, **{key: flipped})
+        moved = O.run_train_step(O.metaformer_training_loss, sd, cfg["optim"], cfg["model"], batch)
+        assert not torch.equal(moved[2][key + "weight"], base[2][key + "weight"])
+        O.RELU_MASKS = {key: flipped[..., :-1]}
+        with pytest.raises(ValueError):
+            O.run_train_step(O.metaformer_training_loss, sd, cfg["optim"], cfg["model"], batch)
+    finally:
+        O.RELU_MASKS = None
