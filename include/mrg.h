@@ -269,6 +269,32 @@ int mrg_lstm_step_fwd(int B, int H, int In, const float* x, const float* h0, con
                       const float* w_ih, const float* w_hh, const float* b_ih, const float* b_hh,
                       float* gates, float* c, float* y, long ldy, float* hT, hipStream_t stream);
 
+/* Per-frame main chain of lstmformer generation (gen.hip; Metaformer.prediction, lstmformer.py:466-521,
+ * every frame a T = 1 forward with zero state): E = 256, FeedForward bottleneck 64, 16 batch rows x
+ * 16 output columns per workgroup, the LayerNorms a stage consumes recomputed in its prologue.
+ * mrg_gen_lstm: X = ms W_fe^T + b_fe (ms [B][fm], fm <= 16; feature_embedding.0) or X = LN(a + r)
+ *   (the previous block's FeedForward residual LayerNorm), written to xw [B][256]; gates =
+ *   X W_ih^T + b_ih + b_hh, zero-state cell (LSTMMixer, mixer_block.py:237-252) -> h [B][256].
+ * mrg_gen_linear mode 0: out = LN(a + r) W^T + b, LN rows to xw (LSTMMixerBlock, mixer_block.py:479-507);
+ *   mode 1: M = LN(a + r), Y_i = LN(a2[i] + M) to xw[:, 256 i:], out[:, 256 i:] = Y_i W_i^T + b_i
+ *   (both integrators' MHAMixerBlocks, mixer_block.py:567-603, with their attention output a2[i]);
+ *   mode 2: out = [LN(a[0] + r[0]) | LN(a[1] + r[1])] W^T + b (cat_linear over the integrators'
+ *   FeedForward LayerNorms, multi_modal_metaformer.py:128-217).  Host arrays of device pointers.
+ * mrg_gen_ffn: Linear(256 -> 64) -> ReLU -> Linear(64 -> N) of X = a or LN(a + r): out [B][256]; or,
+ *   with pred (the output FeedForward, N <= 16), y into pred[b * pred_bs + t * N + n] and the next
+ *   frame's self motion ms_next = mask[t] ? y : ms_src (lstmformer.py:487-492).                      */
+int mrg_gen_lstm(int B, int fm, const float* ms, const float* fe_w, const float* fe_b, const float* a,
+                 const float* r, const float* ga, const float* be, float eps, float* xw, const float* w_ih,
+                 const float* b_ih, const float* b_hh, float* h, hipStream_t stream);
+int mrg_gen_linear(int mode, int B, const float* const* a, const float* const* r, const float* const* ga,
+                   const float* const* be, long lda, const float* const* a2, const float* const* ga2,
+                   const float* const* be2, float eps, float* xw, long ldxw, const float* const* w,
+                   const float* const* bias, float* out, long ldo, hipStream_t stream);
+int mrg_gen_ffn(int B, int N, const float* a, const float* r, const float* ga, const float* be, float eps,
+                const float* w1, const float* b1, const float* w2, const float* b2, float* out, float* pred,
+                long pred_bs, float* ms_next, const float* ms_src, const unsigned char* mask, int t,
+                hipStream_t stream);
+
 /* ---------------------------------------------------------------- attention
  * Scaled-dot-product core of nn.MultiheadAttention as the reference calls it
  * (MHAforSequentail.forward, for_sequential.py:42-51;

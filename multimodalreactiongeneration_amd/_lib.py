@@ -150,6 +150,10 @@ SIGNATURES = {
                                            P, P, c_long, P, P, P, P, P, P, P, P, P]),
     "mrg_ssd_dx": (c_int, [c_int, c_int, P, P, P, P, P]),
     "mrg_lstm_step_fwd": (c_int, [c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, c_long, P, P]),
+    "mrg_gen_lstm": (c_int, [c_int, c_int, P, P, P, P, P, P, P, c_float, P, P, P, P, P, P]),
+    "mrg_gen_linear": (c_int, [c_int, c_int, PP, PP, PP, PP, c_long, PP, PP, PP, c_float, P, c_long, PP, PP, P,
+                               c_long, P]),
+    "mrg_gen_ffn": (c_int, [c_int, c_int, P, P, P, P, c_float, P, P, P, P, P, P, c_long, P, P, P, c_int, P]),
     "mrg_ssd_ffn_z_fwd": (c_int, [c_int, c_int, c_int, P, P, P, P, c_float, P, P, P, P, P, P, P]),
     "mrg_ssd_y_fwd": (c_int, [c_int, c_int, c_int, P, P, P, P, c_long, P]),
     "mrg_ssd_ffn_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_long, P, P, P, P, P, P, P, P, P, P, P,

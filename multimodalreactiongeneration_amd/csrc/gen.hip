@@ -1,0 +1,449 @@
+// Fused per-frame kernels of lstmformer generation (Metaformer.prediction -> head_motion_generation
+// -> generate_one_step, mr_gen/model/lstmformer/lstmformer.py:426-521).
+//
+// Every generated frame is a T = 1 forward with zero recurrent state and empty lead
+// inputs (gen_dummy_input, :549-559).  What depends on the previous frame is only the MAIN chain
+// (self motion -> feature_embedding.0 -> per block: LSTM mixer, two integrators, cat_linear,
+// FeedForward -> output FeedForward -> y -> next frame's self motion).  The other modalities' block-0
+// encoders and, at one audio frame per prediction frame, the integrators' whole attention output
+// (one visible key: softmax weight exactly 1, so MHA(q, kv) = out_proj(V(kv)) whatever q is) are
+// computed for all frames at once by the host (generate.py) as large GEMMs.  Per frame and block
+// this file then runs five launches instead of ~30:
+//
+//   gen_lstm    X = LN(ffn(prev) + prev) (block 0: X = ms_in W_fe^T + b_fe), gates = X W_ih^T + b,
+//               zero-state cell -> h                                    (mixer_block.py:237-252)
+//   gen_linear  Y = LN(h + X), Z = Y W^T + b                           (mixer_block.py:479-507)
+//   gen_linear  M = LN(Z + Y), Y_i = LN(a_i + M), Z_i = Y_i W_i^T + b_i  (both integrators,
+//               mixer_block.py:567-603)
+//   gen_linear  C = [LN(Z_0 + Y_0) | LN(Z_1 + Y_1)], M3 = C W_cat^T + b  (multi_modal_metaformer.py:128-217)
+//   gen_ffn     Zf = relu(M3 W1^T + b1) W2^T + b2                       (multi_modal_metaformer.py:328)
+//
+// and one gen_ffn for the output FeedForward with the sampling select of :487-492 folded in
+// (ms_in(t + 1) = mask[t] ? y(t) : motion_s[t]).  Each launch owns 16 batch rows x 16 output
+// columns per workgroup; the LayerNorms a stage consumes are recomputed from their inputs in the
+// workgroup's prologue (16 rows x 256, L2-resident) instead of a launch of their own, and each
+// workgroup writes its share of the normalised rows the next stage needs as a residual.
+// Products on v_mfma_f32_16x16x4_f32 (exact fp32 multiply-adds; the k order differs from the
+// training kernels', fp32 class).  E = 256, FeedForward bottleneck 64 (the lstmformer config).
+#include "lstm_common.h"
+
+namespace mrg {
+
+typedef float gv4 __attribute__((ext_vector_type(4)));
+static constexpr int GR = 16;    // batch rows per workgroup
+static constexpr int GE = 256;   // model width
+static constexpr int GHB = 64;   // FeedForward bottleneck
+
+struct GenLstmArgs {
+  int B, fm;
+  const float* ms;               // PRO 0: self-motion input [B][fm]
+  const float* fe_w;             // feature_embedding.0 [GE][fm], bias [GE]
+  const float* fe_b;
+  const float* a;                // PRO 1: X = LN(a + r) (the previous block's FeedForward)
+  const float* r;
+  const float* ga;
+  const float* be;
+  float eps;
+  float* xw;                     // X [B][GE] (this block's residual input), each workgroup its share
+  const float* w_ih;             // [4 GE][GE]
+  const float* b_ih;
+  const float* b_hh;
+  float* h;                      // [B][GE]
+};
+
+struct GenLinArgs {
+  int B;
+  const float* a[2];             // first LayerNorm inputs (PRO 2: the two halves)
+  const float* r[2];
+  const float* ga[2];
+  const float* be[2];
+  long lda;                      // row stride of a / r / a2
+  const float* a2[2];            // PRO 1: second LayerNorm: Y_i = LN(a2[i] + LN(a + r))
+  const float* ga2[2];
+  const float* be2[2];
+  float eps;
+  float* xw;                     // the normalised input rows (nullable), each workgroup its share
+  long ldxw;
+  const float* w[2];             // weight [n][K] of the column half (PRO 1: per integrator)
+  const float* bias[2];
+  float* out;
+  long ldo;
+};
+
+struct GenFfnArgs {
+  int B, N;                      // N output columns (256, or fm for the output FeedForward)
+  const float* a;                // PRO 0: X = a; PRO 1: X = LN(a + r)
+  const float* r;
+  const float* ga;
+  const float* be;
+  float eps;
+  const float* w1;               // [GHB][GE]
+  const float* b1;
+  const float* w2;               // [N][GHB]
+  const float* b2;
+  float* out;                    // OUT 0: [B][N]
+  float* pred;                   // OUT 1: pred[b * pred_bs + t * N + n]
+  long pred_bs;
+  float* ms_next;                // OUT 1: [B][N] = mask[t] ? y : ms_src
+  const float* ms_src;           // motion_s frame t [B][N]
+  const unsigned char* mask;     // [T] on the device
+  int t;
+};
+
+// whole-wave sum: DPP within each 16-lane row (no LDS traffic), then the four row sums read out
+__device__ __forceinline__ float gen_wave_sum(float v) {
+  // (readlane moves 32-bit integers: the float travels as its bit pattern)
+  const int u = __float_as_int(group_sum<16>(v));
+  return (__int_as_float(__builtin_amdgcn_readlane(u, 0)) + __int_as_float(__builtin_amdgcn_readlane(u, 16))) +
+         (__int_as_float(__builtin_amdgcn_readlane(u, 32)) + __int_as_float(__builtin_amdgcn_readlane(u, 48)));
+}
+
+// LayerNorm of a 256-wide row held as 4 consecutive values per lane, two-pass (torch.layer_norm:
+// mean, then the mean of squared deviations, biased), eps inside the root; gg / bb: the lane's four
+// gamma / beta values (loaded at kernel start, so their latency hides under the activation loads)
+__device__ __forceinline__ float4 gen_ln(float4 v, float4 gg, float4 bb, float eps) {
+  const float mean = gen_wave_sum((v.x + v.y) + (v.z + v.w)) * (1.0f / GE);
+  const float dx = v.x - mean, dy = v.y - mean, dz = v.z - mean, dw = v.w - mean;
+  const float var = gen_wave_sum((dx * dx + dy * dy) + (dz * dz + dw * dw)) * (1.0f / GE);
+  const float rs = rsqrtf(var + eps);
+  return make_float4(fmaf(dx * rs, gg.x, bb.x), fmaf(dy * rs, gg.y, bb.y), fmaf(dz * rs, gg.z, bb.z),
+                     fmaf(dw * rs, gg.w, bb.w));
+}
+
+__device__ __forceinline__ float4 gen_ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float4 gen_add4(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+__device__ __forceinline__ float4 gen_zero4() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+
+// acc[16 rows x 16 cols] += X[16][k0:k0+NK] W[n][k0:k0+NK]^T on v_mfma_f32_16x16x4_f32: lane l
+// supplies row / column l & 15 at k = kb + 4 (l >> 4) + j for the j-th product of a 16-k group, so
+// its four operands of a group are one float4 (A and B use the same k of each product pair).
+// gen_wload issues the lane's weight loads (at kernel start: independent of the prologue)
+template <int NK>
+__device__ __forceinline__ void gen_wload(const float* __restrict__ wrow, int k0, int lane, float4 (&w)[NK / 16]) {
+#pragma unroll
+  for (int i = 0; i < NK / 16; ++i) w[i] = *reinterpret_cast<const float4*>(wrow + k0 + 16 * i + 4 * (lane >> 4));
+}
+template <int KP, int NK>
+__device__ __forceinline__ gv4 gen_mfma(const float* xs, const float4 (&w)[NK / 16], int k0, int lane, gv4 acc) {
+  const int m = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < NK / 16; ++i) {
+    const float4 x = *reinterpret_cast<const float4*>(xs + m * KP + k0 + 16 * i + 4 * q);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.x, w[i].x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.y, w[i].y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.z, w[i].z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.w, w[i].w, acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+// the four waves' k-quarter partial tiles into red[4][16][17]; accumulator register i of lane l is
+// row 4 (l >> 4) + i, column l & 15
+__device__ __forceinline__ void gen_park(float (*red)[GR][17], int wave, int lane, gv4 acc) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) red[wave][4 * (lane >> 4) + i][lane & 15] = acc[i];
+}
+__device__ __forceinline__ float gen_sum(const float (*red)[GR][17], int m, int n) {
+  return (red[0][m][n] + red[1][m][n]) + (red[2][m][n] + red[3][m][n]);
+}
+
+// Every launch below first issues the loads that do not depend on the previous launch (this lane's
+// weight operands, the LayerNorm gamma / beta, the biases of its outputs), then the activation rows
+// (clamped past B, zeroed after), so a kernel waits about one memory round trip before its products.
+
+// ------------------------------------------------------------------ LSTM mixer gates + cell
+// grid (GE / 4 unit groups, ceil(B / 16)); column n of the tile = gate n >> 2 of unit 4 bx + (n & 3)
+template <int PRO>
+__global__ __launch_bounds__(256) void gen_lstm_kernel(GenLstmArgs p) {
+  constexpr int KP = GE + 4;
+  __shared__ __attribute__((aligned(16))) float xs[GR][KP];
+  __shared__ float red[4][GR][17];
+  __shared__ float msl[GR][16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int row0 = blockIdx.y * GR, u0 = 4 * blockIdx.x;
+  const int share = GE / gridDim.x;   // X columns this workgroup writes back
+  const int n = lane & 15;
+  float4 w[GE / 4 / 16];
+  gen_wload<GE / 4>(p.w_ih + (long)((n >> 2) * GE + u0 + (n & 3)) * GE, wave * (GE / 4), lane, w);
+  // cell thread (m, j): its unit's biases
+  const int cm = tid >> 2, cj = tid & 3, cu = u0 + cj;
+  float bi = 0.f, bg = 0.f, bo = 0.f;
+  if (tid < 4 * GR) {
+    bi = p.b_ih[cu] + p.b_hh[cu];
+    bg = p.b_ih[2 * GE + cu] + p.b_hh[2 * GE + cu];
+    bo = p.b_ih[3 * GE + cu] + p.b_hh[3 * GE + cu];
+  }
+  if (PRO == 0) {
+    // X = ms W_fe^T + b_fe (K = fm <= 16): the 16 rows' inputs staged in LDS, thread = column
+    const int k = tid;
+    float wf[16];
+#pragma unroll
+    for (int f = 0; f < 16; ++f) wf[f] = f < p.fm ? p.fe_w[k * p.fm + f] : 0.0f;
+    const float bk = p.fe_b[k];
+    if (tid < GR * 16) {
+      const int m = tid >> 4, f = tid & 15;
+      msl[m][f] = (f < p.fm && row0 + m < p.B) ? p.ms[(long)(row0 + m) * p.fm + f] : 0.0f;
+    }
+    __syncthreads();
+    const bool mine = k >= blockIdx.x * share && k < (blockIdx.x + 1) * share;
+#pragma unroll
+    for (int m = 0; m < GR; ++m) {
+      float s = 0.0f;
+#pragma unroll
+      for (int f = 0; f < 16; ++f) s = fmaf(msl[m][f], wf[f], s);
+      const float v = row0 + m < p.B ? s + bk : 0.0f;
+      if (mine && row0 + m < p.B) p.xw[(long)(row0 + m) * GE + k] = v;
+      xs[m][k] = v;
+    }
+  } else {
+    const float4 gg = gen_ld4(p.ga + 4 * lane), bb = gen_ld4(p.be + 4 * lane);
+    float4 va[GR / 4], vr[GR / 4];
+#pragma unroll
+    for (int i = 0; i < GR / 4; ++i) {
+      const long b = min(row0 + wave + 4 * i, p.B - 1);
+      va[i] = gen_ld4(p.a + b * GE + 4 * lane);
+      vr[i] = gen_ld4(p.r + b * GE + 4 * lane);
+    }
+    const int k = 4 * lane;
+    const bool mine = k >= blockIdx.x * share && k < (blockIdx.x + 1) * share;
+#pragma unroll
+    for (int i = 0; i < GR / 4; ++i) {
+      const int m = wave + 4 * i, b = row0 + m;
+      float4 v = gen_ln(gen_add4(va[i], vr[i]), gg, bb, p.eps);
+      if (b >= p.B) v = gen_zero4();
+      else if (mine) *reinterpret_cast<float4*>(p.xw + (long)b * GE + k) = v;
+      *reinterpret_cast<float4*>(&xs[m][k]) = v;
+    }
+  }
+  __syncthreads();
+  gv4 acc = gv4{0.f, 0.f, 0.f, 0.f};
+  acc = gen_mfma<KP, GE / 4>(&xs[0][0], w, wave * (GE / 4), lane, acc);
+  gen_park(red, wave, lane, acc);
+  __syncthreads();
+  if (tid < 4 * GR && row0 + cm < p.B) {
+    const float zi = gen_sum(red, cm, cj) + bi;
+    const float zg = gen_sum(red, cm, 8 + cj) + bg;
+    const float zo = gen_sum(red, cm, 12 + cj) + bo;
+    const float c = sigmoidf_(zi) * tanhf_(zg);   // f c0 + i g with c0 = 0
+    p.h[(long)(row0 + cm) * GE + cu] = sigmoidf_(zo) * tanhf_(c);
+  }
+}
+
+// ------------------------------------------------------------------ Linear with LayerNorm prologue
+// PRO 0: X = LN(a + r)                          K = 256, grid (N / 16, rows)
+// PRO 1: X = LN(a2[i] + LN(a + r)), i = half     K = 256, N = 512 (two 256-column halves)
+// PRO 2: X = [LN(a[0] + r[0]) | LN(a[1] + r[1])] K = 512
+template <int PRO>
+__global__ __launch_bounds__(256) void gen_linear_kernel(GenLinArgs p) {
+  constexpr int K = PRO == 2 ? 2 * GE : GE;
+  constexpr int KP = K + 4;
+  constexpr int NH = PRO == 2 ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) float xs[GR][KP];
+  __shared__ float red[4][GR][17];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int row0 = blockIdx.y * GR;
+  const int n0 = 16 * blockIdx.x;
+  const int half = PRO == 1 ? n0 / GE : 0;           // PRO 1: integrator of this column tile
+  const int tiles = PRO == 1 ? gridDim.x / 2 : gridDim.x;
+  const int share = GE / tiles, sh0 = (blockIdx.x % tiles) * share;
+  const int nl = n0 - half * GE;                     // first row of this half's weight
+  float4 w[K / 4 / 16];
+  gen_wload<K / 4>(p.w[half] + (long)(nl + (lane & 15)) * K, wave * (K / 4), lane, w);
+  const float bias = p.bias[half][nl + (tid & 15)];
+  const int k = 4 * lane;
+  float4 gg[NH], bb[NH], g2 = gen_zero4(), b2 = gen_zero4();
+#pragma unroll
+  for (int hh = 0; hh < NH; ++hh) {
+    gg[hh] = gen_ld4(p.ga[hh] + k);
+    bb[hh] = gen_ld4(p.be[hh] + k);
+  }
+  if (PRO == 1) {
+    g2 = gen_ld4(p.ga2[half] + k);
+    b2 = gen_ld4(p.be2[half] + k);
+  }
+  {
+    float4 va[GR / 4][NH], vr[GR / 4][NH], v2[GR / 4];
+#pragma unroll
+    for (int i = 0; i < GR / 4; ++i) {
+      const long b = min(row0 + wave + 4 * i, p.B - 1);
+#pragma unroll
+      for (int hh = 0; hh < NH; ++hh) {
+        va[i][hh] = gen_ld4(p.a[hh] + b * p.lda + k);
+        vr[i][hh] = gen_ld4(p.r[hh] + b * p.lda + k);
+      }
+      if (PRO == 1) v2[i] = gen_ld4(p.a2[half] + b * p.lda + k);
+    }
+    const bool mine = p.xw && k >= sh0 && k < sh0 + share;
+#pragma unroll
+    for (int i = 0; i < GR / 4; ++i) {
+      const int m = wave + 4 * i, b = row0 + m;
+#pragma unroll
+      for (int hh = 0; hh < NH; ++hh) {
+        float4 v = gen_ln(gen_add4(va[i][hh], vr[i][hh]), gg[hh], bb[hh], p.eps);
+        if (PRO == 1) v = gen_ln(gen_add4(v2[i], v), g2, b2, p.eps);
+        if (b >= p.B) v = gen_zero4();
+        else if (mine) *reinterpret_cast<float4*>(p.xw + b * p.ldxw + half * GE + k) = v;
+        *reinterpret_cast<float4*>(&xs[m][hh * GE + k]) = v;
+      }
+    }
+  }
+  __syncthreads();
+  gv4 acc = gv4{0.f, 0.f, 0.f, 0.f};
+  acc = gen_mfma<KP, K / 4>(&xs[0][0], w, wave * (K / 4), lane, acc);
+  gen_park(red, wave, lane, acc);
+  __syncthreads();
+  const int m = tid >> 4, nn = tid & 15, b = row0 + m;
+  if (b < p.B) p.out[b * p.ldo + n0 + nn] = gen_sum(red, m, nn) + bias;
+}
+
+// ------------------------------------------------------------------ FeedForward (Linear-ReLU-Linear)
+// the 16 x 64 hidden rows computed per workgroup (wave w: hidden columns 16w..16w+15 over K = 256),
+// then the output tile 16 x 16 over K = 64 (a k-quarter per wave).  grid (ceil(N / 16), rows).
+// OUT 1: the output FeedForward's y written into pred[:, t] and the next frame's self motion
+template <int PRO, int OUT>
+__global__ __launch_bounds__(256) void gen_ffn_kernel(GenFfnArgs p) {
+  constexpr int KP = GE + 4, HP = GHB + 4;
+  __shared__ __attribute__((aligned(16))) float xs[GR][KP];
+  __shared__ __attribute__((aligned(16))) float hs[GR][HP];
+  __shared__ float red[4][GR][17];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int row0 = blockIdx.y * GR;
+  const int n0 = 16 * blockIdx.x;
+  const int hc = 16 * wave + (lane & 15);            // this lane's hidden column
+  float4 w1[GE / 16];
+  gen_wload<GE>(p.w1 + (long)hc * GE, 0, lane, w1);
+  const float b1 = p.b1[hc];
+  const int nw = n0 + (lane & 15);
+  const bool nok = nw < p.N;
+  // a column past N (the output FeedForward's 6 outputs) multiplies a zero row
+  float4 w2 = *reinterpret_cast<const float4*>(p.w2 + (long)(nok ? nw : 0) * GHB + 16 * wave + 4 * (lane >> 4));
+  if (!nok) w2 = gen_zero4();
+  const int ocol = n0 + (tid & 15);
+  const float b2 = ocol < p.N ? p.b2[ocol] : 0.0f;
+  {
+    float4 gg = gen_zero4(), bb = gen_zero4();
+    if (PRO == 1) {
+      gg = gen_ld4(p.ga + 4 * lane);
+      bb = gen_ld4(p.be + 4 * lane);
+    }
+    float4 va[GR / 4], vr[GR / 4];
+#pragma unroll
+    for (int i = 0; i < GR / 4; ++i) {
+      const long b = min(row0 + wave + 4 * i, p.B - 1);
+      va[i] = gen_ld4(p.a + b * GE + 4 * lane);
+      if (PRO == 1) vr[i] = gen_ld4(p.r + b * GE + 4 * lane);
+    }
+#pragma unroll
+    for (int i = 0; i < GR / 4; ++i) {
+      const int m = wave + 4 * i;
+      float4 v = va[i];
+      if (PRO == 1) v = gen_ln(gen_add4(v, vr[i]), gg, bb, p.eps);
+      if (row0 + m >= p.B) v = gen_zero4();
+      *reinterpret_cast<float4*>(&xs[m][4 * lane]) = v;
+    }
+  }
+  __syncthreads();
+  {
+    gv4 acc = gv4{0.f, 0.f, 0.f, 0.f};
+    acc = gen_mfma<KP, GE>(&xs[0][0], w1, 0, lane, acc);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) hs[4 * (lane >> 4) + i][hc] = fmaxf(acc[i] + b1, 0.0f);
+  }
+  __syncthreads();
+  gv4 acc = gv4{0.f, 0.f, 0.f, 0.f};
+  {
+    const int m = lane & 15, q = lane >> 4, k = 16 * wave;
+    const float4 x = *reinterpret_cast<const float4*>(&hs[m][k + 4 * q]);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.x, w2.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.y, w2.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.z, w2.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.w, w2.w, acc, 0, 0, 0);
+  }
+  gen_park(red, wave, lane, acc);
+  __syncthreads();
+  const int m = tid >> 4, nn = tid & 15, b = row0 + m;
+  if (b >= p.B || ocol >= p.N) return;
+  const float y = gen_sum(red, m, nn) + b2;
+  if (OUT == 0) {
+    p.out[(long)b * p.N + ocol] = y;
+  } else {
+    p.pred[(long)b * p.pred_bs + (long)p.t * p.N + ocol] = y;
+    const long i = (long)b * p.N + ocol;
+    p.ms_next[i] = p.mask[p.t] ? y : p.ms_src[i];
+  }
+}
+
+}  // namespace mrg
+
+using namespace mrg;
+
+static int gen_rows(int B) { return (B + GR - 1) / GR; }
+
+// X [B][256] from the self-motion input (block 0: ms W_fe^T + b_fe, fm <= 16) or from the previous
+// block's FeedForward (LN(a + r)); gates = X W_ih^T + b_ih + b_hh; zero-state cell -> h [B][256].
+MRG_API int mrg_gen_lstm(int B, int fm, const float* ms, const float* fe_w, const float* fe_b, const float* a,
+                         const float* r, const float* ga, const float* be, float eps, float* xw, const float* w_ih,
+                         const float* b_ih, const float* b_hh, float* h, hipStream_t stream) {
+  if (B == 0) return 0;
+  MRG_REQUIRE(ms ? (fm >= 1 && fm <= 16 && fe_w && fe_b) : (a && r && ga && be),
+              "mrg_gen_lstm: give ms + feature embedding (fm <= 16) or the LayerNorm inputs");
+  GenLstmArgs p{B, fm, ms, fe_w, fe_b, a, r, ga, be, eps, xw, w_ih, b_ih, b_hh, h};
+  const dim3 grid(GE / 4, gen_rows(B));
+  if (ms) klaunch(gen_lstm_kernel<0>, grid, 256, 0, stream, p);
+  else klaunch(gen_lstm_kernel<1>, grid, 256, 0, stream, p);
+  return check_launch("gen_lstm_kernel");
+}
+
+// mode 0: out [B][256] = LN(a + r) W^T + b, the normalised rows into xw [B][256]
+// mode 1: the two integrators: M = LN(a + r) (ga[0]), Y_i = LN(a2[i] + M) (ga2[i]) into xw[:, 256 i:],
+//         out[:, 256 i:] = Y_i W_i^T + b_i   (out, xw [B][512])
+// mode 2: out [B][256] = [LN(a[0] + r[0]) | LN(a[1] + r[1])] W^T + b   (W [256][512]; a, r of stride lda)
+MRG_API int mrg_gen_linear(int mode, int B, const float* const* a, const float* const* r, const float* const* ga,
+                           const float* const* be, long lda, const float* const* a2, const float* const* ga2,
+                           const float* const* be2, float eps, float* xw, long ldxw, const float* const* w,
+                           const float* const* bias, float* out, long ldo, hipStream_t stream) {
+  if (B == 0) return 0;
+  MRG_REQUIRE(mode >= 0 && mode <= 2 && a && r && ga && be && w && bias && out,
+              "mrg_gen_linear: bad arguments (mode %d)", mode);
+  GenLinArgs p{};
+  p.B = B;
+  const int nh = mode == 0 ? 1 : 2;
+  for (int i = 0; i < 2; ++i) {
+    const int s = (mode == 2 && i < nh) ? i : 0;
+    p.a[i] = a[s]; p.r[i] = r[s]; p.ga[i] = ga[s]; p.be[i] = be[s];
+    const int t = (mode == 1) ? i : 0;
+    p.w[i] = w[t]; p.bias[i] = bias[t];
+    if (mode == 1) {
+      MRG_REQUIRE(a2 && ga2 && be2, "mrg_gen_linear: mode 1 needs the second LayerNorm's inputs");
+      p.a2[i] = a2[i]; p.ga2[i] = ga2[i]; p.be2[i] = be2[i];
+    }
+  }
+  p.lda = lda; p.eps = eps; p.xw = xw; p.ldxw = ldxw; p.out = out; p.ldo = ldo;
+  const dim3 grid(mode == 1 ? 2 * GE / 16 : GE / 16, gen_rows(B));
+  if (mode == 0) klaunch(gen_linear_kernel<0>, grid, 256, 0, stream, p);
+  else if (mode == 1) klaunch(gen_linear_kernel<1>, grid, 256, 0, stream, p);
+  else klaunch(gen_linear_kernel<2>, grid, 256, 0, stream, p);
+  return check_launch("gen_linear_kernel");
+}
+
+// FeedForward 256 -> 64 -> ReLU -> N of X = a (r null) or LN(a + r).  pred null: out [B][N] (N = 256).
+// pred given (the output FeedForward, N <= 16): y into pred[b * pred_bs + t * N + n] and
+// ms_next [B][N] = mask[t] ? y : ms_src (the next frame's self motion, lstmformer.py:487-492).
+MRG_API int mrg_gen_ffn(int B, int N, const float* a, const float* r, const float* ga, const float* be, float eps,
+                        const float* w1, const float* b1, const float* w2, const float* b2, float* out, float* pred,
+                        long pred_bs, float* ms_next, const float* ms_src, const unsigned char* mask, int t,
+                        hipStream_t stream) {
+  if (B == 0) return 0;
+  MRG_REQUIRE(a && w1 && b1 && w2 && b2 && (r == nullptr || (ga && be)), "mrg_gen_ffn: bad arguments");
+  MRG_REQUIRE(pred ? (N >= 1 && N <= 16 && ms_next && ms_src && mask) : (N == GE && out),
+              "mrg_gen_ffn: N = 256 with out, or N <= 16 with pred / ms_next / ms_src / mask (N=%d)", N);
+  GenFfnArgs p{B, N, a, r, ga, be, eps, w1, b1, w2, b2, out, pred, pred_bs, ms_next, ms_src, mask, t};
+  const dim3 grid((N + 15) / 16, gen_rows(B));
+  if (r && pred) klaunch(gen_ffn_kernel<1, 1>, grid, 256, 0, stream, p);
+  else if (r) klaunch(gen_ffn_kernel<1, 0>, grid, 256, 0, stream, p);
+  else if (pred) klaunch(gen_ffn_kernel<0, 1>, grid, 256, 0, stream, p);
+  else klaunch(gen_ffn_kernel<0, 0>, grid, 256, 0, stream, p);
+  return check_launch("gen_ffn_kernel");
+}

@@ -321,14 +321,21 @@ class Metaformer(LightningSurface):
         fb = fb * (fb != PADDING_VALUE).to(fb.dtype)
         mp = mp * (mp != PADDING_VALUE).to(mp.dtype)
         ms = ms * (ms != PADDING_VALUE).to(ms.dtype)
-        empty = [(torch.empty(x.shape[0], 0, x.shape[2], device=dev), n) for x, n in batch]
-        _, cell = self.forward(*empty[:3], *batch[3:6], hxs=None)
         if sampling_mask is not None:
             mask = sampling_mask
         elif use_scheduled_sampling:
             mask = torch.rand(T) < (self.current_epoch / self.max_epochs)
         else:
             mask = torch.ones(T, dtype=torch.bool) if full_generation else torch.zeros(T, dtype=torch.bool)
+        if not torch.is_grad_enabled():
+            # inference: the frame loop on the fused per-frame kernels (generate.py); the warm-up
+            # forward below only makes a state no frame reads, so it is skipped there
+            from ..generate import plan_for
+            plan = plan_for(self)
+            if plan is not None:
+                return plan.generate(fb, mp, ms, mask)
+        empty = [(torch.empty(x.shape[0], 0, x.shape[2], device=dev), n) for x, n in batch]
+        _, cell = self.forward(*empty[:3], *batch[3:6], hxs=None)
         on_device = mask.device.type != "cpu"
         y = ms[0]
         preds = []
