@@ -32,7 +32,7 @@ METRIC = "training frames/sec/GPU, lstmformer T=300 B=64; 1→8 GPU scaling"
 FP32_MFMA_PEAK_TF = 157.3   # MI355X_MICROARCH.md chip table (f32 matrix, dense)
 BF16_MFMA_PEAK_TF = 2500.0  # MI355X_MICROARCH.md chip table (bf16 matrix, dense)
 HBM_PEAK_GBS = 8000.0
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r05_pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r06_pmc_summary.json")
 
 # probe name (functional._probe) -> kernels it brackets (descriptions and FLOP counts: DESIGN.md §4)
 FAMILIES = {
@@ -43,6 +43,7 @@ FAMILIES = {
     "attn_bwd": "attn_bwd_fused_kernel",                         # 10D FLOP per visible pair per head
     "gru_fwd": "gru_fwd_kernel",                                 # 6H^2 FLOP per (b, t) per layer
     "gru_bwd": "gru_bwd_kernel",                                 # 6H^2 FLOP per (b, t) per layer
+    "gen": "gen_lstm+gen_linear+gen_ffn",                        # generation frame loop, 2MNK FLOP per launch
 }
 PEAK_NOTES = {
     "gemm": "f32 dense matrix peak; x6 bf16 split's own MFMA ceiling 416.7",
@@ -50,6 +51,7 @@ PEAK_NOTES = {
     "lstm_bwd": "latency-bound recurrence; f32 VALU peak",
     "gru_fwd": "latency-bound recurrence; f32 VALU peak",
     "gru_bwd": "latency-bound recurrence; f32 VALU peak",
+    "gen": "launch-latency-bound 64-row products (26 dependent launches per frame); f32 matrix peak",
 }
 HEADLINE_MAX_BYTES = 8000   # the driver parses the LAST stdout line; keep it well inside its window
 # rocprofv3 kernel-name prefix of each family in the PMC summary (tools/tools_pmc_summary.py)
@@ -57,7 +59,7 @@ PMC_KEYS = {"gemm": "gemm_all", "lstm_fwd": "lstm_fwd", "lstm_bwd": "lstm_bwd",
             "attn_fwd": "attn_fwd_kernel", "attn_bwd": "attn_bwd"}
 
 
-TRACE_SUMMARY = os.path.join(ROOT, "profiles", "r05_trace_roofline.json")
+TRACE_SUMMARY = os.path.join(ROOT, "profiles", "r06_trace_roofline.json")
 
 
 def trace_check(roof):
@@ -774,7 +776,7 @@ def secondary(args, dev):
             m._generate(batch, sampling_mask=gmask)
     replay = capture(gen, 2)
     ms = _timed_replay(replay, 5, 2)
-    kern = ({}, None)   # launch-bound (as C3): per-kernel split from rocprof in profiles/, not brackets
+    kern = _probe_steps(gen)   # every frame-loop kernel timed by kernel-bound events (generate.py probes)
     cpu = None
     if cpu_on:
         info = _cpu_setup(args)
@@ -787,7 +789,9 @@ def secondary(args, dev):
                           f"{ct} frames x B={B} (per-frame cost is independent of T), 1 run")
     _put(out, "lstmformer_generation", _secondary_entry(
         "lstmformer autoregressive generation (Metaformer.prediction, full_generation, eval, no grad) "
-        "B=64 x 300 frames, HIP graph; one step = one 64-clip batch", ms, B * T, gen_flops_per_frame(mc, 1), "fp32",
+        "B=64 x 300 frames, HIP graph; one step = one 64-clip batch; fused frame loop (generate.py: other "
+        "modalities' encoders and one-key attention hoisted over all frames, 26 launches per frame)", ms, B * T,
+        gen_flops_per_frame(mc, 1), "fp32",
         kern, cpu))
     del m, replay
 

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-5 profile set (gpurun -- bash tools/r05_profiles.sh <tag>): GPU tests + smoke, the
+# Round-6 profile set (gpurun -- bash tools/r06_profiles.sh <tag>): GPU tests + smoke, the
 # default bench line (secondary configs, CPU baselines), a kernel trace of the bench's headline
 # workload (graph replayed) -> trace roofline summary, FETCH_SIZE / WRITE_SIZE passes over one eager
 # step -> PMC summary.  Every GPU step has its own limit; the script stops at the first failure.
@@ -9,7 +9,7 @@ set -o pipefail
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 TAG=${1:-v1}
-O=$R/gpurun_out/r05_$TAG
+O=$R/gpurun_out/r06_$TAG
 mkdir -p $O
 cd $R
 if [ "${PART:-1}" = "3" ]; then
