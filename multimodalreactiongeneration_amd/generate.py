@@ -154,34 +154,46 @@ class GenPlan:
                 ffn=(w1, b1, w2, b2)))
         ow1, ob1, ow2, ob2, _ = self.out
         lastln = self.blocks[-1]["ffn"][4]
+        # algorithmic FLOPs of each launch (2 x rows x outputs x K; the LayerNorms are O(rows x E))
+        f_lstm, f_lin0 = 2.0 * B * 4 * E * E, 2.0 * B * E * E
+        f_lin1, f_lin2 = 2.0 * B * 2 * E * E, 2.0 * B * E * 2 * E
+        f_ffn, f_out = 2.0 * B * HB_GEN * (E + E), 2.0 * B * HB_GEN * (E + self.fm)
         for t in range(T):
             for bi, c in enumerate(calls):
                 w_ih, b_ih, b_hh, prev = c["lstm"]
                 if bi == 0:
                     src = msc[0] if t == 0 else ms_in
-                    _lib.check(lib.mrg_gen_lstm(B, self.fm, _ptr(src), _ptr(fe0.weight), _ptr(fe0.bias), None, None,
-                                                None, None, eps, _ptr(xb), _ptr(w_ih), _ptr(b_ih), _ptr(b_hh),
-                                                _ptr(hh), st), "gen lstm")
+                    with Fn._probe("gen", f_lstm + 2.0 * B * E * self.fm):
+                        _lib.check(lib.mrg_gen_lstm(B, self.fm, _ptr(src), _ptr(fe0.weight), _ptr(fe0.bias), None, None,
+                                                    None, None, eps, _ptr(xb), _ptr(w_ih), _ptr(b_ih), _ptr(b_hh),
+                                                    _ptr(hh), st), "gen lstm")
                 else:
-                    _lib.check(lib.mrg_gen_lstm(B, self.fm, None, None, None, _ptr(zf), _ptr(m3), _ptr(prev.weight),
-                                                _ptr(prev.bias), eps, _ptr(xb), _ptr(w_ih), _ptr(b_ih), _ptr(b_hh),
-                                                _ptr(hh), st), "gen lstm")
+                    with Fn._probe("gen", f_lstm):
+                        _lib.check(lib.mrg_gen_lstm(B, self.fm, None, None, None, _ptr(zf), _ptr(m3),
+                                                    _ptr(prev.weight), _ptr(prev.bias), eps, _ptr(xb), _ptr(w_ih),
+                                                    _ptr(b_ih), _ptr(b_hh), _ptr(hh), st), "gen lstm")
                 a, r, ga, be, w, bias = c["lin0"]
-                _lib.check(lib.mrg_gen_linear(0, B, a, r, ga, be, E, None, None, None, eps, _ptr(y), E, w, bias,
-                                              _ptr(z), E, st), "gen mixer linear")
+                with Fn._probe("gen", f_lin0):
+                    _lib.check(lib.mrg_gen_linear(0, B, a, r, ga, be, E, None, None, None, eps, _ptr(y), E, w, bias,
+                                                  _ptr(z), E, st), "gen mixer linear")
                 a, r, ga, be, ga2, be2, w, bias = c["lin1"]
                 a2 = _arr(_ptr(att[bi][0], t * B * E), _ptr(att[bi][1], t * B * E))
-                _lib.check(lib.mrg_gen_linear(1, B, a, r, ga, be, E, a2, ga2, be2, eps, _ptr(y01), 2 * E, w, bias,
-                                              _ptr(z01), 2 * E, st), "gen integrators")
+                with Fn._probe("gen", f_lin1):
+                    _lib.check(lib.mrg_gen_linear(1, B, a, r, ga, be, E, a2, ga2, be2, eps, _ptr(y01), 2 * E, w,
+                                                  bias, _ptr(z01), 2 * E, st), "gen integrators")
                 a, r, ga, be, w, bias = c["lin2"]
-                _lib.check(lib.mrg_gen_linear(2, B, a, r, ga, be, 2 * E, None, None, None, eps, None, 0, w, bias,
-                                              _ptr(m3), E, st), "gen cat_linear")
+                with Fn._probe("gen", f_lin2):
+                    _lib.check(lib.mrg_gen_linear(2, B, a, r, ga, be, 2 * E, None, None, None, eps, None, 0, w, bias,
+                                                  _ptr(m3), E, st), "gen cat_linear")
                 w1, b1, w2, b2 = c["ffn"]
-                _lib.check(lib.mrg_gen_ffn(B, E, _ptr(m3), None, None, None, eps, _ptr(w1), _ptr(b1), _ptr(w2),
-                                           _ptr(b2), _ptr(zf), None, 0, None, None, None, t, st), "gen ffn")
-            _lib.check(lib.mrg_gen_ffn(B, self.fm, _ptr(zf), _ptr(m3), _ptr(lastln.weight), _ptr(lastln.bias), eps,
-                                       _ptr(ow1), _ptr(ob1), _ptr(ow2), _ptr(ob2), None, _ptr(pred), T * self.fm,
-                                       _ptr(ms_in), _ptr(msc[t]), _ptr(mask_u8), t, st), "gen output")
+                with Fn._probe("gen", f_ffn):
+                    _lib.check(lib.mrg_gen_ffn(B, E, _ptr(m3), None, None, None, eps, _ptr(w1), _ptr(b1), _ptr(w2),
+                                               _ptr(b2), _ptr(zf), None, 0, None, None, None, t, st), "gen ffn")
+            with Fn._probe("gen", f_out):
+                _lib.check(lib.mrg_gen_ffn(B, self.fm, _ptr(zf), _ptr(m3), _ptr(lastln.weight), _ptr(lastln.bias),
+                                           eps, _ptr(ow1), _ptr(ob1), _ptr(ow2), _ptr(ob2), None, _ptr(pred),
+                                           T * self.fm, _ptr(ms_in), _ptr(msc[t]), _ptr(mask_u8), t, st),
+                           "gen output")
         return pred
 
 
