@@ -294,6 +294,20 @@ int mrg_gen_ffn(int B, int N, const float* a, const float* r, const float* ga, c
                 const float* w1, const float* b1, const float* w2, const float* b2, float* out, float* pred,
                 long pred_bs, float* ms_next, const float* ms_src, const unsigned char* mask, int t,
                 hipStream_t stream);
+/* The whole frame loop in ONE persistent launch (gen.hip gen_loop_kernel): groups of 8 batch rows,
+ * 16 workgroups per group exchanging each stage's outputs as {tag, value} granules; the same stages
+ * as the three entries above.  ptrs: host array of 31 nb + 6 device pointers -- per block w_ih,
+ * b_ih, b_hh, mixer LayerNorm g / b, mixer Linear w / b, mixer FeedForward LayerNorm g / b, per
+ * integrator i = 0, 1 (attention residual LayerNorm g / b, FeedForward w / b, its LayerNorm g / b),
+ * cat_linear w / b, block FeedForward w1 / b1 / w2 / b2, its LayerNorm g / b, the integrators'
+ * attention outputs a_0 / a_1 [T][B][256]; then feature_embedding.0 w / b and the output FeedForward
+ * w1 / b1 / w2 / b2.  ms [T][B][fm], mask [T] bytes, pred [B][T][fm]; ring: mrg_gen_loop_ring_bytes
+ * of zeroed device memory per launch; err: set when a hand-off poll times out.  mrg_gen_loop_fits:
+ * 1 when the grid (16 ceil(B / 8) workgroups) can be resident on `cus` CUs (0: the device's).   */
+long mrg_gen_loop_ring_bytes(int B);
+int mrg_gen_loop_fits(int B, int cus);
+int mrg_gen_loop(int B, int T, int fm, int nb, float eps, const void* const* ptrs, int nptrs, const float* ms,
+                 const unsigned char* mask, float* pred, void* ring, int* err, hipStream_t stream);
 
 /* ---------------------------------------------------------------- attention
  * Scaled-dot-product core of nn.MultiheadAttention as the reference calls it

@@ -52,6 +52,9 @@ int mrg_debug_busy(int blocks, int threads, int lds, double usec, hipStream_t st
 /* Diagnostics: a 1-thread kernel writing the 100 MHz wall clock into ((uint64*)buf)[slot] in `stream`'s
  * order (tools/side_timing.py: when a replayed graph reaches a point). */
 int mrg_debug_stamp(void* buf, int slot, hipStream_t stream);
+/* Diagnostics: block 0's per-stage shader-clock stamps of later mrg_gen_loop launches ([T][32] u64;
+ * slot 31 of frame 0: the group's local hand-off flag); null turns them off (tools/gen_stamps.py). */
+int mrg_gen_loop_debug_stamps(void* buf);
 /* Measurement (bench.py): while on, every kernel launched for a tagged library call (tag >= 0) is
  * timed by start / stop events bound to that kernel (hipExtLaunchKernelGGL): its own execution,
  * as rocprofv3 reports it.  stop waits, writes (ms, tag) per launch and returns the count. */

@@ -375,6 +375,369 @@ __global__ __launch_bounds__(256) void gen_ffn_kernel(GenFfnArgs p) {
   }
 }
 
+
+// ------------------------------------------------------------------ the whole frame loop, one launch
+// gen_loop_kernel runs every frame of the generation in ONE persistent launch.  Rows are independent
+// (every frame is a zero-state T = 1 forward per batch row), so the batch is cut into groups of 8
+// rows and each group is served by 16 workgroups that own 1/16 of every stage's output columns;
+// stage outputs travel as {tag, value} granules (the recurrences' hand-off, lstm_common.h) through a
+// ring the launch zeroes first, and a member polls the full rows it needs instead of waiting at a
+// kernel boundary.  Members of a group share blockIdx % 8 (one XCD under the round-robin dispatch,
+// checked at launch start: then the granules stay in that XCD's L2).  Full-row intermediates a
+// member needs again (the block input X, Y, Y_0 / Y_1, M3) stay in its LDS.  Per block:
+//   S1 gather Zf -> X = LN(Zf + M3) (block 0: ms_in W_fe^T + b_fe) -> 4 x (4 units x 4 gates) ->
+//      zero-state cell -> publish h
+//   S2 gather h -> Y = LN(h + X) -> Z = Y W^T + b            -> publish Z
+//   S3 gather Z -> M = LN(Z + Y), Y_i = LN(a_i[t] + M) -> Z_i -> publish Z_0 | Z_1
+//   S4 gather Z_0 | Z_1 -> [LN(Z_0 + Y_0) | LN(Z_1 + Y_1)] W_cat^T + b -> publish M3
+//   S5 gather M3 -> relu(M3 W1^T + b1) (all 64, per member) W2^T + b2 -> publish Zf
+// and after the last block every member computes the output FeedForward of its rows itself
+// (LN(Zf + M3) -> 64 -> fm), so the next frame's self motion (the sampling select) needs no exchange;
+// member 0 writes the prediction.  Tag of block k's buffers in frame t: t * nb + k + 1.
+static constexpr int GL_ROWS = 8;     // rows per group (MFMA rows 8..15 are zero)
+static constexpr int GL_MEM = 16;     // workgroups per group
+static constexpr int GL_NBMAX = 5;
+static constexpr int GL_PER_BLOCK = 31;
+
+struct GenLoopBlock {
+  const float* p[GL_PER_BLOCK];       // see mrg_gen_loop for the order
+};
+struct GenLoopArgs {
+  GenLoopBlock blk[GL_NBMAX];
+  const float *fe_w, *fe_b, *ow1, *ob1, *ow2, *ob2;
+  const float* ms;                    // [T][B][fm]
+  const unsigned char* mask;          // [T]
+  float* pred;                        // [B][T][fm]
+  unsigned long long* ring;           // h | z | z01 | m3 | zf granules, then the XCC slots
+  int* err;
+  int B, T, fm, nb, ngroups;
+  float eps;
+  unsigned long long* stamps;         // diagnostics (mrg_gen_loop_debug_stamps): [T][32] of block 0, or null
+};
+
+// block 0 / thread 0: shader-clock stamp `slot` of frame t (slot 31: the group's local-hand-off flag)
+#define GL_STAMP(slot)                                                                     do {                                                                                       if (p.stamps && blockIdx.x == 0 && threadIdx.x == 0) {                                     unsigned long long _t;                                                                   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");             p.stamps[(long)t * 32 + (slot)] = _t;                                                  }                                                                                      } while (0)
+
+enum { GL_WIH, GL_BIH, GL_BHH, GL_L1G, GL_L1B, GL_MW, GL_MB, GL_L2G, GL_L2B,
+       GL_I0, GL_I1 = GL_I0 + 6, GL_CW = GL_I1 + 6, GL_CB, GL_FW1, GL_FB1, GL_FW2, GL_FB2, GL_FLG, GL_FLB,
+       GL_ATT0, GL_ATT1 };   // integrator i: GL_Ii + {0 ln1 g, 1 ln1 b, 2 w, 3 b, 4 ln2 g, 5 ln2 b}
+static_assert(GL_ATT1 + 1 == GL_PER_BLOCK, "gen loop pointer table");
+
+// poll N granules per thread of `width`-wide rows: thread column c = tid + 256 q, rows 0..7; rows at
+// or past B read a valid row's slot and are zeroed
+// (sdead: the workgroup's shared flag, so after one timed-out poll every thread stops polling at its
+// next gather and the launch drains within a frame)
+template <int W>
+__device__ __forceinline__ void gl_gather(unsigned long long* buf, int r0, int B, unsigned tag, float* dst, int ldd,
+                                          int* err, bool& dead, int* sdead) {
+  constexpr int N = GL_ROWS * W / 256;
+  if (*sdead) dead = true;
+  int idx[N];
+  float v[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const int row = i / (W / 256), col = threadIdx.x + 256 * (i % (W / 256));
+    idx[i] = min(r0 + row, B - 1) * W + col;
+  }
+  get_granules_idx<N>(buf, idx, tag, v, err, dead);
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const int row = i / (W / 256), col = threadIdx.x + 256 * (i % (W / 256));
+    dst[row * ldd + col] = r0 + row < B ? v[i] : 0.0f;
+  }
+  if (dead) *sdead = 1;
+}
+
+// A wave's weight fragments of one 16-column tile over its k-quarter (K / 64 float4; with K = 4 E a
+// wave takes the whole E-wide k range of its own tile).  Issued at the start of a stage, before the
+// member polls its inputs, so the weights' memory latency hides under the hand-off wait.
+template <int K>
+struct GlW {
+  float4 v[K / 64];
+};
+template <int K>
+__device__ __forceinline__ void gl_wload(GlW<K>& f, const float* __restrict__ wrow, int wave, int lane) {
+  const float* wr = wrow + wave * (K / 4) + 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < K / 64; ++i) f.v[i] = *reinterpret_cast<const float4*>(wr + 16 * i);
+}
+// acc = A[16][wave's k-quarter] x the fragments (lane l: row / column l & 15, k = 16 i + 4 (l >> 4) + j)
+template <int K>
+__device__ __forceinline__ gv4 gl_mma(const float* A, int lda, const GlW<K>& f, int lane, int wave) {
+  const int m = lane & 15, q = lane >> 4;
+  gv4 acc = gv4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < K / 64; ++i) {
+    const float4 x = *reinterpret_cast<const float4*>(A + m * lda + wave * (K / 4) + 16 * i + 4 * q);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.x, f.v[i].x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.y, f.v[i].y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.z, f.v[i].z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.w, f.v[i].w, acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+// a LayerNorm's gamma / beta for this lane's four columns
+struct GlLn {
+  float4 g, b;
+};
+__device__ __forceinline__ GlLn gl_lnp(const float* __restrict__ g, const float* __restrict__ b, int lane) {
+  return GlLn{gen_ld4(g + 4 * lane), gen_ld4(b + 4 * lane)};
+}
+// LN(a[r] + b[r]) of one row (4 values per lane) into out (and out2 when given)
+__device__ __forceinline__ void gl_ln_row(const float* a, const float* b, const GlLn& p, float eps, float* out,
+                                          float* out2, int lane) {
+  const float4 v = gen_ln(gen_add4(*reinterpret_cast<const float4*>(a + 4 * lane),
+                                   *reinterpret_cast<const float4*>(b + 4 * lane)),
+                          p.g, p.b, eps);
+  *reinterpret_cast<float4*>(out + 4 * lane) = v;
+  if (out2) *reinterpret_cast<float4*>(out2 + 4 * lane) = v;
+}
+
+// the four waves' partial tiles of tile q into red[.][q]
+__device__ __forceinline__ void gl_park(float (*red)[4][16][17], int q, int wave, int lane, gv4 acc) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) red[wave][q][4 * (lane >> 4) + i][lane & 15] = acc[i];
+}
+__device__ __forceinline__ float gl_sum(const float (*red)[4][16][17], int q, int m, int n) {
+  return (red[0][q][m][n] + red[1][q][m][n]) + (red[2][q][m][n] + red[3][q][m][n]);
+}
+
+__global__ __launch_bounds__(256) void gen_loop_kernel(GenLoopArgs p) {
+  constexpr int XP = GE + 4, AP = 2 * GE + 4, HP = GHB + 4;
+  __shared__ __attribute__((aligned(16))) float A[16][AP];      // the stage's product operand (rows 8..15 zero)
+  __shared__ __attribute__((aligned(16))) float Xs[GL_ROWS][XP];
+  __shared__ __attribute__((aligned(16))) float Ys[GL_ROWS][XP];
+  __shared__ __attribute__((aligned(16))) float Y01[GL_ROWS][AP];
+  __shared__ __attribute__((aligned(16))) float M3[GL_ROWS][XP];
+  __shared__ __attribute__((aligned(16))) float hs[16][HP];
+  __shared__ float red[4][4][16][17];
+  __shared__ float msin[GL_ROWS][16];
+  __shared__ int sdead, xflag;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = blockIdx.x % p.ngroups, j = blockIdx.x / p.ngroups;   // group (8 rows), member (1/16 of columns)
+  const int r0 = GL_ROWS * g, B = p.B, T = p.T, fm = p.fm;
+  const float eps = p.eps;
+  unsigned long long* bh = p.ring;
+  unsigned long long* bz = bh + (long)B * GE;
+  unsigned long long* bz01 = bz + (long)B * GE;
+  unsigned long long* bm3 = bz01 + (long)B * 2 * GE;
+  unsigned long long* bzf = bm3 + (long)B * GE;
+  unsigned long long* slots = bzf + (long)B * GE;
+  bool dead = false;
+  for (int i = tid; i < 16 * AP; i += 256) (&A[0][0])[i] = 0.0f;
+  if (tid == 0) sdead = 0;
+  const int local = group_on_one_xcd<GL_MEM>(slots + (long)g * GL_MEM, j, p.err, dead, &xflag);
+  if (tid < GL_ROWS * 16) {   // frame 0's self motion
+    const int m = tid >> 4, f = tid & 15;
+    msin[m][f] = (f < fm && r0 + m < B) ? p.ms[(long)(r0 + m) * fm + f] : 0.0f;
+  }
+  __syncthreads();
+  const int m8 = tid >> 4, n16 = tid & 15;   // epilogue thread -> (row, column of the tile), rows < 8 used
+  const bool ep = tid < GL_ROWS * 16 && r0 + m8 < B;
+  const int nl = lane & 15;                  // this lane's tile column (weight row) in the products
+  if (p.stamps && blockIdx.x == 0 && threadIdx.x == 0) p.stamps[31] = (unsigned long long)local;
+  for (int t = 0; t < T && !sdead; ++t) {
+    GL_STAMP(0);
+    for (int k = 0; k < p.nb; ++k) {
+      const float* const* w = p.blk[k].p;
+      const unsigned tag = (unsigned)(t * p.nb + k + 1);
+      // ---- S1: X, gates of units 16 j .. 16 j + 15 (tile q: units 16 j + 4 q + (n & 3), gate n >> 2), cell
+      {
+        GlW<GE> f[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          gl_wload<GE>(f[q], w[GL_WIH] + (long)((nl >> 2) * GE + 16 * j + 4 * q + (nl & 3)) * GE, wave, lane);
+        float bi = 0.f, bg = 0.f, bo = 0.f;
+        const int u = 16 * j + n16;
+        if (tid < GL_ROWS * 16) {
+          bi = w[GL_BIH][u] + w[GL_BHH][u];
+          bg = w[GL_BIH][2 * GE + u] + w[GL_BHH][2 * GE + u];
+          bo = w[GL_BIH][3 * GE + u] + w[GL_BHH][3 * GE + u];
+        }
+        if (k == 0) {
+          const int c = tid;
+          float acc[GL_ROWS];
+          const float bc = p.fe_b[c];
+#pragma unroll
+          for (int m = 0; m < GL_ROWS; ++m) acc[m] = 0.0f;
+          for (int ff = 0; ff < fm; ++ff) {
+            const float wf = p.fe_w[c * fm + ff];
+#pragma unroll
+            for (int m = 0; m < GL_ROWS; ++m) acc[m] = fmaf(msin[m][ff], wf, acc[m]);
+          }
+#pragma unroll
+          for (int m = 0; m < GL_ROWS; ++m) {
+            const float v = r0 + m < B ? acc[m] + bc : 0.0f;
+            Xs[m][c] = v;
+            A[m][c] = v;
+          }
+        } else {
+          const float* const* wp = p.blk[k - 1].p;
+          const GlLn ln = gl_lnp(wp[GL_FLG], wp[GL_FLB], lane);
+          gl_gather<GE>(bzf, r0, B, tag - 1, &A[0][0], AP, p.err, dead, &sdead);
+          __syncthreads();
+          for (int m = wave; m < GL_ROWS; m += 4) gl_ln_row(A[m], M3[m], ln, eps, Xs[m], A[m], lane);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) gl_park(red, q, wave, lane, gl_mma<GE>(&A[0][0], AP, f[q], lane, wave));
+        __syncthreads();
+        if (ep) {
+          const int q = n16 >> 2, jj = n16 & 3;
+          const float zi = gl_sum(red, q, m8, jj) + bi;
+          const float zg = gl_sum(red, q, m8, 8 + jj) + bg;
+          const float zo = gl_sum(red, q, m8, 12 + jj) + bo;
+          const float c = sigmoidf_(zi) * tanhf_(zg);   // f c0 + i g with c0 = 0
+          put_granule(bh + (long)(r0 + m8) * GE + u, tag, sigmoidf_(zo) * tanhf_(c), local);
+        }
+        GL_STAMP(1 + 5 * k);
+      }
+      // ---- S2: Y = LN(h + X), Z = Y W_m^T + b
+      {
+        GlW<GE> f;
+        gl_wload<GE>(f, w[GL_MW] + (long)(16 * j + nl) * GE, wave, lane);
+        const GlLn ln = gl_lnp(w[GL_L1G], w[GL_L1B], lane);
+        const float bias = w[GL_MB][16 * j + n16];
+        gl_gather<GE>(bh, r0, B, tag, &A[0][0], AP, p.err, dead, &sdead);
+        __syncthreads();
+        for (int m = wave; m < GL_ROWS; m += 4) gl_ln_row(A[m], Xs[m], ln, eps, Ys[m], A[m], lane);
+        __syncthreads();
+        gl_park(red, 0, wave, lane, gl_mma<GE>(&A[0][0], AP, f, lane, wave));
+        __syncthreads();
+        if (ep) put_granule(bz + (long)(r0 + m8) * GE + 16 * j + n16, tag, gl_sum(red, 0, m8, n16) + bias, local);
+        GL_STAMP(2 + 5 * k);
+      }
+      // ---- S3: M = LN(Z + Y), Y_i = LN(a_i + M), Z_i = Y_i W_i^T + b_i
+      {
+        GlW<GE> f[2];
+        GlLn l1[2];
+        float bias[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          gl_wload<GE>(f[i], w[GL_I0 + 6 * i + 2] + (long)(16 * j + nl) * GE, wave, lane);
+          l1[i] = gl_lnp(w[GL_I0 + 6 * i + 0], w[GL_I0 + 6 * i + 1], lane);
+          bias[i] = w[GL_I0 + 6 * i + 3][16 * j + n16];
+        }
+        const GlLn ln = gl_lnp(w[GL_L2G], w[GL_L2B], lane);
+        float4 av[2][2];   // this wave's rows' attention outputs (frame t), loaded before the poll
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+            av[rr][i] = gen_ld4(w[GL_ATT0 + i] + ((long)t * B + min(r0 + wave + 4 * rr, B - 1)) * GE + 4 * lane);
+        gl_gather<GE>(bz, r0, B, tag, &A[0][0], AP, p.err, dead, &sdead);
+        __syncthreads();
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr) {
+          const int m = wave + 4 * rr;
+          const float4 mv = gen_ln(gen_add4(*reinterpret_cast<const float4*>(&A[m][4 * lane]),
+                                            *reinterpret_cast<const float4*>(&Ys[m][4 * lane])),
+                                   ln.g, ln.b, eps);
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const float4 y = gen_ln(gen_add4(av[rr][i], mv), l1[i].g, l1[i].b, eps);
+            *reinterpret_cast<float4*>(&Y01[m][GE * i + 4 * lane]) = y;
+            *reinterpret_cast<float4*>(&A[m][GE * i + 4 * lane]) = y;
+          }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 2; ++i) gl_park(red, i, wave, lane, gl_mma<GE>(&A[0][0] + GE * i, AP, f[i], lane, wave));
+        __syncthreads();
+        if (ep) {
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+            put_granule(bz01 + (long)(r0 + m8) * 2 * GE + GE * i + 16 * j + n16, tag, gl_sum(red, i, m8, n16) + bias[i],
+                        local);
+        }
+        GL_STAMP(3 + 5 * k);
+      }
+      // ---- S4: M3 = [LN(Z_0 + Y_0) | LN(Z_1 + Y_1)] W_cat^T + b
+      {
+        GlW<2 * GE> f;
+        gl_wload<2 * GE>(f, w[GL_CW] + (long)(16 * j + nl) * 2 * GE, wave, lane);
+        GlLn l2[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) l2[i] = gl_lnp(w[GL_I0 + 6 * i + 4], w[GL_I0 + 6 * i + 5], lane);
+        const float bias = w[GL_CB][16 * j + n16];
+        gl_gather<2 * GE>(bz01, r0, B, tag, &A[0][0], AP, p.err, dead, &sdead);
+        __syncthreads();
+        for (int m = wave; m < GL_ROWS; m += 4)
+#pragma unroll
+          for (int i = 0; i < 2; ++i) gl_ln_row(A[m] + GE * i, Y01[m] + GE * i, l2[i], eps, A[m] + GE * i, nullptr, lane);
+        __syncthreads();
+        gl_park(red, 0, wave, lane, gl_mma<2 * GE>(&A[0][0], AP, f, lane, wave));
+        __syncthreads();
+        if (ep) put_granule(bm3 + (long)(r0 + m8) * GE + 16 * j + n16, tag, gl_sum(red, 0, m8, n16) + bias, local);
+        GL_STAMP(4 + 5 * k);
+      }
+      // ---- S5: Zf = relu(M3 W1^T + b1) W2^T + b2 (all 64 hidden columns per member, wave w: 16 w ..)
+      {
+        GlW<4 * GE> f1;
+        gl_wload<4 * GE>(f1, w[GL_FW1] + (long)(16 * wave + nl) * GE, 0, lane);
+        GlW<GHB> f2;
+        gl_wload<GHB>(f2, w[GL_FW2] + (long)(16 * j + nl) * GHB, wave, lane);
+        const int hc = 16 * wave + nl;
+        const float b1 = w[GL_FB1][hc];
+        const float bias = w[GL_FB2][16 * j + n16];
+        gl_gather<GE>(bm3, r0, B, tag, &A[0][0], AP, p.err, dead, &sdead);
+        __syncthreads();
+        for (int i = tid; i < GL_ROWS * GE; i += 256) M3[i / GE][i % GE] = A[i / GE][i % GE];
+        {
+          const gv4 acc = gl_mma<4 * GE>(&A[0][0], AP, f1, lane, 0);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) hs[4 * (lane >> 4) + i][hc] = fmaxf(acc[i] + b1, 0.0f);
+        }
+        __syncthreads();
+        gl_park(red, 0, wave, lane, gl_mma<GHB>(&hs[0][0], HP, f2, lane, wave));
+        __syncthreads();
+        if (ep) put_granule(bzf + (long)(r0 + m8) * GE + 16 * j + n16, tag, gl_sum(red, 0, m8, n16) + bias, local);
+        GL_STAMP(5 + 5 * k);
+      }
+    }
+    // ---- output FeedForward of this group's rows (every member), the sampling select
+    {
+      const float* const* wl = p.blk[p.nb - 1].p;
+      GlW<4 * GE> f1;
+      gl_wload<4 * GE>(f1, p.ow1 + (long)(16 * wave + nl) * GE, 0, lane);
+      // columns past fm multiply zeroed fragments of a clamped (valid) weight row
+      GlW<GHB> f2;
+      gl_wload<GHB>(f2, p.ow2 + (long)(nl < fm ? nl : 0) * GHB, wave, lane);
+      if (nl >= fm) f2.v[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+      const GlLn ln = gl_lnp(wl[GL_FLG], wl[GL_FLB], lane);
+      const int hc = 16 * wave + nl;
+      const float b1 = p.ob1[hc];
+      const float b2 = n16 < fm ? p.ob2[n16] : 0.0f;
+      gl_gather<GE>(bzf, r0, B, (unsigned)(t * p.nb + p.nb), &A[0][0], AP, p.err, dead, &sdead);
+      __syncthreads();
+      for (int m = wave; m < GL_ROWS; m += 4) gl_ln_row(A[m], M3[m], ln, eps, A[m], nullptr, lane);
+      __syncthreads();
+      {
+        const gv4 acc = gl_mma<4 * GE>(&A[0][0], AP, f1, lane, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) hs[4 * (lane >> 4) + i][hc] = fmaxf(acc[i] + b1, 0.0f);
+      }
+      __syncthreads();
+      gl_park(red, 0, wave, lane, gl_mma<GHB>(&hs[0][0], HP, f2, lane, wave));
+      __syncthreads();
+      if (tid < GL_ROWS * 16) {
+        const int b = r0 + m8;
+        float nxt = 0.0f;
+        if (n16 < fm && b < B) {
+          const float y = gl_sum(red, 0, m8, n16) + b2;
+          if (j == 0) p.pred[((long)b * T + t) * fm + n16] = y;
+          nxt = p.mask[t] ? y : p.ms[((long)t * B + b) * fm + n16];
+        }
+        msin[m8][n16] = nxt;
+      }
+      if (dead) sdead = 1;
+      __syncthreads();
+      GL_STAMP(30);
+    }
+  }
+}
+
 }  // namespace mrg
 
 using namespace mrg;
@@ -446,4 +809,55 @@ MRG_API int mrg_gen_ffn(int B, int N, const float* a, const float* r, const floa
   else if (pred) klaunch(gen_ffn_kernel<0, 1>, grid, 256, 0, stream, p);
   else klaunch(gen_ffn_kernel<0, 0>, grid, 256, 0, stream, p);
   return check_launch("gen_ffn_kernel");
+}
+
+static unsigned long long* g_gen_stamps = nullptr;
+// Diagnostics (tools/gen_stamps.py): later mrg_gen_loop launches write block 0's per-stage shader-clock
+// stamps into buf ([T][32] u64; slot 31 of frame 0: the group's local hand-off flag); null = off.
+MRG_API int mrg_gen_loop_debug_stamps(void* buf) {
+  g_gen_stamps = static_cast<unsigned long long*>(buf);
+  return 0;
+}
+
+// Bytes of the granule ring mrg_gen_loop needs (zeroed by the caller before every launch).
+MRG_API long mrg_gen_loop_ring_bytes(int B) {
+  const int ng = (B + GL_ROWS - 1) / GL_ROWS;
+  return ((long)B * 6 * GE + (long)ng * GL_MEM) * 8;
+}
+
+// 1 when the whole persistent grid (16 workgroups per 8 batch rows) can be resident on `cus` CUs.
+MRG_API int mrg_gen_loop_fits(int B, int cus) {
+  const long nblk = (long)GL_MEM * ((B + GL_ROWS - 1) / GL_ROWS);
+  return fits(gen_loop_kernel, 256, nblk, cus > 0 ? cus : device_cus()) ? 1 : 0;
+}
+
+// The whole generation frame loop in one persistent launch (gen_loop_kernel above): nb <= 5 blocks.
+// ptrs (host array, 31 nb + 6 device pointers): per block w_ih, b_ih, b_hh, ln1 g / b (mixer
+// LayerNorm), mixer Linear w / b, ln2 g / b (the mixer FeedForward's LayerNorm), per integrator i
+// (ln1 g / b of the attention residual, FeedForward w / b, ln2 g / b), cat_linear w / b, block
+// FeedForward w1 / b1 / w2 / b2, its LayerNorm g / b, the integrators' attention outputs a_0 / a_1
+// [T][B][256]; then feature_embedding.0 w / b and the output FeedForward w1 / b1 / w2 / b2.
+// ms [T][B][fm] (padding zeroed), mask [T] bytes, pred [B][T][fm]; ring: mrg_gen_loop_ring_bytes of
+// zeroed memory; err: the recurrences' error flag (a hand-off poll that times out sets it).
+MRG_API int mrg_gen_loop(int B, int T, int fm, int nb, float eps, const void* const* ptrs, int nptrs, const float* ms,
+                         const unsigned char* mask, float* pred, void* ring, int* err, hipStream_t stream) {
+  if (B == 0 || T == 0) return 0;
+  MRG_REQUIRE(nb >= 1 && nb <= GL_NBMAX && nptrs == GL_PER_BLOCK * nb + 6 && fm >= 1 && fm <= 16 && ptrs && ms &&
+                  mask && pred && ring && err,
+              "mrg_gen_loop: bad arguments (B=%d nb=%d fm=%d nptrs=%d)", B, nb, fm, nptrs);
+  MRG_REQUIRE(mrg_gen_loop_fits(B, 0) == 1, "mrg_gen_loop: %d workgroups cannot all be resident (B=%d)",
+              GL_MEM * ((B + GL_ROWS - 1) / GL_ROWS), B);
+  GenLoopArgs a{};
+  for (int k = 0; k < nb; ++k)
+    for (int i = 0; i < GL_PER_BLOCK; ++i) {
+      a.blk[k].p[i] = static_cast<const float*>(ptrs[k * GL_PER_BLOCK + i]);
+      MRG_REQUIRE(a.blk[k].p[i] != nullptr, "mrg_gen_loop: null pointer %d of block %d", i, k);
+    }
+  const float* const* gp = reinterpret_cast<const float* const*>(ptrs + GL_PER_BLOCK * nb);
+  a.fe_w = gp[0]; a.fe_b = gp[1]; a.ow1 = gp[2]; a.ob1 = gp[3]; a.ow2 = gp[4]; a.ob2 = gp[5];
+  a.ms = ms; a.mask = mask; a.pred = pred; a.ring = static_cast<unsigned long long*>(ring); a.err = err;
+  a.B = B; a.T = T; a.fm = fm; a.nb = nb; a.ngroups = (B + GL_ROWS - 1) / GL_ROWS; a.eps = eps;
+  a.stamps = g_gen_stamps;
+  klaunch(gen_loop_kernel, dim3(GL_MEM * a.ngroups), 256, 0, stream, a);
+  return check_launch("gen_loop_kernel");
 }

@@ -24,6 +24,7 @@ runs the per-frame module forward.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional
 
 import torch
@@ -35,6 +36,9 @@ from .functional import _ptr, _stream
 
 F32 = torch.float32
 E_GEN, HB_GEN = 256, 64
+# the whole frame loop as ONE persistent launch (gen.hip gen_loop_kernel) when its grid fits;
+# MRG_GEN_LOOP=0 keeps the 26 launches per frame
+_LOOP = [os.environ.get("MRG_GEN_LOOP", "1") == "1"]
 
 
 def _arr(*ts):
@@ -136,6 +140,8 @@ class GenPlan:
         y01, z01 = (torch.empty(B, 2 * E, device=dev, dtype=F32) for _ in range(2))
         st = _stream()
         fe0 = self.fe[0]
+        if _LOOP[0] and lib.mrg_gen_loop_fits(B, _lib.cu_count(dev.index or 0)) == 1:
+            return self._generate_loop(lib, B, T, att, msc, mask_u8, pred, st)
         # argument tuples made once (the frame loop only varies the frame pointers)
         calls = []
         for bi, blk in enumerate(self.blocks):
@@ -194,6 +200,31 @@ class GenPlan:
                                            eps, _ptr(ow1), _ptr(ob1), _ptr(ow2), _ptr(ob2), None, _ptr(pred),
                                            T * self.fm, _ptr(ms_in), _ptr(msc[t]), _ptr(mask_u8), t, st),
                            "gen output")
+        return pred
+
+    def _generate_loop(self, lib, B, T, att, msc, mask_u8, pred, st):
+        """The frame loop in one persistent launch (mrg_gen_loop; pointer table order in include/mrg.h)."""
+        ptrs = []
+        for bi, blk in enumerate(self.blocks):
+            w_ih, _w_hh, b_ih, b_hh, l1w, l1b, fw, fbias, l2w, l2b = blk["lstm"]
+            i0, i1 = blk["integ"]
+            cw, cb = blk["cat"]
+            w1, b1, w2, b2, fln = blk["ffn"]
+            ptrs += [w_ih, b_ih, b_hh, l1w, l1b, fw, fbias, l2w, l2b]
+            for ip in (i0, i1):
+                ptrs += [ip[4], ip[5], ip[6], ip[7], ip[8], ip[9]]
+            ptrs += [cw, cb, w1, b1, w2, b2, fln.weight, fln.bias, att[bi][0], att[bi][1]]
+        ow1, ob1, ow2, ob2, _ = self.out
+        fe0 = self.fe[0]
+        ptrs += [fe0.weight, fe0.bias, ow1, ob1, ow2, ob2]
+        ring = Fn.zeros(max(1, lib.mrg_gen_loop_ring_bytes(B) // 8), dtype=torch.int64, device=msc.device)
+        E = E_GEN
+        flop = T * (len(self.blocks) * 2.0 * B * (4 * E * E + E * E + 2 * E * E + 2 * E * E + 2 * HB_GEN * E)
+                    + 2.0 * B * HB_GEN * (E + self.fm))
+        with Fn._probe("gen", flop):
+            _lib.check(lib.mrg_gen_loop(B, T, self.fm, len(self.blocks), self.eps, _arr(*ptrs), len(ptrs), _ptr(msc),
+                                        _ptr(mask_u8), _ptr(pred), _ptr(ring), _ptr(Fn._err_flag(msc.device)), st),
+                       "gen loop")
         return pred
 
 

@@ -956,14 +956,18 @@ def test_feature_input_gradient_vs_oracle():
         assert rel_err(gb[i][0].grad, cb[i][0].grad) < TOL, i
 
 
-@pytest.mark.parametrize("B,T", [(37, 25), (64, 12)])
-def test_generation_fused_frame_loop_matches_module_path(B, T):
+@pytest.mark.parametrize("loop", [True, False])
+@pytest.mark.parametrize("B,T", [(37, 25), (64, 12), (3, 9)])
+def test_generation_fused_frame_loop_matches_module_path(B, T, loop):
     """The fused frame loop (generate.py / gen.hip: other modalities' encoders and the one-key attention
-    outputs hoisted over all frames, 26 launches per frame) vs the per-frame module forward the
-    grad-enabled path runs, on ragged padded inputs (B not a multiple of the kernels' 16-row tiles)
-    under a scheduled-sampling mask: the predictions agree within fp32 reordering.
+    outputs hoisted over all frames; loop=True: the whole loop as one persistent launch with granule
+    hand-offs between 16 workgroups per 8 rows, False: 26 launches per frame) vs the per-frame module
+    forward the grad-enabled path runs, on ragged padded inputs (B not a multiple of the kernels' row
+    tiles) under a scheduled-sampling mask: the predictions agree within fp32 reordering.
     Reference: lstmformer.py:426-547."""
     from multimodalreactiongeneration_amd import configs as C
+    from multimodalreactiongeneration_amd import functional as Fn
+    from multimodalreactiongeneration_amd import generate as G
     from multimodalreactiongeneration_amd.generate import plan_for
     from multimodalreactiongeneration_amd.model import Metaformer
     from multimodalreactiongeneration_amd.synthetic import make_batch
@@ -975,10 +979,16 @@ def test_generation_fused_frame_loop_matches_module_path(B, T):
     lengths[1] = T - 4
     batch = make_batch(B=B, T=T, lead=12, seed=5, lengths=lengths, device=DEV)
     mask = torch.from_numpy(np.random.RandomState(9).rand(T) < 0.5).to(DEV)
-    with torch.no_grad():
-        fast = m._generate(batch, sampling_mask=mask)
+    prev = G._LOOP[0]
+    G._LOOP[0] = loop
+    try:
+        with torch.no_grad():
+            fast = m._generate(batch, sampling_mask=mask)
+    finally:
+        G._LOOP[0] = prev
     with torch.enable_grad():
         slow = m._generate(batch, sampling_mask=mask).detach()
     torch.cuda.synchronize()
+    Fn.check_errors()
     assert fast.shape == slow.shape == (B, T, 6)
     assert rel_err(fast, slow) < 1e-5, rel_err(fast, slow)
