@@ -29,12 +29,6 @@ int mrg_gemm_set_wide(int cfg);
  * (sample, head); D = 64, Tq <= 320, 16-B rows) where it applies, 0 = always the two-pass dQ, dK / dV
  * kernels; returns the previous setting.                                                           */
 int mrg_attention_set_fused(int on);
-/* Diagnostics: block 0 of gemm_x6r_kernel records per-wave s_memtime stamps into buf ([waves][16] u64: start,
- * B slice resident, each row block's start, end); null disables.  Never in timed runs.              */
-int mrg_gemm_debug_stamps(void* buf);
-/* Timing only: gemm_x6r_kernel structural variants (1 no epilogue stores, 2 no split, 3 no B reads, 4 no
- * MFMA; outputs meaningless); 0 = the real kernel.  Returns the previous setting.                   */
-int mrg_gemm_x6r_debug(int v);
 /* Tuning only: force the tile shape (0: 128x128, 1: 128x64, 2: 64x64), -1 = heuristic. */
 int mrg_gemm_force_tile(int tile);
 /* Tuning only: structural variants of the x6 kernel (0 product, 1 split + one MFMA, 2 plane-0 +

@@ -43,8 +43,6 @@ SIGNATURES = {
     "mrg_gemm_set_wide": (c_int, [c_int]),
     "mrg_gemm_x6_planes_batched": (c_int, [c_int, c_int, c_int, c_int, c_float, P, c_long, P, c_long, c_long, c_float,
                                            P, c_long, P, c_int, P, c_long, P]),
-    "mrg_gemm_debug_stamps": (c_int, [P]),
-    "mrg_gemm_x6r_debug": (c_int, [c_int]),
     "mrg_gemm_x6_planes": (c_int, [c_int, c_int, c_int, c_float, P, c_long, c_long, c_int, P, c_long, c_long,
                                    c_float, P, c_long, P, c_int, P, c_long, P]),
     "mrg_lstm_set_blocks_per_cu": (c_int, [c_int]),

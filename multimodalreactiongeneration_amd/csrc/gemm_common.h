@@ -151,7 +151,6 @@ void launch_x6g_wgrad(GemmArgs a, int splits, int bm, int bn, hipStream_t s, int
 void launch_x6w(GemmArgs a, int bn, int ns, long bplane, hipStream_t s, const GemmBatch* gb = nullptr);
 // B-resident form (gemm_wide.hip) for K in {128, 256}: one workgroup of `waves` waves per CU; returns -1
 // when K is not supported
-int launch_x6r(GemmArgs a, long bplane, hipStream_t s, int waves);
 
 static constexpr int MRG_TP_MAX = 32;
 struct TransposeBatch {

@@ -642,8 +642,6 @@ MRG_API int mrg_gemm_x6_planes(int M, int N, int K, float alpha, const float* A,
   a.kchunk = K;
   a.vec = ((((uintptr_t)C | (uintptr_t)bias | (uintptr_t)aux) & 15) == 0 && (ldc & 3) == 0 &&
            (!aux || (ldaux & 3) == 0)) ? 1 : 0;
-  if ((g_wide_cfg == 4 || g_wide_cfg == 8) && launch_x6r(a, bplane, stream, g_wide_cfg) == 0)
-    return check_launch("gemm_x6r_kernel");
   if (g_wide_cfg > 8) {   // row-owning kernel (gemm_wide.hip); cfg = 10 * bn / 64 + ns, 0 = the kernel below
     const int bn = N <= 64 ? 64 : 64 * (g_wide_cfg / 10), ns = g_wide_cfg % 10;
     launch_x6w(a, bn, ns, bplane, stream);
@@ -695,19 +693,11 @@ MRG_API int mrg_gemm_x6_planes_batched(int n, int M, int N, int K, float alpha, 
   return check_launch("gemm_x6w_kernel (batched)");
 }
 
-namespace mrg { int x6r_debug_stamps(void* buf); extern int g_x6r_dbg; }
-// Timing only: gemm_x6r_kernel structural variants (1 no epilogue stores, 2 no split, 3 no B reads,
-// 4 no MFMA; outputs meaningless), 0 = the real kernel.  Returns the previous setting.
-MRG_API int mrg_gemm_x6r_debug(int v) { const int p = mrg::g_x6r_dbg; mrg::g_x6r_dbg = v; return p; }
-// Diagnostics: gemm_x6r_kernel's block 0 records s_memtime stamps per wave into buf ([waves][16] u64:
-// start, B resident, each row block's start, end); null disables.  Never in timed runs.
-MRG_API int mrg_gemm_debug_stamps(void* buf) { return mrg::x6r_debug_stamps(buf); }
-
 // Tuning: which kernel mrg_gemm_x6_planes runs (0 = gemm_x6g_kernel with pre-split B; 10 * (bn / 64) + ns =
 // gemm_x6w_kernel with bn columns and ring depth ns); returns the previous setting.
 MRG_API int mrg_gemm_set_wide(int cfg) {
   const int prev = g_wide_cfg;
-  if (cfg == 0 || cfg == 4 || cfg == 8 || cfg == 12 || cfg == 13 || cfg == 22 || cfg == 23 || cfg == 42)
+  if (cfg == 0 || cfg == 12 || cfg == 13 || cfg == 22 || cfg == 23 || cfg == 42)
     g_wide_cfg = cfg;
   return prev;
 }

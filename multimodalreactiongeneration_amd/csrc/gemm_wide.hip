@@ -181,220 +181,6 @@ __global__ __launch_bounds__(256, 2) void gemm_x6w_kernel(GemmArgs a_in, long bp
   }
 }
 
-// ----------------------------------------------------------------------------------------------
-// B-resident form for K <= 256 (most of the step's products: K = H = 256): the grid is one
-// workgroup per CU; workgroup (slice, range) holds the planes of a 64-column slice of B for the whole
-// K in LDS (3 x 64 x K bf16 = 96 KB at K = 256, loaded once by LDS-DMA) and walks the 16-row blocks
-// of its row range; a wave owns whole row blocks, loads their A fragments straight from memory into
-// registers (a lane's 8 consecutive k are 32 contiguous bytes; no LDS for A, the next block's loads in
-// flight during this block's MFMAs), splits each once and multiplies it with the 4 column blocks'
-// resident planes.  The LDS-DMA ring of gemm_x6w_kernel moved B (3 x BN x 64 B per k-tile per
-// 64-row tile) on every tile: ~115 MB through LDS-DMA for a 19200 x 256 x 256 product, which bounds
-// it; here B crosses once per workgroup (24 MB for the whole grid).
-//   B plane row n (64 B per 32 k), 16-B chunk c at n * 2K + ((c ^ (n & 15)) << 4): a fragment read
-//   (16 rows at chunks 4 kt + (l >> 4)) hits 16 distinct bank quads in every ds_read_b128 lane group
-//   (rows' low 4 bits XORed into the chunk; needs >= 16 chunks per row, i.e. K >= 128).
-__device__ unsigned long long* g_x6r_stamps = nullptr;   // diagnostics (mrg_gemm_debug_stamps)
-
-template <int NK, int NW, int DBG = 0>
-__global__ __launch_bounds__(64 * NW, 1) void gemm_x6r_kernel(GemmArgs a, long bplane, int nslice, int nrange) {
-  unsigned long long* const stamps = (blockIdx.x == 0 && (threadIdx.x & 63) == 0) ? g_x6r_stamps : nullptr;
-  int nst = 0;
-  auto stamp = [&]() {
-    if (stamps && nst < 16) stamps[(threadIdx.x >> 6) * 16 + nst++] = __builtin_amdgcn_s_memtime();
-  };
-  stamp();
-  constexpr int SW = 64;                        // columns per slice
-  constexpr int K = 32 * NK;
-  constexpr int RP = 2 * K;                     // bytes per plane row
-  constexpr int PL = SW * RP;                   // bytes per plane
-  constexpr int CPR = K / 8;                    // 16-B chunks per plane row
-  constexpr int RPP = 64 / CPR;                 // plane rows per 1-KB DMA piece
-  constexpr int NPC = 3 * PL / 1024;            // pieces
-  constexpr int PITCH = SW + 4;                 // epilogue staging row pitch (floats)
-  static_assert(CPR >= 16 && NPC % NW == 0, "gemm_x6r: K in {128, 256}");
-  __shared__ __attribute__((aligned(16))) unsigned char lds[3 * PL + NW * 16 * PITCH * 4];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int slice = t % nslice, range = t / nslice;
-  if (range >= nrange) return;
-  const int n0 = slice * SW;
-  const int mb = (a.M + 15) / 16;                                  // 16-row blocks
-  const int b0 = (int)((long)mb * range / nrange), b1 = (int)((long)mb * (range + 1) / nrange);
-
-  const int lr = lane & 15, lq = lane >> 4;
-  // A streams k-tile by k-tile through a 4-slot register ring (k-tile kt of any block sits in slot kt % 4):
-  // k-tile kt + PD is requested while k-tile kt multiplies (and k-tile kt + 1 is split), so the A reads
-  // spread over the kernel instead of bursting at its start
-  constexpr int PD = 4;
-  f32x4w ar[4][2];
-  auto load_a = [&](int blk, int kt) {
-    const float* ap = a.A + a.amap.off(min(16 * blk + lr, a.M - 1)) + 8 * lq + 32 * kt;
-    ar[kt & 3][0] = *reinterpret_cast<const f32x4w*>(ap);
-    ar[kt & 3][1] = *reinterpret_cast<const f32x4w*>(ap + 4);
-  };
-  if (b0 + wave < b1) {   // the first block's first k-tiles travel while the B slice loads
-#pragma unroll
-    for (int kt = 0; kt < PD; ++kt) load_a(b0 + wave, kt);
-  }
-  // B slice planes -> LDS (every wave its share of the pieces)
-  {
-    const __bf16* pb = reinterpret_cast<const __bf16*>(a.B);
-#pragma unroll
-    for (int i = 0; i < NPC / NW; ++i) {
-      const int pc = wave * (NPC / NW) + i;
-      const int p = pc / (PL / 1024), pr = pc % (PL / 1024);
-      const int row = pr * RPP + lane / CPR, slot = lane % CPR, chunk = slot ^ (row & 15);
-      const __bf16* s = pb + p * bplane + (long)min(n0 + row, a.N - 1) * a.bmap.ld_lo + 8 * chunk;
-      __builtin_amdgcn_global_load_lds((const void*)s,
-                                       (__attribute__((address_space(3))) void*)(lds + p * PL + pc % (PL / 1024) * 1024),
-                                       16, 0, 0);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  stamp();
-
-  float* stg = reinterpret_cast<float*>(lds + 3 * PL) + wave * 16 * PITCH;
-  const unsigned lds_base = (unsigned)(uintptr_t)((__attribute__((address_space(3))) unsigned char*)lds);
-  // B fragment addresses: lane row lr of column block j, chunk 4 kt + lq swizzled by lr; the plane and
-  // column-block parts are constant offsets, so a k-tile's 12 reads share one per-lane address
-  unsigned xo[NK];
-#pragma unroll
-  for (int kt = 0; kt < NK; ++kt) xo[kt] = lds_base + lr * RP + (((4 * kt + lq) ^ lr) << 4);
-  // three plane fragments of column block j at k-tile kt (untracked reads: the caller waits)
-  auto read_b = [&](int kt, int j, f32x4w (&r)[3]) {
-    if constexpr (DBG == 3) {   // timing only: no B fragment reads
-      r[0] = r[1] = r[2] = f32x4w{(float)kt, (float)j, 1.f, 2.f};
-      return;
-    }
-#pragma unroll
-    for (int p = 0; p < 3; ++p) {
-      const unsigned addr = xo[kt] + p * PL + 16 * j * RP;
-      asm volatile("ds_read_b128 %0, %1" : "=v"(r[p]) : "v"(addr) : "memory");
-    }
-  };
-  auto block = [&](int blk, int nb) {
-    stamp();
-    f32x4w acc[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] = f32x4w{0.f, 0.f, 0.f, 0.f};
-    // reads run RD (k-tile, column block) steps ahead of the MFMAs through a ring of RD + 1 fragment sets;
-    // the A split of k-tile kt + 1 is formed during k-tile kt's products
-    constexpr int RD = 3, NSTEP = 4 * NK;
-    f32x4w rb[RD + 1][3];
-#pragma unroll
-    for (int q = 0; q < RD; ++q) read_b(q >> 2, q & 3, rb[q]);
-    bf16x8 fa[2][3];
-    wsplit8(ar[0][0], ar[0][1], fa[0]);
-#pragma unroll
-    for (int st = 0; st < NSTEP; ++st) {
-      const int kt = st >> 2, j = st & 3;
-      if (st + RD < NSTEP) {
-        read_b((st + RD) >> 2, (st + RD) & 3, rb[(st + RD) % (RD + 1)]);
-        asm volatile("s_waitcnt lgkmcnt(9)" : "+v"(rb[st % (RD + 1)][0]), "+v"(rb[st % (RD + 1)][1]),
-                     "+v"(rb[st % (RD + 1)][2])::"memory");
-      } else if (st + 2 < NSTEP) {
-        asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(rb[st % (RD + 1)][0]), "+v"(rb[st % (RD + 1)][1]),
-                     "+v"(rb[st % (RD + 1)][2])::"memory");
-      } else if (st + 1 < NSTEP) {
-        asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(rb[st % (RD + 1)][0]), "+v"(rb[st % (RD + 1)][1]),
-                     "+v"(rb[st % (RD + 1)][2])::"memory");
-      } else {
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(rb[st % (RD + 1)][0]), "+v"(rb[st % (RD + 1)][1]),
-                     "+v"(rb[st % (RD + 1)][2])::"memory");
-      }
-      if (j == 1) {   // next k-tile's A: prefetch PD + 1 ahead, split it while this k-tile multiplies
-        const int kp = kt + PD;   // into the slot of k-tile kt, split one k-tile ago
-        if (kp < NK) load_a(blk, kp);
-        else if (nb >= 0) load_a(nb, kp - NK);
-        if (kt + 1 < NK) {
-          if constexpr (DBG == 2) {
-            fa[(kt + 1) & 1][0] = __builtin_bit_cast(bf16x8, ar[(kt + 1) & 3][0]);
-            fa[(kt + 1) & 1][1] = __builtin_bit_cast(bf16x8, ar[(kt + 1) & 3][1]);
-            fa[(kt + 1) & 1][2] = fa[(kt + 1) & 1][0];
-          } else {
-            wsplit8(ar[(kt + 1) & 3][0], ar[(kt + 1) & 3][1], fa[(kt + 1) & 1]);
-          }
-        }
-      }
-      if constexpr (DBG == 4) {   // timing only: no MFMA
-        acc[j] += rb[st % (RD + 1)][0] + rb[st % (RD + 1)][1] + rb[st % (RD + 1)][2];
-        continue;
-      }
-      acc[j] = wmfma6(fa[kt & 1], __builtin_bit_cast(bf16x8, rb[st % (RD + 1)][0]),
-                      __builtin_bit_cast(bf16x8, rb[st % (RD + 1)][1]), __builtin_bit_cast(bf16x8, rb[st % (RD + 1)][2]),
-                      acc[j]);
-    }
-    // epilogue: 16 x 64 through the wave's staging rows, then 16-B row pieces through store4
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) stg[(4 * lq + i) * PITCH + 16 * j + lr] = acc[j][i];
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int qq = lane + 64 * it, row = qq >> 4, c4 = qq & 15;
-      const float4 o = *reinterpret_cast<const float4*>(stg + row * PITCH + 4 * c4);
-      const int m = 16 * blk + row, n = n0 + 4 * c4;
-      if (DBG == 1) {   // timing only: no epilogue stores
-        if (o.x == 1.2345f) a.C[0] = o.y;
-        continue;
-      }
-      if (m < a.M && n < a.N) store4(a, 0, m, n, o);
-    }
-    __builtin_amdgcn_wave_barrier();
-  };
-  for (int blk = b0 + wave; blk < b1; blk += NW) {
-    const int nb = blk + NW < b1 ? blk + NW : -1;
-    block(blk, nb);
-  }
-  stamp();
-}
-
-int x6r_debug_stamps(void* buf) {
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_x6r_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
-}
-
-int g_x6r_dbg = 0;   // timing-only structural variants (mrg_gemm_x6r_debug)
-
-// B-resident launch: one workgroup per CU (grid = slices x ranges <= the CU count)
-static int g_cu_count = 0;
-int launch_x6r(GemmArgs a, long bplane, hipStream_t s, int waves) {
-  if (!g_cu_count) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&g_cu_count, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      g_cu_count = 256;
-  }
-  const int nslice = (a.N + 63) / 64;
-  int nrange = g_cu_count / nslice;
-  if (nrange < 1) nrange = 1;
-  const int mb = (a.M + 15) / 16;
-  if (nrange > mb) nrange = mb;
-  const unsigned grid = (unsigned)(nslice * nrange);
-  if (a.K == 256 && g_x6r_dbg > 0) {
-    switch (g_x6r_dbg) {
-      case 1: klaunch(gemm_x6r_kernel<8, 8, 1>, grid, 512, 0, s, a, bplane, nslice, nrange); break;
-      case 2: klaunch(gemm_x6r_kernel<8, 8, 2>, grid, 512, 0, s, a, bplane, nslice, nrange); break;
-      case 3: klaunch(gemm_x6r_kernel<8, 8, 3>, grid, 512, 0, s, a, bplane, nslice, nrange); break;
-      default: klaunch(gemm_x6r_kernel<8, 8, 4>, grid, 512, 0, s, a, bplane, nslice, nrange); break;
-    }
-    return 0;
-  }
-  if (a.K == 256) {
-    if (waves == 8) klaunch(gemm_x6r_kernel<8, 8>, grid, 512, 0, s, a, bplane, nslice, nrange);
-    else klaunch(gemm_x6r_kernel<8, 4>, grid, 256, 0, s, a, bplane, nslice, nrange);
-  } else if (a.K == 128) {
-    if (waves == 8) klaunch(gemm_x6r_kernel<4, 8>, grid, 512, 0, s, a, bplane, nslice, nrange);
-    else klaunch(gemm_x6r_kernel<4, 4>, grid, 256, 0, s, a, bplane, nslice, nrange);
-  } else {
-    return -1;
-  }
-  return 0;
-}
-
 template <int BN, int NS>
 static void launch_w(GemmArgs a, long bplane, hipStream_t s, const GemmBatch& gb) {
   a.tiles_n = (a.N + BN - 1) / BN;

@@ -34,7 +34,7 @@ def test_boundary_header_holds_no_tuning_hooks():
     tuning = set(_header_functions(("mrg_tuning.h",)))
     assert not boundary & tuning
     for name in ("mrg_gemm_x6_variant", "mrg_gemm_force_tile", "mrg_ssd_gate_cell_fwd_dbg", "mrg_gemm_set_wide",
-                 "mrg_gemm_x6r_debug", "mrg_lstm_debug_inject", "mrg_lstm_debug_stamps", "mrg_probe_start"):
+                 "mrg_lstm_debug_inject", "mrg_lstm_debug_stamps", "mrg_probe_start"):
         assert name in tuning and name not in boundary, name
     for name in ("mrg_split_planes_batched", "mrg_gemm_x6_planes", "mrg_gemm_x6_planes_batched"):
         assert name in boundary, name

@@ -1211,9 +1211,8 @@ def test_batched_gemm_matches_single_products(M, N, K, epi, n, gemm_mode):
                                             (6400, 256, 128, 3, 1.0), (1000, 200, 256, 1, 0.0)])
 def test_weight_plane_products_every_kernel(M, N, K, epi, beta):
     """C = epi(A W^T + beta C + bias) on W's pre-split bf16 planes (mrg_gemm_x6_planes) through each kernel
-    mrg_gemm_set_wide selects: the LDS-DMA tile kernel (0), the B-resident kernel (gemm_x6r_kernel, 4 / 8
-    waves, K in {128, 256}; other K fall through to the next form) and the row-owning ring kernel
-    (gemm_x6w_kernel, 64 / 128 columns), vs fp64: every epilogue, accumulation into C, ragged M and N."""
+    mrg_gemm_set_wide selects: the LDS-DMA tile kernel (0) and the row-owning ring kernel (gemm_x6w_kernel,
+    64 / 128 columns), vs fp64: every epilogue, accumulation into C, ragged M and N."""
     import ctypes
     from multimodalreactiongeneration_amd import _lib as L
     from multimodalreactiongeneration_amd import functional as Fn
@@ -1237,7 +1236,7 @@ def test_weight_plane_products_every_kernel(M, N, K, epi, beta):
         exact = exact + aux.double()
     prev = lib.mrg_gemm_set_wide(0)
     try:
-        for cfg in (0, 4, 8, 12, 22):
+        for cfg in (0, 12, 22):
             lib.mrg_gemm_set_wide(cfg)
             C = C0.clone()
             L.check(lib.mrg_gemm_x6_planes(M, N, K, 1.0, VP(A.data_ptr()), K, 0, 0, VP(planes.data_ptr()), K, N * K,

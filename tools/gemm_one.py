@@ -21,7 +21,6 @@ st = VP(torch.cuda.current_stream().cuda_stream)
 _lib.check(lib.mrg_split_planes_batched(1, (VP * 1)(Fn._ptr(B)), (VP * 1)(VP(planes.data_ptr())), (CI * 1)(N),
                                         (CI * 1)(K), (CI * 1)(0), st), "split")
 lib.mrg_gemm_set_wide(cfg)
-lib.mrg_gemm_x6r_debug(int(os.environ.get("DBG", "0")))
 for _ in range(iters):
     _lib.check(lib.mrg_gemm_x6_planes(M, N, K, 1.0, Fn._ptr(A), K, 0, 0, VP(planes.data_ptr()), K, N * K, 0.0,
                                       Fn._ptr(C), N, None, 0, None, 0, st), "planes")
