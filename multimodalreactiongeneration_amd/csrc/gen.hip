@@ -25,14 +25,11 @@
 // workgroup writes its share of the normalised rows the next stage needs as a residual.
 // Products on v_mfma_f32_16x16x4_f32 (exact fp32 multiply-adds; the k order differs from the
 // training kernels', fp32 class).  E = 256, FeedForward bottleneck 64 (the lstmformer config).
-#include "lstm_common.h"
+#include "gen_loop.h"
 
 namespace mrg {
 
-typedef float gv4 __attribute__((ext_vector_type(4)));
 static constexpr int GR = 16;    // batch rows per workgroup
-static constexpr int GE = 256;   // model width
-static constexpr int GHB = 64;   // FeedForward bottleneck
 
 struct GenLstmArgs {
   int B, fm;
@@ -90,31 +87,6 @@ struct GenFfnArgs {
   int t;
 };
 
-// whole-wave sum: DPP within each 16-lane row (no LDS traffic), then the four row sums read out
-__device__ __forceinline__ float gen_wave_sum(float v) {
-  // (readlane moves 32-bit integers: the float travels as its bit pattern)
-  const int u = __float_as_int(group_sum<16>(v));
-  return (__int_as_float(__builtin_amdgcn_readlane(u, 0)) + __int_as_float(__builtin_amdgcn_readlane(u, 16))) +
-         (__int_as_float(__builtin_amdgcn_readlane(u, 32)) + __int_as_float(__builtin_amdgcn_readlane(u, 48)));
-}
-
-// LayerNorm of a 256-wide row held as 4 consecutive values per lane, two-pass (torch.layer_norm:
-// mean, then the mean of squared deviations, biased), eps inside the root; gg / bb: the lane's four
-// gamma / beta values (loaded at kernel start, so their latency hides under the activation loads)
-__device__ __forceinline__ float4 gen_ln(float4 v, float4 gg, float4 bb, float eps) {
-  const float mean = gen_wave_sum((v.x + v.y) + (v.z + v.w)) * (1.0f / GE);
-  const float dx = v.x - mean, dy = v.y - mean, dz = v.z - mean, dw = v.w - mean;
-  const float var = gen_wave_sum((dx * dx + dy * dy) + (dz * dz + dw * dw)) * (1.0f / GE);
-  const float rs = rsqrtf(var + eps);
-  return make_float4(fmaf(dx * rs, gg.x, bb.x), fmaf(dy * rs, gg.y, bb.y), fmaf(dz * rs, gg.z, bb.z),
-                     fmaf(dw * rs, gg.w, bb.w));
-}
-
-__device__ __forceinline__ float4 gen_ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
-__device__ __forceinline__ float4 gen_add4(float4 a, float4 b) {
-  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
-}
-__device__ __forceinline__ float4 gen_zero4() { return make_float4(0.f, 0.f, 0.f, 0.f); }
 
 // acc[16 rows x 16 cols] += X[16][k0:k0+NK] W[n][k0:k0+NK]^T on v_mfma_f32_16x16x4_f32: lane l
 // supplies row / column l & 15 at k = kb + 4 (l >> 4) + j for the j-th product of a 16-k group, so
@@ -394,8 +366,6 @@ __global__ __launch_bounds__(256) void gen_ffn_kernel(GenFfnArgs p) {
 // and after the last block every member computes the output FeedForward of its rows itself
 // (LN(Zf + M3) -> 64 -> fm), so the next frame's self motion (the sampling select) needs no exchange;
 // member 0 writes the prediction.  Tag of block k's buffers in frame t: t * nb + k + 1.
-static constexpr int GL_ROWS = 8;     // rows per group (MFMA rows 8..15 are zero)
-static constexpr int GL_MEM = 16;     // workgroups per group
 static constexpr int GL_NBMAX = 5;
 static constexpr int GL_PER_BLOCK = 31;
 
@@ -423,85 +393,6 @@ enum { GL_WIH, GL_BIH, GL_BHH, GL_L1G, GL_L1B, GL_MW, GL_MB, GL_L2G, GL_L2B,
        GL_ATT0, GL_ATT1 };   // integrator i: GL_Ii + {0 ln1 g, 1 ln1 b, 2 w, 3 b, 4 ln2 g, 5 ln2 b}
 static_assert(GL_ATT1 + 1 == GL_PER_BLOCK, "gen loop pointer table");
 
-// poll N granules per thread of `width`-wide rows: thread column c = tid + 256 q, rows 0..7; rows at
-// or past B read a valid row's slot and are zeroed
-// (sdead: the workgroup's shared flag, so after one timed-out poll every thread stops polling at its
-// next gather and the launch drains within a frame)
-template <int W>
-__device__ __forceinline__ void gl_gather(unsigned long long* buf, int r0, int B, unsigned tag, float* dst, int ldd,
-                                          int* err, bool& dead, int* sdead) {
-  constexpr int N = GL_ROWS * W / 256;
-  if (*sdead) dead = true;
-  int idx[N];
-  float v[N];
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    const int row = i / (W / 256), col = threadIdx.x + 256 * (i % (W / 256));
-    idx[i] = min(r0 + row, B - 1) * W + col;
-  }
-  get_granules_idx<N>(buf, idx, tag, v, err, dead);
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    const int row = i / (W / 256), col = threadIdx.x + 256 * (i % (W / 256));
-    dst[row * ldd + col] = r0 + row < B ? v[i] : 0.0f;
-  }
-  if (dead) *sdead = 1;
-}
-
-// A wave's weight fragments of one 16-column tile over its k-quarter (K / 64 float4; with K = 4 E a
-// wave takes the whole E-wide k range of its own tile).  Issued at the start of a stage, before the
-// member polls its inputs, so the weights' memory latency hides under the hand-off wait.
-template <int K>
-struct GlW {
-  float4 v[K / 64];
-};
-template <int K>
-__device__ __forceinline__ void gl_wload(GlW<K>& f, const float* __restrict__ wrow, int wave, int lane) {
-  const float* wr = wrow + wave * (K / 4) + 4 * (lane >> 4);
-#pragma unroll
-  for (int i = 0; i < K / 64; ++i) f.v[i] = *reinterpret_cast<const float4*>(wr + 16 * i);
-}
-// acc = A[16][wave's k-quarter] x the fragments (lane l: row / column l & 15, k = 16 i + 4 (l >> 4) + j)
-template <int K>
-__device__ __forceinline__ gv4 gl_mma(const float* A, int lda, const GlW<K>& f, int lane, int wave) {
-  const int m = lane & 15, q = lane >> 4;
-  gv4 acc = gv4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int i = 0; i < K / 64; ++i) {
-    const float4 x = *reinterpret_cast<const float4*>(A + m * lda + wave * (K / 4) + 16 * i + 4 * q);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.x, f.v[i].x, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.y, f.v[i].y, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.z, f.v[i].z, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.w, f.v[i].w, acc, 0, 0, 0);
-  }
-  return acc;
-}
-
-// a LayerNorm's gamma / beta for this lane's four columns
-struct GlLn {
-  float4 g, b;
-};
-__device__ __forceinline__ GlLn gl_lnp(const float* __restrict__ g, const float* __restrict__ b, int lane) {
-  return GlLn{gen_ld4(g + 4 * lane), gen_ld4(b + 4 * lane)};
-}
-// LN(a[r] + b[r]) of one row (4 values per lane) into out (and out2 when given)
-__device__ __forceinline__ void gl_ln_row(const float* a, const float* b, const GlLn& p, float eps, float* out,
-                                          float* out2, int lane) {
-  const float4 v = gen_ln(gen_add4(*reinterpret_cast<const float4*>(a + 4 * lane),
-                                   *reinterpret_cast<const float4*>(b + 4 * lane)),
-                          p.g, p.b, eps);
-  *reinterpret_cast<float4*>(out + 4 * lane) = v;
-  if (out2) *reinterpret_cast<float4*>(out2 + 4 * lane) = v;
-}
-
-// the four waves' partial tiles of tile q into red[.][q]
-__device__ __forceinline__ void gl_park(float (*red)[4][16][17], int q, int wave, int lane, gv4 acc) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) red[wave][q][4 * (lane >> 4) + i][lane & 15] = acc[i];
-}
-__device__ __forceinline__ float gl_sum(const float (*red)[4][16][17], int q, int m, int n) {
-  return (red[0][q][m][n] + red[1][q][m][n]) + (red[2][q][m][n] + red[3][q][m][n]);
-}
 
 __global__ __launch_bounds__(256) void gen_loop_kernel(GenLoopArgs p) {
   constexpr int XP = GE + 4, AP = 2 * GE + 4, HP = GHB + 4;
@@ -512,7 +403,9 @@ __global__ __launch_bounds__(256) void gen_loop_kernel(GenLoopArgs p) {
   __shared__ __attribute__((aligned(16))) float M3[GL_ROWS][XP];
   __shared__ __attribute__((aligned(16))) float hs[16][HP];
   __shared__ float red[4][4][16][17];
-  __shared__ float msin[GL_ROWS][16];
+  __shared__ __attribute__((aligned(16))) float msin[GL_ROWS][16];
+  __shared__ float fe_s[16][GE];   // feature_embedding.0 W^T (rows past fm zero) and its bias
+  __shared__ float feb_s[GE];
   __shared__ int sdead, xflag;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = blockIdx.x % p.ngroups, j = blockIdx.x / p.ngroups;   // group (8 rows), member (1/16 of columns)
@@ -526,6 +419,8 @@ __global__ __launch_bounds__(256) void gen_loop_kernel(GenLoopArgs p) {
   unsigned long long* slots = bzf + (long)B * GE;
   bool dead = false;
   for (int i = tid; i < 16 * AP; i += 256) (&A[0][0])[i] = 0.0f;
+  for (int f = 0; f < 16; ++f) fe_s[f][tid] = f < p.fm ? p.fe_w[tid * p.fm + f] : 0.0f;
+  feb_s[tid] = p.fe_b[tid];
   if (tid == 0) sdead = 0;
   const int local = group_on_one_xcd<GL_MEM>(slots + (long)g * GL_MEM, j, p.err, dead, &xflag);
   if (tid < GL_ROWS * 16) {   // frame 0's self motion
@@ -556,19 +451,25 @@ __global__ __launch_bounds__(256) void gen_loop_kernel(GenLoopArgs p) {
           bo = w[GL_BIH][3 * GE + u] + w[GL_BHH][3 * GE + u];
         }
         if (k == 0) {
+          // all 16 self-motion columns from LDS, unrolled (msin and fe_s are zero past fm: the same
+          // sums), so the reads issue back to back instead of one round trip per column
           const int c = tid;
-          float acc[GL_ROWS];
-          const float bc = p.fe_b[c];
+          float wv[16];
 #pragma unroll
-          for (int m = 0; m < GL_ROWS; ++m) acc[m] = 0.0f;
-          for (int ff = 0; ff < fm; ++ff) {
-            const float wf = p.fe_w[c * fm + ff];
-#pragma unroll
-            for (int m = 0; m < GL_ROWS; ++m) acc[m] = fmaf(msin[m][ff], wf, acc[m]);
-          }
+          for (int f = 0; f < 16; ++f) wv[f] = fe_s[f][c];
+          const float bc = feb_s[c];
 #pragma unroll
           for (int m = 0; m < GL_ROWS; ++m) {
-            const float v = r0 + m < B ? acc[m] + bc : 0.0f;
+            float acc = 0.0f;
+#pragma unroll
+            for (int f4 = 0; f4 < 4; ++f4) {
+              const float4 ms4 = *reinterpret_cast<const float4*>(&msin[m][4 * f4]);
+              acc = fmaf(ms4.x, wv[4 * f4], acc);
+              acc = fmaf(ms4.y, wv[4 * f4 + 1], acc);
+              acc = fmaf(ms4.z, wv[4 * f4 + 2], acc);
+              acc = fmaf(ms4.w, wv[4 * f4 + 3], acc);
+            }
+            const float v = r0 + m < B ? acc + bc : 0.0f;
             Xs[m][c] = v;
             A[m][c] = v;
           }

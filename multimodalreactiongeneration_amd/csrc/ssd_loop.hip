@@ -1,0 +1,388 @@
+// The forward frame loop of lstm_with_sampling's scheduled-sampling decode (BASELINE configs[2]) in
+// ONE persistent launch.
+//
+// Reference: LSTMwithSample.prediction -> head_motion_generation -> generate_one_step
+// (mr_gen/model/lstm_with_sampling/lstm_with_sample.py:339-433).  decode.hip runs the same chain as
+// L + 1 launches per frame (decode.py, _SSDecodeFn.forward); each launch costs a kernel boundary
+// (~5 us at 64 rows) for ~1 us of work.  Here the batch is cut into groups of 8 rows served by 16
+// workgroups each (gen_loop.h, the generation loop's layout), member j owning hidden units
+// 16 j .. 16 j + 15 of every layer.  Per frame t:
+//   L0  X_0 = P(t) + ms_in(t) W_ms^T (every member the full rows, in LDS) -> gates of its 16 units
+//       (4 MFMA tiles of 4 units x 4 gates, v_mfma_f32_16x16x4_f32) -> zero-state cell -> publish h_0
+//   Li  gather h_{i-1} -> X_i = LN(h_{i-1} + X_{i-1}) (full rows, LDS) -> gates -> cell -> publish h_i
+//   F   gather h_{L-1} -> U = LN(h_{L-1} + X_{L-1}) -> Z = relu(U W1^T + b1) (all 64 hidden columns,
+//       per member) -> y = Z W2^T + b2 -> ms_in(t + 1) = mask[t] ? y : ms[t]  (no exchange: every
+//       member holds its rows' next input)
+// so a frame is L hand-offs instead of L + 1 kernel boundaries.  Every tensor the backward reads
+// (decode.py: X_f's ms columns, X_i, post-activation gates, c, h, the LayerNorm statistics, U, Z, y)
+// is written with the per-frame kernels' layout; member j writes its 16 columns, member 0 the
+// row-wide values.  Hand-off buffers alternate by frame parity: a slot is rewritten two frames
+// later, after every reader of it has passed the next frame's last gather.
+#include "gen_loop.h"
+
+namespace mrg {
+
+static constexpr int SL_MAXL = 4;        // layered LSTM depth
+static constexpr int SL_PER_LAYER = 11;  // see mrg_ssd_loop_fwd
+
+struct SsdLoopLayer {
+  const float *w_ih, *b_ih, *b_hh, *ln_g, *ln_b;   // ln: the LayerNorm after this layer
+  float *X, *G, *C, *Hs;                          // [T][B][H], [T][B][4H], [T][B][H], [T][B][H]
+  float *mean, *rstd;                             // that LayerNorm's statistics [T][B]
+};
+struct SsdLoopArgs {
+  SsdLoopLayer L[SL_MAXL];
+  const float* P;                 // [T][B][H] feature projection of [sampler | partner] + b_f
+  const float* wms;               // W_ms^T [FO][H]
+  const float *w1, *b1, *w2, *b2; // FFN [HB][H], [HB], [FO][HB], [FO]
+  const float* ms;                // ms[b * ms_bs + t * ms_ts + o]
+  long ms_bs, ms_ts;
+  const unsigned char* mask;      // [T]
+  float* xf_ms;                   // ms_in(t) -> xf_ms[(t * B + b) * F + o]
+  float *U, *Z, *y;               // [T][B][H], [T][B][HB], [B][T][FO]
+  unsigned long long* ring;       // 2 x L x [B][H] granules, then the XCC slots
+  int* err;
+  int B, T, FO, F, nl, ngroups;
+  float eps;
+  unsigned long long* stamps;     // diagnostics (mrg_ssd_loop_debug_stamps): [T][16] of block 0, or null
+};
+
+// block 0 / thread 0: shader-clock stamp `slot` of frame t (slot 15 of frame 0: the local hand-off flag)
+#define SL_STAMP(slot)                                                                   \
+  do {                                                                                   \
+    if (p.stamps && blockIdx.x == 0 && threadIdx.x == 0) {                               \
+      unsigned long long _t;                                                             \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");         \
+      p.stamps[(long)t * 16 + (slot)] = _t;                                              \
+    }                                                                                    \
+  } while (0)
+
+// LN(a + r) of one 256-wide row (4 values per lane) into out (and out2); the statistics returned
+__device__ __forceinline__ void sl_ln_row(const float* a, const float* r, const GlLn& p, float eps, float* out,
+                                          float* out2, int lane, float& mean, float& rs) {
+  const float4 v = gen_add4(*reinterpret_cast<const float4*>(a + 4 * lane), *reinterpret_cast<const float4*>(r + 4 * lane));
+  mean = gen_wave_sum((v.x + v.y) + (v.z + v.w)) * (1.0f / GE);
+  const float dx = v.x - mean, dy = v.y - mean, dz = v.z - mean, dw = v.w - mean;
+  rs = rsqrtf(gen_wave_sum((dx * dx + dy * dy) + (dz * dz + dw * dw)) * (1.0f / GE) + eps);
+  const float4 o = make_float4(fmaf(dx * rs, p.g.x, p.b.x), fmaf(dy * rs, p.g.y, p.b.y), fmaf(dz * rs, p.g.z, p.b.z),
+                               fmaf(dw * rs, p.g.w, p.b.w));
+  *reinterpret_cast<float4*>(out + 4 * lane) = o;
+  if (out2) *reinterpret_cast<float4*>(out2 + 4 * lane) = o;
+}
+
+__global__ __launch_bounds__(256) void ssd_loop_kernel(SsdLoopArgs p) {
+  constexpr int AP = GE + 4, HP = GHB + 4;
+  __shared__ __attribute__((aligned(16))) float A[16][AP];     // the stage's product operand (rows 8..15 zero)
+  __shared__ __attribute__((aligned(16))) float Xs[GL_ROWS][AP]; // the current layer's input rows
+  __shared__ __attribute__((aligned(16))) float hs[16][HP];     // Z (rows 8..15 unused)
+  __shared__ float red[4][4][16][17];
+  __shared__ __attribute__((aligned(16))) float msin[GL_ROWS][16];
+  __shared__ float wms_s[16][GE];                               // W_ms^T (rows past FO unused)
+  __shared__ float bias_s[SL_MAXL][4][16];                      // b_ih + b_hh of this member's units
+  // layer 0's 64 W_ih rows of this member (row 16 q + n: the tile-q column n of the products), resident:
+  // layer 0 has no hand-off wait to hide a weight fetch under
+  __shared__ __attribute__((aligned(16))) float W0s[64][AP];
+  __shared__ float Ps[GL_ROWS][GE];                             // P rows of the next frame
+  __shared__ int sdead, xflag;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = blockIdx.x % p.ngroups, j = blockIdx.x / p.ngroups;   // group (8 rows), member (16 units)
+  const int r0 = GL_ROWS * g, B = p.B, T = p.T, FO = p.FO, nl = p.nl;
+  const long BH = (long)B * GE;
+  const float eps = p.eps;
+  unsigned long long* slots = p.ring + 2L * nl * BH;
+  bool dead = false;
+  for (int i = tid; i < 16 * AP; i += 256) (&A[0][0])[i] = 0.0f;
+  for (int o = 0; o < 16; ++o) wms_s[o][tid] = o < FO ? p.wms[(long)o * GE + tid] : 0.0f;
+  if (tid < 64 * nl) {
+    const int i = tid >> 6, q = (tid >> 4) & 3, n = tid & 15;
+    bias_s[i][q][n] = p.L[i].b_ih[q * GE + 16 * j + n] + p.L[i].b_hh[q * GE + 16 * j + n];
+  }
+  for (int e = tid; e < 64 * (GE / 4); e += 256) {
+    const int rr = e / (GE / 4), k4 = e % (GE / 4), q = rr >> 4, n = rr & 15;
+    *reinterpret_cast<float4*>(&W0s[rr][4 * k4]) = *reinterpret_cast<const float4*>(
+        p.L[0].w_ih + (long)((n >> 2) * GE + 16 * j + 4 * q + (n & 3)) * GE + 4 * k4);
+  }
+  if (tid == 0) sdead = 0;
+  const int local = group_on_one_xcd<GL_MEM>(slots + (long)g * GL_MEM, j, p.err, dead, &xflag);
+  if (tid < GL_ROWS * 16) {   // ms_in(0) = ms[0]
+    const int m = tid >> 4, o = tid & 15;
+    msin[m][o] = (o < FO && r0 + m < B) ? p.ms[(long)(r0 + m) * p.ms_bs + o] : 0.0f;
+  }
+  __syncthreads();
+  const int m8 = tid >> 4, n16 = tid & 15;   // epilogue thread -> (row, tile column), rows < 8 used
+  const int b8 = r0 + m8;
+  const bool ep = tid < GL_ROWS * 16 && b8 < B;
+  const int c16 = lane & 15;                 // this lane's tile column (weight row) in the products
+  const int u = 16 * j + n16;                // the epilogue thread's hidden unit
+  if (p.stamps && blockIdx.x == 0 && tid == 0) p.stamps[15] = (unsigned long long)local;
+  // Saved-tensor stores are deferred to just after the NEXT hand-off poll: on gfx9 a store holds a
+  // vmcnt slot until the memory acknowledges it, and the counter retires in order, so stores issued
+  // before a poll would sit in front of the poll's loads.  Pending: one layer's gate / cell / input
+  // values (epilogue threads), one LayerNorm's statistics (member 0, lane 0 of each wave: rows wave
+  // and wave + 4) and the FFN stage's U / Z / y.
+  int pl = -1, pst = -1, pft = -1;     // pending layer, statistics layer, FFN frame (-1: none)
+  long prt = 0, pstrt = 0;             // their frames' first rows
+  float pg[4] = {0.f, 0.f, 0.f, 0.f}, pc = 0.f, ph = 0.f, px = 0.f, pms = 0.f;
+  float pmean[2] = {0.f, 0.f}, prs[2] = {0.f, 0.f};
+  float pu = 0.f, py = 0.f, pz[4] = {0.f, 0.f, 0.f, 0.f};
+  auto flush = [&]() {
+    if (pl >= 0 && ep) {
+      const SsdLoopLayer& L = p.L[pl];
+      const long row = prt + b8;
+      float* gs = L.G + row * 4 * GE + u;
+      gs[0] = pg[0]; gs[GE] = pg[1]; gs[2 * GE] = pg[2]; gs[3 * GE] = pg[3];
+      L.C[row * GE + u] = pc;
+      L.Hs[row * GE + u] = ph;
+      L.X[row * GE + u] = px;
+      if (pl == 0 && j == 0 && n16 < FO) p.xf_ms[row * p.F + n16] = pms;
+    }
+    pl = -1;
+    if (pst >= 0 && j == 0 && lane == 0) {
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr) {
+        const int m = wave + 4 * rr;
+        if (r0 + m < B) {
+          p.L[pst].mean[pstrt + r0 + m] = pmean[rr];
+          p.L[pst].rstd[pstrt + r0 + m] = prs[rr];
+        }
+      }
+    }
+    pst = -1;
+    if (pft >= 0) {
+      const long rt = (long)pft * B;
+      if (ep) p.U[(rt + b8) * GE + u] = pu;
+      if (j == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = 4 * (lane >> 4) + i;
+          if (m < GL_ROWS && r0 + m < B) p.Z[(rt + r0 + m) * GHB + 16 * wave + c16] = pz[i];
+        }
+        if (ep && n16 < FO) p.y[((long)b8 * T + pft) * FO + n16] = py;
+      }
+    }
+    pft = -1;
+  };
+  // the gate tiles of layer i from A (4 tiles q: units 16 j + 4 q + (n & 3), gate n >> 2), the
+  // zero-state cell, h published; the values saved for the backward become the pending set
+  auto gates = [&](int i, const GlW<GE> (&f)[4], unsigned long long* hbuf, unsigned tag, long row_t) {
+    __syncthreads();
+    if (tid < GL_ROWS * 16) px = Xs[m8][u];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) gl_park(red, q, wave, lane, gl_mma<GE>(&A[0][0], AP, f[q], lane, wave));
+    __syncthreads();
+    if (ep) {
+      const int q = n16 >> 2, jj = n16 & 3;
+      pg[0] = sigmoidf_(gl_sum(red, q, m8, jj) + bias_s[i][0][n16]);
+      pg[1] = sigmoidf_(gl_sum(red, q, m8, 4 + jj) + bias_s[i][1][n16]);
+      pg[2] = tanhf_(gl_sum(red, q, m8, 8 + jj) + bias_s[i][2][n16]);
+      pg[3] = sigmoidf_(gl_sum(red, q, m8, 12 + jj) + bias_s[i][3][n16]);
+      pc = pg[0] * pg[2];   // f c0 + i g with c0 = 0
+      ph = pg[3] * tanhf_(pc);
+      put_granule(hbuf + (long)b8 * GE + u, tag, ph, local);
+    }
+    pl = i;
+    prt = row_t;
+  };
+  // the P rows of the next frame, loaded one frame ahead (after layer 1's hand-off poll, or the
+  // FFN stage's with one layer; frame 0's here) and parked in LDS after the FFN stage's poll (which
+  // waits for them anyway): layer 0 has no hand-off wait to hide an HBM fetch under, and a register
+  // carried across the frame loop's back edge costs a full vmcnt(0) wait where it is used
+  float pp[GL_ROWS];
+  auto load_p = [&](int tn) {
+#pragma unroll
+    for (int m = 0; m < GL_ROWS; ++m) pp[m] = p.P[((long)tn * B + min(r0 + m, B - 1)) * GE + tid];
+  };
+  auto park_p = [&]() {
+#pragma unroll
+    for (int m = 0; m < GL_ROWS; ++m) Ps[m][tid] = pp[m];
+  };
+  load_p(0);
+  park_p();
+  for (int t = 0; t < T && !sdead; ++t) {
+    SL_STAMP(0);
+    unsigned long long* hb = p.ring + (long)(t & 1) * nl * BH;   // this frame's h_i buffers
+    const unsigned tag = (unsigned)(t + 1);
+    const long row_t = (long)t * B;   // frame t's first row in the [T][B][.] tensors
+    // ---- layer 0: X_0 = P(t) + ms_in(t) W_ms^T (thread = column)
+    {
+      // all 16 ms columns, unrolled (msin and wms_s are zero past FO: the same sums), so the LDS
+      // reads issue back to back instead of one round trip per column
+      float wv[16];
+#pragma unroll
+      for (int o = 0; o < 16; ++o) wv[o] = wms_s[o][tid];
+#pragma unroll
+      for (int m = 0; m < GL_ROWS; ++m) {
+        float v = Ps[m][tid];
+#pragma unroll
+        for (int o4 = 0; o4 < 4; ++o4) {
+          const float4 ms4 = *reinterpret_cast<const float4*>(&msin[m][4 * o4]);
+          v = fmaf(ms4.x, wv[4 * o4], v);
+          v = fmaf(ms4.y, wv[4 * o4 + 1], v);
+          v = fmaf(ms4.z, wv[4 * o4 + 2], v);
+          v = fmaf(ms4.w, wv[4 * o4 + 3], v);
+        }
+        v = r0 + m < B ? v : 0.0f;
+        Xs[m][tid] = v;
+        A[m][tid] = v;
+      }
+      SL_STAMP(1);
+      if (tid < GL_ROWS * 16) pms = msin[m8][n16];
+      // the weight fragments after the build (a barrier keeps the compiler from hoisting them: held
+      // through it they leave too few registers and the build's LDS reads serialise)
+      __syncthreads();
+      GlW<GE> f0[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) gl_wload<GE>(f0[q], W0s[16 * q + c16], wave, lane);
+      gates(0, f0, hb, tag, row_t);
+      SL_STAMP(2);
+    }
+    // ---- layer i > 0: X_i = LN(h_{i-1} + X_{i-1}) (the LayerNorm after layer i - 1)
+    for (int i = 1; i < nl; ++i) {
+      const SsdLoopLayer& Lp = p.L[i - 1];
+      GlW<GE> f[4];   // weights first: their latency hides under the hand-off wait
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        gl_wload<GE>(f[q], p.L[i].w_ih + (long)((c16 >> 2) * GE + 16 * j + 4 * q + (c16 & 3)) * GE, wave, lane);
+      const GlLn ln = gl_lnp(Lp.ln_g, Lp.ln_b, lane);
+      gl_gather<GE>(hb + (long)(i - 1) * BH, r0, B, tag, &A[0][0], AP, p.err, dead, &sdead);
+      __syncthreads();
+      flush();
+      if (i == 1 && t + 1 < T) load_p(t + 1);
+      SL_STAMP(1 + 2 * i);
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr) {
+        const int m = wave + 4 * rr;
+        sl_ln_row(A[m], Xs[m], ln, eps, Xs[m], A[m], lane, pmean[rr], prs[rr]);
+      }
+      pst = i - 1;
+      pstrt = row_t;
+      gates(i, f, hb + (long)i * BH, tag, row_t);
+      SL_STAMP(2 + 2 * i);
+    }
+    // ---- F: U = LN(h + X) of the last layer, Z = relu(U W1^T + b1), y = Z W2^T + b2, the select
+    {
+      const SsdLoopLayer& Ll = p.L[nl - 1];
+      GlW<4 * GE> f1;   // wave w: hidden columns 16 w .. 16 w + 15 over the whole k range
+      gl_wload<4 * GE>(f1, p.w1 + (long)(16 * wave + c16) * GE, 0, lane);
+      GlW<GHB> f2;      // output columns past FO multiply zeroed fragments of a valid weight row
+      gl_wload<GHB>(f2, p.w2 + (long)(c16 < FO ? c16 : 0) * GHB, wave, lane);
+      if (c16 >= FO) f2.v[0] = gen_zero4();
+      const GlLn ln = gl_lnp(Ll.ln_g, Ll.ln_b, lane);
+      const int hc = 16 * wave + c16;
+      const float b1 = p.b1[hc];
+      const bool yv_ok = tid < GL_ROWS * 16 && n16 < FO && b8 < B;
+      const float b2 = yv_ok ? p.b2[n16] : 0.0f;
+      const bool sel = p.mask[t] != 0;
+      const float msv = yv_ok ? p.ms[(long)b8 * p.ms_bs + (long)t * p.ms_ts + n16] : 0.0f;
+      gl_gather<GE>(hb + (long)(nl - 1) * BH, r0, B, tag, &A[0][0], AP, p.err, dead, &sdead);
+      __syncthreads();
+      flush();
+      if (t + 1 < T) {
+        if (nl == 1) load_p(t + 1);
+        else park_p();   // Ps is free: layer 0 of this frame read it before its publish
+      }
+      SL_STAMP(1 + 2 * nl);
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr) {
+        const int m = wave + 4 * rr;
+        sl_ln_row(A[m], Xs[m], ln, eps, A[m], nullptr, lane, pmean[rr], prs[rr]);
+      }
+      pst = nl - 1;
+      pstrt = row_t;
+      __syncthreads();
+      if (tid < GL_ROWS * 16) pu = A[m8][u];
+      {
+        const gv4 acc = gl_mma<4 * GE>(&A[0][0], AP, f1, lane, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          pz[i] = fmaxf(acc[i] + b1, 0.0f);
+          hs[4 * (lane >> 4) + i][hc] = pz[i];
+        }
+      }
+      __syncthreads();
+      gl_park(red, 0, wave, lane, gl_mma<GHB>(&hs[0][0], HP, f2, lane, wave));
+      __syncthreads();
+      if (tid < GL_ROWS * 16) {
+        float nxt = 0.0f;
+        if (yv_ok) {
+          py = gl_sum(red, 0, m8, n16) + b2;
+          nxt = sel ? py : msv;
+        }
+        msin[m8][n16] = nxt;
+      }
+      if (nl == 1 && t + 1 < T) park_p();
+      pft = t;
+      if (dead) sdead = 1;
+      __syncthreads();
+      SL_STAMP(2 + 2 * nl);
+    }
+  }
+  flush();
+}
+
+}  // namespace mrg
+
+using namespace mrg;
+
+static unsigned long long* g_ssd_stamps = nullptr;
+// Diagnostics (tools/ssd_stamps.py): later mrg_ssd_loop_fwd launches write block 0's per-stage
+// shader-clock stamps into buf ([T][16] u64; slot 15 of frame 0: the group's local hand-off flag); null = off.
+MRG_API int mrg_ssd_loop_debug_stamps(void* buf) {
+  g_ssd_stamps = static_cast<unsigned long long*>(buf);
+  return 0;
+}
+
+// Bytes of the granule ring mrg_ssd_loop_fwd needs for B rows and nl layers (zeroed by the caller
+// before every launch).
+MRG_API long mrg_ssd_loop_ring_bytes(int B, int nl) {
+  const int ng = (B + GL_ROWS - 1) / GL_ROWS;
+  return (2L * nl * B * GE + (long)ng * GL_MEM) * 8;
+}
+
+// 1 when the persistent grid (16 workgroups per 8 batch rows) can be resident on `cus` CUs (0: this device's).
+MRG_API int mrg_ssd_loop_fits(int B, int cus) {
+  const long nblk = (long)GL_MEM * ((B + GL_ROWS - 1) / GL_ROWS);
+  return fits(ssd_loop_kernel, 256, nblk, cus > 0 ? cus : device_cus()) ? 1 : 0;
+}
+
+// The scheduled-sampling decode's forward frame loop in one persistent launch (ssd_loop_kernel;
+// replaces the per-frame mrg_ssd_feat_gate_cell_fwd / mrg_ssd_gate_cell_fwd / mrg_ssd_ffn_z_fwd /
+// mrg_ssd_y_fwd sequence of decode.py with the same outputs).  H = 256, HB = 64, FO <= 16, nl <= 4.
+// lptrs (host array, 11 per layer): w_ih [4H][H], b_ih, b_hh, the LayerNorm after the layer (gamma,
+// beta), then the saved X [T][B][H], gates [T][B][4H], c, h [T][B][H] and that LayerNorm's mean / rstd
+// [T][B].  P [T][B][H]; wms = W_ms^T [FO][H]; FFN w1 [HB][H], b1, w2 [FO][HB], b2; ms, mask as in
+// mrg_ssd_feat_gate_cell_fwd; xf_ms: X_f's ms columns (row stride F); U [T][B][H], Z [T][B][HB],
+// y [B][T][FO]; ring: mrg_ssd_loop_ring_bytes of zeroed memory; err: the recurrences' error flag.
+MRG_API int mrg_ssd_loop_fwd(int B, int T, int H, int HB, int FO, int F, int nl, float eps, const void* const* lptrs,
+                             int nptrs, const float* P, const float* wms, const float* w1, const float* b1,
+                             const float* w2, const float* b2, const float* ms, long ms_bs, long ms_ts,
+                             const unsigned char* mask, float* xf_ms, float* U, float* Z, float* y, void* ring,
+                             int* err, hipStream_t stream) {
+  if (B == 0 || T == 0) return 0;
+  MRG_REQUIRE(H == GE && HB == GHB && FO >= 1 && FO <= 16 && nl >= 1 && nl <= SL_MAXL && F >= FO,
+              "mrg_ssd_loop_fwd: needs H = %d, HB = %d, 1 <= FO <= 16, 1 <= nl <= %d (H=%d HB=%d FO=%d nl=%d)", GE,
+              GHB, SL_MAXL, H, HB, FO, nl);
+  MRG_REQUIRE(lptrs && nptrs == SL_PER_LAYER * nl && P && wms && w1 && b1 && w2 && b2 && ms && mask && xf_ms && U &&
+                  Z && y && ring && err,
+              "mrg_ssd_loop_fwd: null argument or nptrs %d != %d", nptrs, SL_PER_LAYER * nl);
+  MRG_REQUIRE(mrg_ssd_loop_fits(B, 0) == 1, "mrg_ssd_loop_fwd: %d workgroups cannot all be resident (B=%d)",
+              GL_MEM * ((B + GL_ROWS - 1) / GL_ROWS), B);
+  SsdLoopArgs a{};
+  for (int i = 0; i < nl; ++i) {
+    const void* const* q = lptrs + SL_PER_LAYER * i;
+    for (int k = 0; k < SL_PER_LAYER; ++k) MRG_REQUIRE(q[k] != nullptr, "mrg_ssd_loop_fwd: null pointer %d of layer %d", k, i);
+    SsdLoopLayer& L = a.L[i];
+    L.w_ih = static_cast<const float*>(q[0]); L.b_ih = static_cast<const float*>(q[1]);
+    L.b_hh = static_cast<const float*>(q[2]); L.ln_g = static_cast<const float*>(q[3]);
+    L.ln_b = static_cast<const float*>(q[4]);
+    L.X = (float*)q[5]; L.G = (float*)q[6]; L.C = (float*)q[7]; L.Hs = (float*)q[8];
+    L.mean = (float*)q[9]; L.rstd = (float*)q[10];
+  }
+  a.P = P; a.wms = wms; a.w1 = w1; a.b1 = b1; a.w2 = w2; a.b2 = b2;
+  a.ms = ms; a.ms_bs = ms_bs; a.ms_ts = ms_ts; a.mask = mask; a.xf_ms = xf_ms;
+  a.U = U; a.Z = Z; a.y = y; a.ring = static_cast<unsigned long long*>(ring); a.err = err;
+  a.B = B; a.T = T; a.FO = FO; a.F = F; a.nl = nl; a.ngroups = (B + GL_ROWS - 1) / GL_ROWS; a.eps = eps;
+  a.stamps = g_ssd_stamps;
+  klaunch(ssd_loop_kernel, dim3(GL_MEM * a.ngroups), 256, 0, stream, a);
+  return check_launch("ssd_loop_kernel");
+}

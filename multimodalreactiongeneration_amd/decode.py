@@ -24,6 +24,9 @@ reference's golden and to the oracle at benchmark width).
 from __future__ import annotations
 
 
+import ctypes
+import os
+
 import torch
 from torch.autograd import Function
 
@@ -31,6 +34,9 @@ from . import _lib
 from .functional import _err_flag, _gbuf, _keeps_precision, _ptr, _resln_bwd, _stream, _wgrad, _side, gemm
 
 F32 = torch.float32
+# the forward frame loop as ONE persistent launch (ssd_loop.hip) when H = 256, HB = 64, FO <= 16,
+# nl <= 4 and its grid fits; MRG_SSD_LOOP=0 keeps the L + 1 launches per frame
+_LOOP = [os.environ.get("MRG_SSD_LOOP", "1") == "1"]
 
 
 class _SSDecodeFn(Function):
@@ -77,7 +83,20 @@ class _SSDecodeFn(Function):
         msc = ms.contiguous()
         slab, gslab, zslab = B * H, B * 4 * H, B * HB
         lw, lb = layers[-1][4], layers[-1][5]
-        for t in range(T):
+        if _LOOP[0] and H == 256 and HB == 64 and FO <= 16 and nl <= 4 and lib.mrg_ssd_loop_fits(B, 0) == 1:
+            lp = []
+            for i, (w_ih, _w_hh, b_ih, b_hh, g_, b_) in enumerate(layers):
+                lp += [w_ih, b_ih, b_hh, g_, b_, X[i], G[i], C[i], Hs[i], stats[i][0], stats[i][1]]
+            lpa = (ctypes.c_void_p * len(lp))(*[_ptr(q) for q in lp])
+            ring = torch.zeros(max(1, lib.mrg_ssd_loop_ring_bytes(B, nl) // 8), dtype=torch.int64, device=dev)
+            _lib.check(lib.mrg_ssd_loop_fwd(
+                B, T, H, HB, FO, F, nl, eps, lpa, len(lp), _ptr(P), _ptr(wms_t), _ptr(w1), _ptr(b1), _ptr(w2),
+                _ptr(b2), _ptr(msc), msc.stride(0), msc.stride(1), _ptr(mask), _ptr(xf, SA + FMp), _ptr(U), _ptr(Z),
+                _ptr(y), _ptr(ring), _ptr(_err_flag(dev)), _stream()), "ssd loop fwd")
+            T_launch = 0
+        else:
+            T_launch = T
+        for t in range(T_launch):
             for i, (w_ih, _w_hh, b_ih, b_hh, _g, _b) in enumerate(layers):
                 cell = (_ptr(w_ih), _ptr(b_ih), _ptr(b_hh), _ptr(G[i], t * gslab), _ptr(C[i], t * slab),
                         _ptr(Hs[i], t * slab), _stream())
@@ -98,8 +117,9 @@ class _SSDecodeFn(Function):
                 B, H, HB, _ptr(Hs[-1], t * slab), _ptr(X[-1], t * slab), _ptr(lw), _ptr(lb), eps, _ptr(U, t * slab),
                 _ptr(stats[-1][0], t * B), _ptr(stats[-1][1], t * B), _ptr(w1), _ptr(b1), _ptr(Z, t * zslab),
                 _stream()), "ssd ffn z fwd")
-        _lib.check(lib.mrg_ssd_y_fwd(B, HB, FO, _ptr(Z, (T - 1) * zslab), _ptr(w2), _ptr(b2), _ptr(y, (T - 1) * FO),
-                                     T * FO, _stream()), "ssd y fwd")
+        if T_launch:
+            _lib.check(lib.mrg_ssd_y_fwd(B, HB, FO, _ptr(Z, (T - 1) * zslab), _ptr(w2), _ptr(b2),
+                                         _ptr(y, (T - 1) * FO), T * FO, _stream()), "ssd y fwd")
         ctx.spec = (nl, eps, B, T, SA, FMp, FM, H, F, HB, FO)
         ctx.save_for_backward(mask, w_f, b_f, *params, xf, U, Z, wms_t, *X, *G, *C, *Hs, *stats)
         ctx.set_materialize_grads(False)

@@ -992,3 +992,57 @@ def test_generation_fused_frame_loop_matches_module_path(B, T, loop):
     Fn.check_errors()
     assert fast.shape == slow.shape == (B, T, 6)
     assert rel_err(fast, slow) < 1e-5, rel_err(fast, slow)
+
+
+@pytest.mark.parametrize("B,T,nl,FO", [(64, 40, 2, 6), (37, 25, 1, 6), (3, 9, 3, 8), (20, 30, 4, 1)])
+def test_ssd_persistent_loop_matches_per_frame_launches(B, T, nl, FO):
+    """The scheduled-sampling decode's forward frame loop as ONE persistent launch (ssd_loop.hip: 16
+    workgroups per 8 rows, each layer's h handed over as granules, buffers alternating by frame
+    parity) vs the L + 1 launches per frame of decode.hip, on the same inputs under a random sampling
+    mask, ragged B, 1..4 layers and 1..8 output features (the per-frame kernels take FO <= 8): the prediction and, through the backward
+    that reads every saved tensor (X_f's ms columns, X, gates, c, h, LayerNorm statistics, U, Z), the
+    sampler-output and every parameter gradient agree within fp32 reordering.
+    Reference: lstm_with_sample.py:379-433."""
+    from multimodalreactiongeneration_amd import decode as D
+    from multimodalreactiongeneration_amd import functional as Fn
+    H, HB, SA, FMp = 256, 64, 128, 6
+    F = SA + FMp + FO
+    g = torch.Generator().manual_seed(B * 100 + nl)
+
+    def u(*shape, k):
+        return ((torch.rand(*shape, generator=g) * 2 - 1) * k).to(DEV)
+    base = dict(w_f=u(H, F, k=F ** -0.5), b_f=u(H, k=F ** -0.5))
+    layers = []
+    for _ in range(nl):
+        layers.append([u(4 * H, H, k=H ** -0.5), u(4 * H, H, k=H ** -0.5), u(4 * H, k=H ** -0.5),
+                       u(4 * H, k=H ** -0.5), 1 + u(H, k=0.2), u(H, k=0.2)])
+    ffn = [u(HB, H, k=H ** -0.5), u(HB, k=H ** -0.5), u(FO, HB, k=HB ** -0.5), u(FO, k=HB ** -0.5)]
+    a_s = torch.randn(B, T, SA, generator=g).to(DEV)
+    mp = torch.randn(B, T, FMp, generator=g).to(DEV)
+    ms = torch.randn(B, T, FO, generator=g).to(DEV)
+    mask = torch.from_numpy(np.random.RandomState(B + T).rand(T) < 0.5).to(DEV)
+    dy = torch.randn(B, T, FO, generator=g).to(DEV)
+    outs = []
+    prev = D._LOOP[0]
+    try:
+        for loop in (True, False):
+            D._LOOP[0] = loop
+            ps = [t.clone().requires_grad_(True) for t in [base["w_f"], base["b_f"]] + sum(layers, []) + ffn]
+            a = a_s.clone().requires_grad_(True)
+            lay = [ps[2 + 6 * i:8 + 6 * i] for i in range(nl)]
+            y = D.scheduled_sampling_decode(a, mp, ms, mask, ps[0], ps[1], lay, ps[2 + 6 * nl:])
+            (y * dy).sum().backward()
+            torch.cuda.synchronize()
+            Fn.check_errors()
+            outs.append((y.detach(), a.grad, [p.grad for p in ps]))
+    finally:
+        D._LOOP[0] = prev
+    (y0, a0, g0), (y1, a1, g1) = outs
+    assert y0.shape == (B, T, FO)
+    assert rel_err(y0, y1) < 1e-5, rel_err(y0, y1)
+    assert rel_err(a0, a1) < 1e-5, rel_err(a0, a1)
+    for i, (p, q) in enumerate(zip(g0, g1)):
+        if q is None or q.abs().max() == 0:   # W_hh (zero state): exactly zero on both paths
+            assert p is None or p.abs().max() == 0, i
+            continue
+        assert rel_err(p, q) < 1e-5, (i, rel_err(p, q))
