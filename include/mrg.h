@@ -268,6 +268,21 @@ int mrg_ssd_loop_fwd(int B, int T, int H, int HB, int FO, int F, int nl, float e
                      const float* w2, const float* b2, const float* ms, long ms_bs, long ms_ts,
                      const unsigned char* mask, float* xf_ms, float* U, float* Z, float* y, void* ring, int* err,
                      hipStream_t stream);
+/* The backward frame loop (mrg_ssd_ffn_bwd / mrg_ssd_dx / mrg_ssd_ln_cell_bwd of every frame, nl >= 2)
+ * in ONE persistent launch (ssd_loop.hip ssd_loop_bwd_kernel; decode.py uses it under the same
+ * conditions as the forward loop): per frame the last layer's FFN / LayerNorm / cell backward needs no
+ * exchange (the row sums through v), then per lower layer one hand-off of dG rows (dX = dG W_ih + g
+ * on MFMA) and one of partial LayerNorm row sums, and the bottom layer's partial dyx feeds the
+ * previous frame.  lptrs: 11 per layer (W_ih^T [H][4H] or null for layer 0, the LayerNorm gamma, the
+ * forward's X, gates, c, h, mean, rstd, then g, dG and dX (null for layer 0)); dy [B][T][FO]; v =
+ * [W1 gamma | W1 beta] [HB][2]; z [T][B][HB]; vt = W_ms^T W_ih0 [FO][4H]; outputs dyt [T][B][FO], dz
+ * [T][B][HB], du [T][B][H]; ring: mrg_ssd_loop_bwd_ring_bytes(B) of zeroed memory per launch.       */
+long mrg_ssd_loop_bwd_ring_bytes(int B);
+int mrg_ssd_loop_bwd_fits(int B, int cus);
+int mrg_ssd_loop_bwd(int B, int T, int H, int HB, int FO, int nl, const void* const* lptrs, int nptrs,
+                     const float* dy, const unsigned char* mask, const float* w1, const float* w2, const float* b1,
+                     const float* v, const float* z, const float* vt, const float* wms_t, float* dyt, float* dz,
+                     float* du, void* ring, int* err, hipStream_t stream);
 int mrg_ssd_ffn_bwd(int B, int H, int HB, int FO, int t, const float* dy, long dy_bs, const float* dfeat_next,
                     const float* dyx_next, const float* wms_t, const unsigned char* mask, const float* w1,
                     const float* w2,

@@ -53,6 +53,8 @@ int mrg_gen_loop_debug_stamps(void* buf);
  * input / after its publish, then the FFN stage; slot 15 of frame 0: the local hand-off flag)
  * (tools/ssd_stamps.py). */
 int mrg_ssd_loop_debug_stamps(void* buf);
+/* Diagnostics: the same for mrg_ssd_loop_bwd ([T][16] u64 by backward iteration). */
+int mrg_ssd_loop_bwd_debug_stamps(void* buf);
 /* Measurement (bench.py): while on, every kernel launched for a tagged library call (tag >= 0) is
  * timed by start / stop events bound to that kernel (hipExtLaunchKernelGGL): its own execution,
  * as rocprofv3 reports it.  stop waits, writes (ms, tag) per launch and returns the count. */

@@ -320,6 +320,305 @@ __global__ __launch_bounds__(256) void ssd_loop_kernel(SsdLoopArgs p) {
   flush();
 }
 
+// ------------------------------------------------------------------ the backward frame loop, one launch
+// ssd_loop_bwd_kernel: the per-frame backward of decode.py (mrg_ssd_ffn_bwd, mrg_ssd_dx,
+// mrg_ssd_ln_cell_bwd for L >= 2 layers) in ONE persistent launch over frames T-1 .. 0, with the
+// same row groups and members as the forward (member j: hidden units 16 j .. 16 j + 15).  Per frame:
+//   F  gather the 16 members' partial dyx(t+1) -> dy_total = dy(t) + mask[t] dyx(t+1) (every member
+//      its rows) -> dz = relu'(z) (dy_total W2) (all 64, per member) -> du = dz W1 (own columns) and
+//      the LayerNorm's two row sums through v = [W1 gamma | W1 beta] (no exchange, decode.hip's
+//      identity) -> g, the zero-state cell backward -> publish dG (i, g, o blocks) of the last layer
+//   D  (layer l = L-1 .. 1) gather dG rows -> dX_l = dG W_ih + g (own 16 columns, MFMA over the
+//      768 nonzero gate columns) -> the next LayerNorm backward's two partial row sums -> publish
+//   B  gather the partial sums -> LayerNorm backward of layer l-1 (own columns) -> cell backward ->
+//      publish dG (l-1 > 0), or at the bottom layer the partial dyx(t) = dfeat(t) W_ms over own units
+//      (dG vt^T + g wms^T, vt = W_ms^T W_ih0), which frame t - 1's F stage sums
+// so a frame is 1 + 2 (L - 1) hand-offs instead of 2L launches.  Hand-off buffers are single: a
+// member writes a buffer again only after a gather that needs every member past its last read.
+static constexpr int SB_KD = 3 * GE;   // dX product K: the i, g, o blocks (the f block of dG is zero)
+static constexpr int SB_NP = 10;       // pending saved-tensor stores per thread
+
+struct SsdBwdLayer {
+  const float* w_t;                    // W_ih^T [H][4H] (layers >= 1)
+  const float* ln_g;                   // gamma of the LayerNorm after this layer
+  const float *X, *G, *C, *Hs, *mean, *rstd;   // the forward's saved tensors
+  float *g, *dG, *dX;                  // d(h + x) [T][B][H], dG [T][B][4H], dX (layers >= 1) [T][B][H]
+};
+struct SsdBwdArgs {
+  SsdBwdLayer L[SL_MAXL];
+  const float* dy;                     // [B][T][FO]
+  const unsigned char* mask;           // [T]
+  const float *w1, *w2, *b1, *v;       // FFN W1 [HB][H], W2 [FO][HB], b1, v = [W1 gamma | W1 beta] [HB][2]
+  const float* z;                      // Z [T][B][HB]
+  const float *vt, *wms;               // vt = W_ms^T W_ih0 [FO][4H], W_ms^T [FO][H]
+  float *dyt, *dz, *du;                // [T][B][FO], [T][B][HB], [T][B][H]
+  unsigned long long* ring;            // dG [B][768] | partial sums [B][32] | dyx [B][256] granules, XCC slots
+  int* err;
+  int B, T, FO, nl, ngroups;
+  unsigned long long* stamps;          // diagnostics: [T][16] of block 0 (mrg_ssd_loop_debug_stamps), or null
+};
+
+#define SB_STAMP(slot)                                                                   \
+  do {                                                                                   \
+    if (p.stamps && blockIdx.x == 0 && threadIdx.x == 0) {                               \
+      unsigned long long _t;                                                             \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");         \
+      p.stamps[(long)it * 16 + (slot)] = _t;                                             \
+    }                                                                                    \
+  } while (0)
+
+__global__ __launch_bounds__(256) void ssd_loop_bwd_kernel(SsdBwdArgs p) {
+  constexpr int KP = SB_KD + 4;
+  __shared__ __attribute__((aligned(16))) float A[16][KP];   // gathered rows (8..15 zero)
+  __shared__ float red[4][16][17];
+  __shared__ float w2s[16][GHB];        // W2 (rows past FO zero)
+  __shared__ float w1c[GHB][16];        // W1 columns of this member's units
+  __shared__ float hv1[GHB], hv2[GHB], hb1[GHB];
+  __shared__ float gam_s[SL_MAXL][16];
+  __shared__ float vts[3][16][16];      // vt[o][blk H + unit], blocks i, g, o (rows past FO zero)
+  __shared__ float wmc[16][16];         // W_ms^T[o][unit]
+  __shared__ float dys[GL_ROWS][16];
+  __shared__ float dzs[GL_ROWS][GHB + 1];
+  __shared__ float msum[GL_ROWS][2];
+  __shared__ float part[GL_ROWS][33];
+  __shared__ int sdead, xflag;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = blockIdx.x % p.ngroups, j = blockIdx.x / p.ngroups;
+  const int r0 = GL_ROWS * g, B = p.B, T = p.T, FO = p.FO, nl = p.nl;
+  unsigned long long* bdg = p.ring;
+  unsigned long long* bsum = bdg + (long)B * SB_KD;
+  unsigned long long* bdyx = bsum + (long)B * 32;
+  unsigned long long* slots = bdyx + (long)B * 256;
+  bool dead = false;
+  for (int i = tid; i < 16 * KP; i += 256) (&A[0][0])[i] = 0.0f;
+  {
+    const int o = tid >> 4, n = tid & 15, u = 16 * j + n;
+    const bool ov = o < FO;
+    for (int i = tid; i < 16 * GHB; i += 256) w2s[i / GHB][i % GHB] = i / GHB < FO ? p.w2[i] : 0.0f;
+    for (int i = tid; i < GHB * 16; i += 256) w1c[i >> 4][i & 15] = p.w1[(long)(i >> 4) * GE + 16 * j + (i & 15)];
+    if (tid < GHB) {
+      hv1[tid] = p.v[2 * tid];
+      hv2[tid] = p.v[2 * tid + 1];
+      hb1[tid] = p.b1[tid];
+    }
+    if (tid < 16 * nl) gam_s[tid >> 4][tid & 15] = p.L[tid >> 4].ln_g[16 * j + (tid & 15)];
+    vts[0][o][n] = ov ? p.vt[(long)o * 4 * GE + u] : 0.0f;
+    vts[1][o][n] = ov ? p.vt[(long)o * 4 * GE + 2 * GE + u] : 0.0f;
+    vts[2][o][n] = ov ? p.vt[(long)o * 4 * GE + 3 * GE + u] : 0.0f;
+    wmc[o][n] = ov ? p.wms[(long)o * GE + u] : 0.0f;
+  }
+  if (tid == 0) sdead = 0;
+  const int local = group_on_one_xcd<GL_MEM>(slots + (long)g * GL_MEM, j, p.err, dead, &xflag);
+  __syncthreads();
+  const int m8 = tid >> 4, n16 = tid & 15;
+  const int b8 = r0 + m8, bc = min(b8, B - 1);
+  const bool ep = tid < GL_ROWS * 16 && b8 < B;
+  const int u = 16 * j + n16;
+  const int c16 = lane & 15;
+  if (p.stamps && blockIdx.x == 0 && tid == 0) p.stamps[15] = (unsigned long long)local;
+  // pending saved-tensor stores, issued after the next hand-off poll (see the forward)
+  float* pa[SB_NP];
+  float pv[SB_NP];
+#pragma unroll
+  for (int s = 0; s < SB_NP; ++s) {
+    pa[s] = nullptr;
+    pv[s] = 0.0f;
+  }
+  auto flush = [&]() {
+#pragma unroll
+    for (int s = 0; s < SB_NP; ++s) {
+      if (pa[s]) *pa[s] = pv[s];
+      pa[s] = nullptr;
+    }
+  };
+  auto defer = [&](int s, float* a, float v) {
+    pa[s] = a;
+    pv[s] = v;
+  };
+  // zero-state cell backward of unit u (c0 = 0: d f = 0), the four dG values pending from slot s
+  auto cell_bwd = [&](const SsdBwdLayer& Ly, long row, float gv, float ig, float gg, float og, float cc, int s,
+                      float& d_i, float& d_g, float& d_o) {
+    const float tc = tanhf_(cc);
+    const float dc = gv * og * (1.0f - tc * tc);
+    d_i = dc * gg * ig * (1.0f - ig);
+    d_g = dc * ig * (1.0f - gg * gg);
+    d_o = gv * tc * og * (1.0f - og);
+    float* d = Ly.dG + row * 4 * GE + u;
+    defer(s, d, d_i);
+    defer(s + 1, d + GE, 0.0f);
+    defer(s + 2, d + 2 * GE, d_g);
+    defer(s + 3, d + 3 * GE, d_o);
+  };
+  float gprev = 0.0f;   // g of the layer whose dX the next D stage forms (own column)
+  for (int it = 0; it < T && !sdead; ++it) {
+    const int t = T - 1 - it;
+    const long rt = (long)t * B;
+    SB_STAMP(0);
+    // ---- F: the last layer
+    {
+      const SsdBwdLayer& Ly = p.L[nl - 1];
+      const long row = rt + bc;
+      const float hx = Ly.Hs[row * GE + u] + Ly.X[row * GE + u];
+      const float mn = Ly.mean[row], rs = Ly.rstd[row];
+      const float ig = Ly.G[row * 4 * GE + u], gg = Ly.G[row * 4 * GE + 2 * GE + u];
+      const float og = Ly.G[row * 4 * GE + 3 * GE + u], cc = Ly.C[row * GE + u];
+      const int mz = tid >> 5, jz = tid & 31, bz = min(r0 + mz, B - 1);
+      const float z0 = p.z[(rt + bz) * GHB + jz], z1 = p.z[(rt + bz) * GHB + jz + 32];
+      const bool dyv = tid < GL_ROWS * 16 && n16 < FO && b8 < B;
+      const float dyin = dyv ? p.dy[((long)b8 * T + t) * FO + n16] : 0.0f;
+      const bool fed = it > 0 && p.mask[t] != 0;
+      if (it > 0) gl_gather<256>(bdyx, r0, B, (unsigned)it, &A[0][0], KP, p.err, dead, &sdead);
+      __syncthreads();
+      flush();
+      SB_STAMP(1);
+      if (tid < GL_ROWS * 16) {
+        float dyx = 0.0f;
+#pragma unroll
+        for (int jm = 0; jm < GL_MEM; ++jm) dyx += A[m8][16 * jm + n16];
+        const float v = dyv ? dyin + (fed ? dyx : 0.0f) : 0.0f;
+        dys[m8][n16] = v;
+        if (j == 0 && dyv) defer(0, p.dyt + (rt + b8) * FO + n16, v);
+      }
+      __syncthreads();
+      float m0 = 0.0f, m1 = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int jh = jz + 32 * i;
+        const float zv = i ? z1 : z0;
+        float acc = 0.0f;
+#pragma unroll
+        for (int o = 0; o < 16; ++o) acc = fmaf(dys[mz][o], w2s[o][jh], acc);
+        const float d = zv > 0.0f ? acc : 0.0f;
+        dzs[mz][jh] = d;
+        if (j == 0 && r0 + mz < B) defer(1 + i, p.dz + (rt + r0 + mz) * GHB + jh, d);
+        m0 = fmaf(d, hv1[jh], m0);
+        m1 = fmaf(d, (zv - hb1[jh]) - hv2[jh], m1);
+      }
+#pragma unroll
+      for (int o = 16; o >= 1; o >>= 1) {
+        m0 += __shfl_xor(m0, o, 64);
+        m1 += __shfl_xor(m1, o, 64);
+      }
+      if (jz == 0) {
+        msum[mz][0] = m0;
+        msum[mz][1] = m1;
+      }
+      __syncthreads();
+      if (ep) {
+        float du = 0.0f;
+#pragma unroll 16
+        for (int jh = 0; jh < GHB; ++jh) du = fmaf(dzs[m8][jh], w1c[jh][n16], du);
+        defer(3, p.du + (rt + b8) * GE + u, du);
+        const float xh = (hx - mn) * rs;
+        const float gd = du * gam_s[nl - 1][n16];
+        const float gv = rs * (gd - msum[m8][0] / (float)GE - xh * (msum[m8][1] / (float)GE));
+        defer(4, Ly.g + (rt + b8) * GE + u, gv);
+        float d_i, d_g, d_o;
+        cell_bwd(Ly, rt + b8, gv, ig, gg, og, cc, 5, d_i, d_g, d_o);
+        const unsigned tag = (unsigned)(it * nl + 1);
+        unsigned long long* q = bdg + (long)b8 * SB_KD + u;
+        put_granule(q, tag, d_i, local);
+        put_granule(q + GE, tag, d_g, local);
+        put_granule(q + 2 * GE, tag, d_o, local);
+        gprev = gv;
+      }
+      SB_STAMP(2);
+    }
+    for (int l = nl - 1; l >= 1; --l) {
+      const SsdBwdLayer& Ly = p.L[l];
+      const SsdBwdLayer& Lb = p.L[l - 1];
+      const unsigned tag = (unsigned)(it * nl + (nl - 1 - l) + 1);
+      // ---- D: dX_l = dG W_ih + g (own columns), the partial row sums of LayerNorm l-1's backward
+      float gd = 0.0f, xh = 0.0f, rs = 0.0f, ig = 0.0f, gg = 0.0f, og = 0.0f, cc = 0.0f;
+      {
+        GlW<SB_KD> f;
+        const float* wr = Ly.w_t + (long)(16 * j + c16) * 4 * GE;
+#pragma unroll
+        for (int i = 0; i < SB_KD / 64; ++i) {
+          const int kk = wave * (SB_KD / 4) + 16 * i + 4 * (lane >> 4);
+          f.v[i] = *reinterpret_cast<const float4*>(wr + (kk < GE ? kk : kk + GE));
+        }
+        const long row = rt + bc;
+        const float hx = Lb.Hs[row * GE + u] + Lb.X[row * GE + u];
+        const float mn = Lb.mean[row];
+        rs = Lb.rstd[row];
+        ig = Lb.G[row * 4 * GE + u]; gg = Lb.G[row * 4 * GE + 2 * GE + u];
+        og = Lb.G[row * 4 * GE + 3 * GE + u]; cc = Lb.C[row * GE + u];
+        gl_gather<SB_KD>(bdg, r0, B, tag, &A[0][0], KP, p.err, dead, &sdead);
+        __syncthreads();
+        flush();
+        SB_STAMP(3 + 4 * (nl - 1 - l));
+        {
+          const gv4 acc = gl_mma<SB_KD>(&A[0][0], KP, f, lane, wave);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) red[wave][4 * (lane >> 4) + i][lane & 15] = acc[i];
+        }
+        __syncthreads();
+        float s0 = 0.0f, s1 = 0.0f;
+        if (tid < GL_ROWS * 16) {
+          const float dx = ((red[0][m8][n16] + red[1][m8][n16]) + (red[2][m8][n16] + red[3][m8][n16])) + gprev;
+          if (ep) defer(0, Ly.dX + (rt + b8) * GE + u, dx);
+          xh = (hx - mn) * rs;
+          gd = ep ? dx * gam_s[l - 1][n16] : 0.0f;
+          s0 = gd;
+          s1 = gd * xh;
+        }
+        s0 = group_sum<16>(s0);
+        s1 = group_sum<16>(s1);
+        if (ep && n16 < 2) put_granule(bsum + (long)b8 * 32 + 2 * j + n16, tag, n16 ? s1 : s0, local);
+        SB_STAMP(4 + 4 * (nl - 1 - l));
+      }
+      // ---- B: LayerNorm l-1 and cell backward (own columns); publish dG, or the partial dyx
+      {
+        const int row = tid >> 5, e = tid & 31;
+        int idx[1] = {min(r0 + row, B - 1) * 32 + e};
+        float v[1];
+        if (sdead) dead = true;
+        get_granules_idx<1>(bsum, idx, tag, v, p.err, dead);
+        part[row][e] = r0 + row < B ? v[0] : 0.0f;
+        if (dead) sdead = 1;
+        __syncthreads();
+        flush();
+        SB_STAMP(5 + 4 * (nl - 1 - l));
+        float d_i = 0.0f, d_g = 0.0f, d_o = 0.0f, gv = 0.0f;
+        if (ep) {
+          float q0 = 0.0f, q1 = 0.0f;
+#pragma unroll
+          for (int jm = 0; jm < GL_MEM; ++jm) {
+            q0 += part[m8][2 * jm];
+            q1 += part[m8][2 * jm + 1];
+          }
+          gv = rs * (gd - q0 / (float)GE - xh * (q1 / (float)GE));
+          defer(1, Lb.g + (rt + b8) * GE + u, gv);
+          cell_bwd(Lb, rt + b8, gv, ig, gg, og, cc, 2, d_i, d_g, d_o);
+        }
+        if (l - 1 > 0) {
+          if (ep) {
+            const unsigned tg = (unsigned)(it * nl + (nl - l) + 1);
+            unsigned long long* q = bdg + (long)b8 * SB_KD + u;
+            put_granule(q, tg, d_i, local);
+            put_granule(q + GE, tg, d_g, local);
+            put_granule(q + 2 * GE, tg, d_o, local);
+            gprev = gv;
+          }
+        } else {
+          // partial dyx(t)[b][o] = sum over own units of dG . vt[o] + g . W_ms^T[o] (lane n16: output o = n16)
+          float mine = 0.0f;
+#pragma unroll
+          for (int o = 0; o < 16; ++o) {
+            float q = fmaf(d_i, vts[0][o][n16], fmaf(d_g, vts[1][o][n16], fmaf(d_o, vts[2][o][n16], gv * wmc[o][n16])));
+            q = group_sum<16>(q);
+            mine = (n16 == o) ? q : mine;
+          }
+          if (ep) put_granule(bdyx + (long)b8 * 256 + 16 * j + n16, (unsigned)(it + 1), mine, local);
+        }
+        SB_STAMP(6 + 4 * (nl - 1 - l));
+      }
+    }
+  }
+  flush();
+}
+
 }  // namespace mrg
 
 using namespace mrg;
@@ -385,4 +684,68 @@ MRG_API int mrg_ssd_loop_fwd(int B, int T, int H, int HB, int FO, int F, int nl,
   a.stamps = g_ssd_stamps;
   klaunch(ssd_loop_kernel, dim3(GL_MEM * a.ngroups), 256, 0, stream, a);
   return check_launch("ssd_loop_kernel");
+}
+
+static unsigned long long* g_ssd_bwd_stamps = nullptr;
+// Diagnostics (tools/ssd_stamps.py): later mrg_ssd_loop_bwd launches write block 0's per-stage
+// shader-clock stamps into buf ([T][16] u64 by backward iteration; slot 15 of iteration 0: the local
+// hand-off flag); null = off.
+MRG_API int mrg_ssd_loop_bwd_debug_stamps(void* buf) {
+  g_ssd_bwd_stamps = static_cast<unsigned long long*>(buf);
+  return 0;
+}
+
+// Bytes of the granule ring mrg_ssd_loop_bwd needs for B rows (zeroed by the caller before every launch).
+MRG_API long mrg_ssd_loop_bwd_ring_bytes(int B) {
+  const int ng = (B + GL_ROWS - 1) / GL_ROWS;
+  return ((long)B * (SB_KD + 32 + 256) + (long)ng * GL_MEM) * 8;
+}
+
+MRG_API int mrg_ssd_loop_bwd_fits(int B, int cus) {
+  const long nblk = (long)GL_MEM * ((B + GL_ROWS - 1) / GL_ROWS);
+  return fits(ssd_loop_bwd_kernel, 256, nblk, cus > 0 ? cus : device_cus()) ? 1 : 0;
+}
+
+// The scheduled-sampling decode's backward frame loop (nl >= 2 layers) in one persistent launch
+// (ssd_loop_bwd_kernel; replaces decode.py's per-frame mrg_ssd_ffn_bwd / mrg_ssd_dx /
+// mrg_ssd_ln_cell_bwd sequence with the same outputs).  H = 256, HB = 64, FO <= 16, 2 <= nl <= 4.
+// lptrs (host array, 11 per layer): W_ih^T [H][4H] (null for layer 0), the gamma of the LayerNorm
+// after the layer, the forward's saved X, gates, c, h and that LayerNorm's mean / rstd, then the
+// outputs g = d(h + x) [T][B][H], dG [T][B][4H] and dX [T][B][H] (layers >= 1; null for layer 0).
+// dy [B][T][FO]; mask [T] bytes; w1 [HB][H], w2 [FO][HB], b1, v = [W1 gamma | W1 beta] [HB][2] of the
+// last LayerNorm; z [T][B][HB]; vt = W_ms^T W_ih0 [FO][4H]; wms_t [FO][H]; outputs dyt [T][B][FO],
+// dz [T][B][HB], du [T][B][H]; ring: mrg_ssd_loop_bwd_ring_bytes of zeroed memory; err as the forward's.
+MRG_API int mrg_ssd_loop_bwd(int B, int T, int H, int HB, int FO, int nl, const void* const* lptrs, int nptrs,
+                             const float* dy, const unsigned char* mask, const float* w1, const float* w2,
+                             const float* b1, const float* v, const float* z, const float* vt, const float* wms_t,
+                             float* dyt, float* dz, float* du, void* ring, int* err, hipStream_t stream) {
+  if (B == 0 || T == 0) return 0;
+  MRG_REQUIRE(H == GE && HB == GHB && FO >= 1 && FO <= 16 && nl >= 2 && nl <= SL_MAXL,
+              "mrg_ssd_loop_bwd: needs H = %d, HB = %d, 1 <= FO <= 16, 2 <= nl <= %d (H=%d HB=%d FO=%d nl=%d)", GE,
+              GHB, SL_MAXL, H, HB, FO, nl);
+  MRG_REQUIRE(lptrs && nptrs == SL_PER_LAYER * nl && dy && mask && w1 && w2 && b1 && v && z && vt && wms_t && dyt &&
+                  dz && du && ring && err,
+              "mrg_ssd_loop_bwd: null argument or nptrs %d != %d", nptrs, SL_PER_LAYER * nl);
+  MRG_REQUIRE(mrg_ssd_loop_bwd_fits(B, 0) == 1, "mrg_ssd_loop_bwd: %d workgroups cannot all be resident (B=%d)",
+              GL_MEM * ((B + GL_ROWS - 1) / GL_ROWS), B);
+  SsdBwdArgs a{};
+  for (int i = 0; i < nl; ++i) {
+    const void* const* q = lptrs + SL_PER_LAYER * i;
+    for (int k = 0; k < SL_PER_LAYER; ++k) {
+      const bool optional = i == 0 && (k == 0 || k == 10);
+      MRG_REQUIRE(optional || q[k] != nullptr, "mrg_ssd_loop_bwd: null pointer %d of layer %d", k, i);
+    }
+    SsdBwdLayer& L = a.L[i];
+    L.w_t = static_cast<const float*>(q[0]); L.ln_g = static_cast<const float*>(q[1]);
+    L.X = static_cast<const float*>(q[2]); L.G = static_cast<const float*>(q[3]);
+    L.C = static_cast<const float*>(q[4]); L.Hs = static_cast<const float*>(q[5]);
+    L.mean = static_cast<const float*>(q[6]); L.rstd = static_cast<const float*>(q[7]);
+    L.g = (float*)q[8]; L.dG = (float*)q[9]; L.dX = (float*)q[10];
+  }
+  a.dy = dy; a.mask = mask; a.w1 = w1; a.w2 = w2; a.b1 = b1; a.v = v; a.z = z; a.vt = vt; a.wms = wms_t;
+  a.dyt = dyt; a.dz = dz; a.du = du; a.ring = static_cast<unsigned long long*>(ring); a.err = err;
+  a.B = B; a.T = T; a.FO = FO; a.nl = nl; a.ngroups = (B + GL_ROWS - 1) / GL_ROWS;
+  a.stamps = g_ssd_bwd_stamps;
+  klaunch(ssd_loop_bwd_kernel, dim3(GL_MEM * a.ngroups), 256, 0, stream, a);
+  return check_launch("ssd_loop_bwd_kernel");
 }

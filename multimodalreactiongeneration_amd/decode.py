@@ -37,6 +37,9 @@ F32 = torch.float32
 # the forward frame loop as ONE persistent launch (ssd_loop.hip) when H = 256, HB = 64, FO <= 16,
 # nl <= 4 and its grid fits; MRG_SSD_LOOP=0 keeps the L + 1 launches per frame
 _LOOP = [os.environ.get("MRG_SSD_LOOP", "1") == "1"]
+# the backward frame loop likewise (ssd_loop.hip ssd_loop_bwd_kernel; nl >= 2); MRG_SSD_LOOP_BWD=0
+# keeps the 2L launches per frame
+_LOOP_BWD = [os.environ.get("MRG_SSD_LOOP_BWD", "1") == "1"]
 
 
 class _SSDecodeFn(Function):
@@ -164,7 +167,20 @@ class _SSDecodeFn(Function):
             vt = torch.empty(FM, 4 * H, device=dev, dtype=F32)
             gemm(FM, 4 * H, H, _ptr(wms_t), 0, H, _ptr(layers[0][0]), 1, H, _ptr(vt), 4 * H, device=dev)
             dyx = torch.empty(T, B, FM, device=dev, dtype=F32)
-        for t in range(T - 1, -1, -1):
+        loop = (ext and _LOOP_BWD[0] and H == 256 and HB == 64 and FO <= 16 and nl <= 4
+                and lib.mrg_ssd_loop_bwd_fits(B, 0) == 1)
+        if loop:
+            lp = []
+            for i, lay in enumerate(layers):
+                lp += [w_t[i], lay[4], X[i], G[i], C[i], Hs[i], stats[i][0], stats[i][1], gs[i], dG[i],
+                       dX[i] if i else None]
+            lpa = (ctypes.c_void_p * len(lp))(*[_ptr(q) for q in lp])
+            ring = torch.zeros(max(1, lib.mrg_ssd_loop_bwd_ring_bytes(B) // 8), dtype=torch.int64, device=dev)
+            _lib.check(lib.mrg_ssd_loop_bwd(
+                B, T, H, HB, FO, nl, lpa, len(lp), _ptr(dy), _ptr(mask), _ptr(w1), _ptr(w2), _ptr(b1), _ptr(v),
+                _ptr(Z), _ptr(vt), _ptr(wms_t), _ptr(dyt), _ptr(dz), _ptr(duL), _ptr(ring), _ptr(_err_flag(dev)),
+                _stream()), "ssd loop bwd")
+        for t in (range(T - 1, -1, -1) if not loop else ()):
             for i in range(nl - 1, -1, -1):
                 cell = (_ptr(gs[i], t * slab), _ptr(G[i], t * gslab), _ptr(C[i], t * slab), _ptr(dG[i], t * gslab))
                 if i == nl - 1:

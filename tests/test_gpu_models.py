@@ -998,7 +998,8 @@ def test_generation_fused_frame_loop_matches_module_path(B, T, loop):
 def test_ssd_persistent_loop_matches_per_frame_launches(B, T, nl, FO):
     """The scheduled-sampling decode's forward frame loop as ONE persistent launch (ssd_loop.hip: 16
     workgroups per 8 rows, each layer's h handed over as granules, buffers alternating by frame
-    parity) vs the L + 1 launches per frame of decode.hip, on the same inputs under a random sampling
+    parity) and its backward frame loop (ssd_loop_bwd_kernel, L >= 2), each on and off, vs the L + 1
+    forward and 2L backward launches per frame of decode.hip, on the same inputs under a random sampling
     mask, ragged B, 1..4 layers and 1..8 output features (the per-frame kernels take FO <= 8): the prediction and, through the backward
     that reads every saved tensor (X_f's ms columns, X, gates, c, h, LayerNorm statistics, U, Z), the
     sampler-output and every parameter gradient agree within fp32 reordering.
@@ -1023,10 +1024,10 @@ def test_ssd_persistent_loop_matches_per_frame_launches(B, T, nl, FO):
     mask = torch.from_numpy(np.random.RandomState(B + T).rand(T) < 0.5).to(DEV)
     dy = torch.randn(B, T, FO, generator=g).to(DEV)
     outs = []
-    prev = D._LOOP[0]
+    prev = D._LOOP[0], D._LOOP_BWD[0]
     try:
-        for loop in (True, False):
-            D._LOOP[0] = loop
+        for fwd, bwd in ((True, True), (False, True), (True, False), (False, False)):
+            D._LOOP[0], D._LOOP_BWD[0] = fwd, bwd
             ps = [t.clone().requires_grad_(True) for t in [base["w_f"], base["b_f"]] + sum(layers, []) + ffn]
             a = a_s.clone().requires_grad_(True)
             lay = [ps[2 + 6 * i:8 + 6 * i] for i in range(nl)]
@@ -1036,13 +1037,14 @@ def test_ssd_persistent_loop_matches_per_frame_launches(B, T, nl, FO):
             Fn.check_errors()
             outs.append((y.detach(), a.grad, [p.grad for p in ps]))
     finally:
-        D._LOOP[0] = prev
-    (y0, a0, g0), (y1, a1, g1) = outs
-    assert y0.shape == (B, T, FO)
-    assert rel_err(y0, y1) < 1e-5, rel_err(y0, y1)
-    assert rel_err(a0, a1) < 1e-5, rel_err(a0, a1)
-    for i, (p, q) in enumerate(zip(g0, g1)):
-        if q is None or q.abs().max() == 0:   # W_hh (zero state): exactly zero on both paths
-            assert p is None or p.abs().max() == 0, i
-            continue
-        assert rel_err(p, q) < 1e-5, (i, rel_err(p, q))
+        D._LOOP[0], D._LOOP_BWD[0] = prev
+    y1, a1, g1 = outs[-1]
+    for v, (y0, a0, g0) in enumerate(outs[:-1]):
+        assert y0.shape == (B, T, FO)
+        assert rel_err(y0, y1) < 1e-5, (v, rel_err(y0, y1))
+        assert rel_err(a0, a1) < 1e-5, (v, rel_err(a0, a1))
+        for i, (p, q) in enumerate(zip(g0, g1)):
+            if q is None or q.abs().max() == 0:   # W_hh (zero state): exactly zero on both paths
+                assert p is None or p.abs().max() == 0, (v, i)
+                continue
+            assert rel_err(p, q) < 1e-5, (v, i, rel_err(p, q))
