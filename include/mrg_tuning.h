@@ -49,11 +49,12 @@ int mrg_debug_stamp(void* buf, int slot, hipStream_t stream);
 /* Diagnostics: block 0's per-stage shader-clock stamps of later mrg_gen_loop launches ([T][32] u64;
  * slot 31 of frame 0: the group's local hand-off flag); null turns them off (tools/gen_stamps.py). */
 int mrg_gen_loop_debug_stamps(void* buf);
-/* Diagnostics: the same for mrg_ssd_loop_fwd ([T][16] u64: frame start, then per layer after its
- * input / after its publish, then the FFN stage; slot 15 of frame 0: the local hand-off flag)
- * (tools/ssd_stamps.py). */
+/* Diagnostics: per-stage 100 MHz real-time stamps (s_memrealtime, one clock for all CUs) of the 16
+ * members of row group 0 in later mrg_ssd_loop_fwd launches ([T][16 members][16] u64: frame start, then
+ * per layer after its input / after its publish, then the FFN stage; frame 0: slot 15 the local
+ * hand-off flag, slot 14 the HW_ID register) (tools/ssd_stamps.py). */
 int mrg_ssd_loop_debug_stamps(void* buf);
-/* Diagnostics: the same for mrg_ssd_loop_bwd ([T][16] u64 by backward iteration). */
+/* Diagnostics: the same for mrg_ssd_loop_bwd (by backward iteration). */
 int mrg_ssd_loop_bwd_debug_stamps(void* buf);
 /* Measurement (bench.py): while on, every kernel launched for a tagged library call (tag >= 0) is
  * timed by start / stop events bound to that kernel (hipExtLaunchKernelGGL): its own execution,

@@ -47,13 +47,24 @@ struct SsdLoopArgs {
   unsigned long long* stamps;     // diagnostics (mrg_ssd_loop_debug_stamps): [T][16] of block 0, or null
 };
 
-// block 0 / thread 0: shader-clock stamp `slot` of frame t (slot 15 of frame 0: the local hand-off flag)
+// thread 0 of each member of group 0: 100 MHz real-time stamp (s_memrealtime: one clock for every CU)
+// `slot` of frame t into stamps[t][member][slot] (frame 0 of each member: slot 15 the local hand-off
+// flag, slot 14 the hardware id register)
 #define SL_STAMP(slot)                                                                   \
   do {                                                                                   \
-    if (p.stamps && blockIdx.x == 0 && threadIdx.x == 0) {                               \
+    if (p.stamps && g == 0 && threadIdx.x == 0) {                                        \
       unsigned long long _t;                                                             \
-      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");         \
-      p.stamps[(long)t * 16 + (slot)] = _t;                                              \
+      asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");     \
+      p.stamps[((long)t * GL_MEM + j) * 16 + (slot)] = _t;                               \
+    }                                                                                    \
+  } while (0)
+#define SL_STAMP_ID()                                                                    \
+  do {                                                                                   \
+    if (p.stamps && g == 0 && threadIdx.x == 0) {                                        \
+      unsigned _id;                                                                      \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(_id));                  \
+      p.stamps[(long)j * 16 + 15] = (unsigned long long)local;                           \
+      p.stamps[(long)j * 16 + 14] = (unsigned long long)_id;                             \
     }                                                                                    \
   } while (0)
 
@@ -114,7 +125,7 @@ __global__ __launch_bounds__(256) void ssd_loop_kernel(SsdLoopArgs p) {
   const bool ep = tid < GL_ROWS * 16 && b8 < B;
   const int c16 = lane & 15;                 // this lane's tile column (weight row) in the products
   const int u = 16 * j + n16;                // the epilogue thread's hidden unit
-  if (p.stamps && blockIdx.x == 0 && tid == 0) p.stamps[15] = (unsigned long long)local;
+  SL_STAMP_ID();
   // Saved-tensor stores are deferred to just after the NEXT hand-off poll: on gfx9 a store holds a
   // vmcnt slot until the memory acknowledges it, and the counter retires in order, so stores issued
   // before a poll would sit in front of the poll's loads.  Pending: one layer's gate / cell / input
@@ -360,10 +371,10 @@ struct SsdBwdArgs {
 
 #define SB_STAMP(slot)                                                                   \
   do {                                                                                   \
-    if (p.stamps && blockIdx.x == 0 && threadIdx.x == 0) {                               \
+    if (p.stamps && g == 0 && threadIdx.x == 0) {                                        \
       unsigned long long _t;                                                             \
-      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");         \
-      p.stamps[(long)it * 16 + (slot)] = _t;                                             \
+      asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");     \
+      p.stamps[((long)it * GL_MEM + j) * 16 + (slot)] = _t;                              \
     }                                                                                    \
   } while (0)
 
@@ -415,7 +426,7 @@ __global__ __launch_bounds__(256) void ssd_loop_bwd_kernel(SsdBwdArgs p) {
   const bool ep = tid < GL_ROWS * 16 && b8 < B;
   const int u = 16 * j + n16;
   const int c16 = lane & 15;
-  if (p.stamps && blockIdx.x == 0 && tid == 0) p.stamps[15] = (unsigned long long)local;
+  SL_STAMP_ID();
   // pending saved-tensor stores, issued after the next hand-off poll (see the forward)
   float* pa[SB_NP];
   float pv[SB_NP];
@@ -624,8 +635,9 @@ __global__ __launch_bounds__(256) void ssd_loop_bwd_kernel(SsdBwdArgs p) {
 using namespace mrg;
 
 static unsigned long long* g_ssd_stamps = nullptr;
-// Diagnostics (tools/ssd_stamps.py): later mrg_ssd_loop_fwd launches write block 0's per-stage
-// shader-clock stamps into buf ([T][16] u64; slot 15 of frame 0: the group's local hand-off flag); null = off.
+// Diagnostics (tools/ssd_stamps.py): later mrg_ssd_loop_fwd launches write group 0's members' per-stage
+// real-time (10 ns) stamps into buf ([T][16 members][16] u64; frame 0: slot 15 the local hand-off flag,
+// 14 the HW_ID register); null = off.
 MRG_API int mrg_ssd_loop_debug_stamps(void* buf) {
   g_ssd_stamps = static_cast<unsigned long long*>(buf);
   return 0;
@@ -687,9 +699,8 @@ MRG_API int mrg_ssd_loop_fwd(int B, int T, int H, int HB, int FO, int F, int nl,
 }
 
 static unsigned long long* g_ssd_bwd_stamps = nullptr;
-// Diagnostics (tools/ssd_stamps.py): later mrg_ssd_loop_bwd launches write block 0's per-stage
-// shader-clock stamps into buf ([T][16] u64 by backward iteration; slot 15 of iteration 0: the local
-// hand-off flag); null = off.
+// Diagnostics (tools/ssd_stamps.py): later mrg_ssd_loop_bwd launches write group 0's members' per-stage
+// real-time (10 ns) stamps into buf ([T][16 members][16] u64 by backward iteration, as the forward's); null = off.
 MRG_API int mrg_ssd_loop_bwd_debug_stamps(void* buf) {
   g_ssd_bwd_stamps = static_cast<unsigned long long*>(buf);
   return 0;
