@@ -43,7 +43,8 @@ FAMILIES = {
     "attn_bwd": "attn_bwd_fused_kernel",                         # 10D FLOP per visible pair per head
     "gru_fwd": "gru_fwd_kernel",                                 # 6H^2 FLOP per (b, t) per layer
     "gru_bwd": "gru_bwd_kernel",                                 # 6H^2 FLOP per (b, t) per layer
-    "gen": "gen_lstm+gen_linear+gen_ffn",                        # generation frame loop, 2MNK FLOP per launch
+    "gen": "gen_loop_kernel (or gen_lstm+gen_linear+gen_ffn)",   # generation frame loop, 2MNK FLOP per launch
+    "ssd": "ssd_loop_kernel+ssd_loop_bwd_kernel",                # C3 frame loops, their products' 2MNK FLOP
 }
 PEAK_NOTES = {
     "gemm": "f32 dense matrix peak; x6 bf16 split's own MFMA ceiling 416.7",
@@ -51,7 +52,8 @@ PEAK_NOTES = {
     "lstm_bwd": "latency-bound recurrence; f32 VALU peak",
     "gru_fwd": "latency-bound recurrence; f32 VALU peak",
     "gru_bwd": "latency-bound recurrence; f32 VALU peak",
-    "gen": "launch-latency-bound 64-row products (26 dependent launches per frame); f32 matrix peak",
+    "gen": "hand-off-latency-bound 8-row products (26 hand-off stages per frame, one launch); f32 matrix peak",
+    "ssd": "hand-off-latency-bound 8-row products (2 forward / 3 backward hand-offs per frame); f32 matrix peak",
 }
 HEADLINE_MAX_BYTES = 8000   # the driver parses the LAST stdout line; keep it well inside its window
 # rocprofv3 kernel-name prefix of each family in the PMC summary (tools/tools_pmc_summary.py)
@@ -741,9 +743,10 @@ def secondary(args, dev):
         opt.step()
     replay = capture(step_c3, 2, preserve=opt.state_tensors())
     ms = _timed_replay(replay, K, W, pre=refresh)
-    # no per-family brackets here: ~2100 launches of 3-6 us per step, where eager HIP-event brackets
-    # time host gaps, not kernels (r02: families summed past the step); profiles/ has the rocprof split
-    kern = ({}, None)
+    # per-family kernel time from kernel-bound probes: the frame loops are two launches (the "ssd"
+    # family), the rest ~100 launches (sampler recurrences, products over all frames)
+    refresh()
+    kern = _probe_steps(step_c3)
     cpu = None
     if cpu_on:
         info = _cpu_setup(args)

@@ -31,7 +31,7 @@ import torch
 from torch.autograd import Function
 
 from . import _lib
-from .functional import _err_flag, _gbuf, _keeps_precision, _ptr, _resln_bwd, _stream, _wgrad, _side, gemm
+from .functional import _err_flag, _gbuf, _keeps_precision, _probe, _ptr, _resln_bwd, _stream, _wgrad, _side, gemm
 
 F32 = torch.float32
 # the forward frame loop as ONE persistent launch (ssd_loop.hip) when H = 256, HB = 64, FO <= 16,
@@ -92,10 +92,13 @@ class _SSDecodeFn(Function):
                 lp += [w_ih, b_ih, b_hh, g_, b_, X[i], G[i], C[i], Hs[i], stats[i][0], stats[i][1]]
             lpa = (ctypes.c_void_p * len(lp))(*[_ptr(q) for q in lp])
             ring = torch.zeros(max(1, lib.mrg_ssd_loop_ring_bytes(B, nl) // 8), dtype=torch.int64, device=dev)
-            _lib.check(lib.mrg_ssd_loop_fwd(
-                B, T, H, HB, FO, F, nl, eps, lpa, len(lp), _ptr(P), _ptr(wms_t), _ptr(w1), _ptr(b1), _ptr(w2),
-                _ptr(b2), _ptr(msc), msc.stride(0), msc.stride(1), _ptr(mask), _ptr(xf, SA + FMp), _ptr(U), _ptr(Z),
-                _ptr(y), _ptr(ring), _ptr(_err_flag(dev)), _stream()), "ssd loop fwd")
+            # algorithmic FLOPs (bench's "ssd" family): gates 8H^2 per row and layer, FFN, the ms columns
+            flop = 2.0 * T * B * (4 * H * H * nl + H * HB + HB * FO + FO * H)
+            with _probe("ssd", flop):
+                _lib.check(lib.mrg_ssd_loop_fwd(
+                    B, T, H, HB, FO, F, nl, eps, lpa, len(lp), _ptr(P), _ptr(wms_t), _ptr(w1), _ptr(b1), _ptr(w2),
+                    _ptr(b2), _ptr(msc), msc.stride(0), msc.stride(1), _ptr(mask), _ptr(xf, SA + FMp), _ptr(U),
+                    _ptr(Z), _ptr(y), _ptr(ring), _ptr(_err_flag(dev)), _stream()), "ssd loop fwd")
             T_launch = 0
         else:
             T_launch = T
@@ -176,10 +179,13 @@ class _SSDecodeFn(Function):
                        dX[i] if i else None]
             lpa = (ctypes.c_void_p * len(lp))(*[_ptr(q) for q in lp])
             ring = torch.zeros(max(1, lib.mrg_ssd_loop_bwd_ring_bytes(B) // 8), dtype=torch.int64, device=dev)
-            _lib.check(lib.mrg_ssd_loop_bwd(
-                B, T, H, HB, FO, nl, lpa, len(lp), _ptr(dy), _ptr(mask), _ptr(w1), _ptr(w2), _ptr(b1), _ptr(v),
-                _ptr(Z), _ptr(vt), _ptr(wms_t), _ptr(dyt), _ptr(dz), _ptr(duL), _ptr(ring), _ptr(_err_flag(dev)),
-                _stream()), "ssd loop bwd")
+            # dX = dG W_ih over the 3 nonzero gate blocks per lower layer, FFN backward, the dyx products
+            flop = 2.0 * T * B * (3 * H * H * (nl - 1) + HB * (H + FO) + FO * 4 * H)
+            with _probe("ssd", flop):
+                _lib.check(lib.mrg_ssd_loop_bwd(
+                    B, T, H, HB, FO, nl, lpa, len(lp), _ptr(dy), _ptr(mask), _ptr(w1), _ptr(w2), _ptr(b1), _ptr(v),
+                    _ptr(Z), _ptr(vt), _ptr(wms_t), _ptr(dyt), _ptr(dz), _ptr(duL), _ptr(ring),
+                    _ptr(_err_flag(dev)), _stream()), "ssd loop bwd")
         for t in (range(T - 1, -1, -1) if not loop else ()):
             for i in range(nl - 1, -1, -1):
                 cell = (_ptr(gs[i], t * slab), _ptr(G[i], t * gslab), _ptr(C[i], t * slab), _ptr(dG[i], t * gslab))
