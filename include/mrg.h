@@ -273,8 +273,8 @@ int mrg_ssd_loop_fwd(int B, int T, int H, int HB, int FO, int F, int nl, float e
  * conditions as the forward loop): per frame the last layer's FFN / LayerNorm / cell backward needs no
  * exchange (the row sums through v), then per lower layer one hand-off of dG rows (dX = dG W_ih + g
  * on MFMA) and one of partial LayerNorm row sums, and the bottom layer's partial dyx feeds the
- * previous frame.  lptrs: 11 per layer (W_ih^T [H][4H] or null for layer 0, the LayerNorm gamma, the
- * forward's X, gates, c, h, mean, rstd, then g, dG and dX (null for layer 0)); dy [B][T][FO]; v =
+ * previous frame.  lptrs: 12 per layer (W_ih [4H][H] or null for layer 0, the LayerNorm gamma and
+ * beta, the forward's X, gates, c, h, mean, rstd, then g, dG and dX (null for layer 0)); dy [B][T][FO]; v =
  * [W1 gamma | W1 beta] [HB][2]; z [T][B][HB]; vt = W_ms^T W_ih0 [FO][4H]; outputs dyt [T][B][FO], dz
  * [T][B][HB], du [T][B][H]; ring: mrg_ssd_loop_bwd_ring_bytes(B) of zeroed memory per launch.       */
 long mrg_ssd_loop_bwd_ring_bytes(int B);

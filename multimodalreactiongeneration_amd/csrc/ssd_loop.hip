@@ -338,20 +338,24 @@ __global__ __launch_bounds__(256) void ssd_loop_kernel(SsdLoopArgs p) {
 //   F  gather the 16 members' partial dyx(t+1) -> dy_total = dy(t) + mask[t] dyx(t+1) (every member
 //      its rows) -> dz = relu'(z) (dy_total W2) (all 64, per member) -> du = dz W1 (own columns) and
 //      the LayerNorm's two row sums through v = [W1 gamma | W1 beta] (no exchange, decode.hip's
-//      identity) -> g, the zero-state cell backward -> publish dG (i, g, o blocks) of the last layer
-//   D  (layer l = L-1 .. 1) gather dG rows -> dX_l = dG W_ih + g (own 16 columns, MFMA over the
-//      768 nonzero gate columns) -> the next LayerNorm backward's two partial row sums -> publish
-//   B  gather the partial sums -> LayerNorm backward of layer l-1 (own columns) -> cell backward ->
-//      publish dG (l-1 > 0), or at the bottom layer the partial dyx(t) = dfeat(t) W_ms over own units
-//      (dG vt^T + g wms^T, vt = W_ms^T W_ih0), which frame t - 1's F stage sums
-// so a frame is 1 + 2 (L - 1) hand-offs instead of 2L launches.  Hand-off buffers are single: a
-// member writes a buffer again only after a gather that needs every member past its last read.
-static constexpr int SB_KD = 3 * GE;   // dX product K: the i, g, o blocks (the f block of dG is zero)
+//      identity) -> g, the zero-state cell backward -> dG of the last layer's own units
+//   P  (after each dG of a layer l >= 1) this member's PARTIAL dX_l = dG[:, own gate columns] W_ih[own
+//      rows, :] over all 256 columns (MFMA, K = 48), and its partial LayerNorm row sums of layer l-1's
+//      backward over all columns: sum_k P[k] gamma[k] and sum_k P[k] (X_l[k] - beta[k]) (= gamma xh),
+//      plus the own columns' g terms -> publish
+//   B  gather the own columns of every member's partial and every member's row sums -> dX_l (own
+//      columns) = the sum + g -> LayerNorm backward of layer l-1 -> cell backward -> P for l-1 > 0, or
+//      at the bottom layer the partial dyx(t) = dfeat(t) W_ms over own units (dG vt^T + g wms^T,
+//      vt = W_ms^T W_ih0), which frame t - 1's F stage sums
+// so a frame is L hand-offs (2 at L = 2) instead of 2L launches.  The partial buffers alternate by
+// level (a member writes one again only after a gather that needs every member past its last read).
+static constexpr int SB_KP = 48;       // partial product K: the i, g, o gate columns of 16 units
 static constexpr int SB_NP = 10;       // pending saved-tensor stores per thread
+static constexpr int SB_PER_LAYER = 12;  // see mrg_ssd_loop_bwd
 
 struct SsdBwdLayer {
-  const float* w_t;                    // W_ih^T [H][4H] (layers >= 1)
-  const float* ln_g;                   // gamma of the LayerNorm after this layer
+  const float* w_ih;                   // W_ih [4H][H] (layers >= 1)
+  const float *ln_g, *ln_b;            // the LayerNorm after this layer
   const float *X, *G, *C, *Hs, *mean, *rstd;   // the forward's saved tensors
   float *g, *dG, *dX;                  // d(h + x) [T][B][H], dG [T][B][4H], dX (layers >= 1) [T][B][H]
 };
@@ -363,10 +367,10 @@ struct SsdBwdArgs {
   const float* z;                      // Z [T][B][HB]
   const float *vt, *wms;               // vt = W_ms^T W_ih0 [FO][4H], W_ms^T [FO][H]
   float *dyt, *dz, *du;                // [T][B][FO], [T][B][HB], [T][B][H]
-  unsigned long long* ring;            // dG [B][768] | partial sums [B][32] | dyx [B][256] granules, XCC slots
+  unsigned long long* ring;            // 2 x (partials [B][16][256] | sums [B][16][2]) | dyx [B][256] granules, XCC slots
   int* err;
   int B, T, FO, nl, ngroups;
-  unsigned long long* stamps;          // diagnostics: [T][16] of block 0 (mrg_ssd_loop_debug_stamps), or null
+  unsigned long long* stamps;          // diagnostics (mrg_ssd_loop_bwd_debug_stamps), or null
 };
 
 #define SB_STAMP(slot)                                                                   \
@@ -379,9 +383,14 @@ struct SsdBwdArgs {
   } while (0)
 
 __global__ __launch_bounds__(256) void ssd_loop_bwd_kernel(SsdBwdArgs p) {
-  constexpr int KP = SB_KD + 4;
-  __shared__ __attribute__((aligned(16))) float A[16][KP];   // gathered rows (8..15 zero)
-  __shared__ float red[4][16][17];
+  constexpr int DP = SB_KP + 4;
+  __shared__ __attribute__((aligned(16))) float A[GL_ROWS][GE + 4];   // gathered dyx partials
+  __shared__ __attribute__((aligned(16))) float dgs[16][DP];          // own dG (rows 8..15 zero)
+  __shared__ float ys[GL_ROWS][GE + 1];  // X_l - beta_{l-1} of the rows (the row sums' gamma xh)
+  __shared__ float gam_f[GE], bet_f[GE]; // gamma / beta of LayerNorm l-1 (full width, this stage)
+  __shared__ float parts[GL_ROWS][GL_MEM][17];   // gathered partials of the own columns
+  __shared__ float sums[GL_ROWS][2 * GL_MEM];
+  __shared__ float rsum[4][GL_ROWS][2];  // per-wave partial row sums
   __shared__ float w2s[16][GHB];        // W2 (rows past FO zero)
   __shared__ float w1c[GHB][16];        // W1 columns of this member's units
   __shared__ float hv1[GHB], hv2[GHB], hb1[GHB];
@@ -391,17 +400,17 @@ __global__ __launch_bounds__(256) void ssd_loop_bwd_kernel(SsdBwdArgs p) {
   __shared__ float dys[GL_ROWS][16];
   __shared__ float dzs[GL_ROWS][GHB + 1];
   __shared__ float msum[GL_ROWS][2];
-  __shared__ float part[GL_ROWS][33];
   __shared__ int sdead, xflag;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = blockIdx.x % p.ngroups, j = blockIdx.x / p.ngroups;
   const int r0 = GL_ROWS * g, B = p.B, T = p.T, FO = p.FO, nl = p.nl;
-  unsigned long long* bdg = p.ring;
-  unsigned long long* bsum = bdg + (long)B * SB_KD;
-  unsigned long long* bdyx = bsum + (long)B * 32;
+  const long PB = (long)B * GL_MEM * GE, SBn = (long)B * GL_MEM * 2;
+  unsigned long long* bpart = p.ring;                 // [2][B][16][256]
+  unsigned long long* bsum = bpart + 2 * PB;          // [2][B][16][2]
+  unsigned long long* bdyx = bsum + 2 * SBn;          // [B][256]
   unsigned long long* slots = bdyx + (long)B * 256;
   bool dead = false;
-  for (int i = tid; i < 16 * KP; i += 256) (&A[0][0])[i] = 0.0f;
+  for (int i = tid; i < 16 * DP; i += 256) (&dgs[0][0])[i] = 0.0f;
   {
     const int o = tid >> 4, n = tid & 15, u = 16 * j + n;
     const bool ov = o < FO;
@@ -425,7 +434,7 @@ __global__ __launch_bounds__(256) void ssd_loop_bwd_kernel(SsdBwdArgs p) {
   const int b8 = r0 + m8, bc = min(b8, B - 1);
   const bool ep = tid < GL_ROWS * 16 && b8 < B;
   const int u = 16 * j + n16;
-  const int c16 = lane & 15;
+  const int c16 = lane & 15, q4 = lane >> 4;
   SL_STAMP_ID();
   // pending saved-tensor stores, issued after the next hand-off poll (see the forward)
   float* pa[SB_NP];
@@ -460,12 +469,115 @@ __global__ __launch_bounds__(256) void ssd_loop_bwd_kernel(SsdBwdArgs p) {
     defer(s + 2, d + 2 * GE, d_g);
     defer(s + 3, d + 3 * GE, d_o);
   };
-  float gprev = 0.0f;   // g of the layer whose dX the next D stage forms (own column)
+  // P's operands of layer l, loaded ahead: W_ih rows of the own i, g, o gate columns (lane: k = 4 s +
+  // q4, column 64 wave + 16 q + c16) and the rows' X_l into ys, gamma / beta of LayerNorm l-1
+  float wf[SB_KP / 4][4];
+  float xr[GL_ROWS];
+  float gmv = 0.0f, btv = 0.0f;
+  auto load_p = [&](int l, long rt) {
+    const SsdBwdLayer& Ly = p.L[l];
+#pragma unroll
+    for (int s = 0; s < SB_KP / 4; ++s) {
+      const int k = 4 * s + q4, blk = k >> 4;
+      const float* wr = Ly.w_ih + (long)((blk == 0 ? 0 : blk + 1) * GE + 16 * j + (k & 15)) * GE + 64 * wave + c16;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) wf[s][q] = wr[16 * q];
+    }
+#pragma unroll
+    for (int m = 0; m < GL_ROWS; ++m) xr[m] = Ly.X[(rt + min(r0 + m, B - 1)) * GE + tid];
+    gmv = p.L[l - 1].ln_g[tid];
+    btv = p.L[l - 1].ln_b[tid];
+  };
+  // P of layer l: this member's partial dX_l and partial row sums, published at level `lv`; d_*, gv:
+  // the epilogue threads' own dG / g of layer l
+  auto partial = [&](int lv, float d_i, float d_g, float d_o, float gv) {
+    if (ep) {
+      dgs[m8][n16] = d_i;
+      dgs[m8][16 + n16] = d_g;
+      dgs[m8][32 + n16] = d_o;
+    }
+#pragma unroll
+    for (int m = 0; m < GL_ROWS; ++m) ys[m][tid] = xr[m] - btv;
+    gam_f[tid] = gmv;
+    bet_f[tid] = btv;
+    __syncthreads();
+    gv4 acc[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = gv4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < SB_KP / 4; ++s) {
+      const float av = dgs[c16][4 * s + q4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, wf[s][q], acc[q], 0, 0, 0);
+    }
+    // lane: rows 4 q4 + i (i < 4), column 64 wave + 16 q + c16; rows 8..15 (q4 >= 2) are padding
+    const unsigned tag = (unsigned)(lv + 1);
+    unsigned long long* pb = bpart + (long)(lv & 1) * PB;
+    float s0[4] = {0.f, 0.f, 0.f, 0.f}, s1[4] = {0.f, 0.f, 0.f, 0.f};
+    if (q4 < 2) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int col = 64 * wave + 16 * q + c16;
+        const float gm = gam_f[col];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = 4 * q4 + i;
+          s0[i] = fmaf(acc[q][i], gm, s0[i]);
+          s1[i] = fmaf(acc[q][i], ys[m][col], s1[i]);
+          if (r0 + m < B) put_granule(pb + ((long)(r0 + m) * GL_MEM + j) * GE + col, tag, acc[q][i], local);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      s0[i] = group_sum<16>(s0[i]);
+      s1[i] = group_sum<16>(s1[i]);
+    }
+    if (c16 == 0 && q4 < 2) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        rsum[wave][4 * q4 + i][0] = s0[i];
+        rsum[wave][4 * q4 + i][1] = s1[i];
+      }
+    }
+    // the own columns' g terms (g enters dX_l once, through its owner)
+    float g0 = ep ? gv * gam_f[u] : 0.0f, g1 = ep ? gv * ys[m8][u] : 0.0f;
+    g0 = group_sum<16>(g0);
+    g1 = group_sum<16>(g1);
+    __syncthreads();
+    if (tid < GL_ROWS * 16 && n16 < 2 && b8 < B) {
+      const float t0 = n16 ? g1 : g0;
+      const float v = ((rsum[0][m8][n16] + rsum[1][m8][n16]) + (rsum[2][m8][n16] + rsum[3][m8][n16])) + t0;
+      put_granule(bsum + (long)(lv & 1) * SBn + ((long)b8 * GL_MEM + j) * 2 + n16, tag, v, local);
+    }
+  };
+  // B's gather: the own columns of every member's partial (8 a thread) and every member's sums (1)
+  auto gather_p = [&](int lv) {
+    if (sdead) dead = true;
+    const unsigned tag = (unsigned)(lv + 1);
+    const unsigned long long* pb = bpart + (long)(lv & 1) * PB;
+    const unsigned long long* sb = bsum + (long)(lv & 1) * SBn;
+    const int m = tid >> 5, jm = (tid >> 1) & 15, hf = tid & 1, rr = min(r0 + m, B - 1);
+    int ip[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) ip[c] = (rr * GL_MEM + jm) * GE + 16 * j + 8 * hf + c;
+    float v[8];
+    get_granules_idx<8>(const_cast<unsigned long long*>(pb), ip, tag, v, p.err, dead);
+    int is[1] = {rr * GL_MEM * 2 + (tid & 31)};
+    float vs[1];
+    get_granules_idx<1>(const_cast<unsigned long long*>(sb), is, tag, vs, p.err, dead);
+    const bool ok = r0 + m < B;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) parts[m][jm][8 * hf + c] = ok ? v[c] : 0.0f;
+    sums[m][tid & 31] = ok ? vs[0] : 0.0f;
+    if (dead) sdead = 1;
+  };
+  float gprev = 0.0f;   // g of layer l (own column), for dX_l
   for (int it = 0; it < T && !sdead; ++it) {
     const int t = T - 1 - it;
     const long rt = (long)t * B;
     SB_STAMP(0);
-    // ---- F: the last layer
+    // ---- F: the last layer, then its P
     {
       const SsdBwdLayer& Ly = p.L[nl - 1];
       const long row = rt + bc;
@@ -478,9 +590,10 @@ __global__ __launch_bounds__(256) void ssd_loop_bwd_kernel(SsdBwdArgs p) {
       const bool dyv = tid < GL_ROWS * 16 && n16 < FO && b8 < B;
       const float dyin = dyv ? p.dy[((long)b8 * T + t) * FO + n16] : 0.0f;
       const bool fed = it > 0 && p.mask[t] != 0;
-      if (it > 0) gl_gather<256>(bdyx, r0, B, (unsigned)it, &A[0][0], KP, p.err, dead, &sdead);
+      if (it > 0) gl_gather<256>(bdyx, r0, B, (unsigned)it, &A[0][0], GE + 4, p.err, dead, &sdead);
       __syncthreads();
       flush();
+      load_p(nl - 1, rt);
       SB_STAMP(1);
       if (tid < GL_ROWS * 16) {
         float dyx = 0.0f;
@@ -515,6 +628,7 @@ __global__ __launch_bounds__(256) void ssd_loop_bwd_kernel(SsdBwdArgs p) {
         msum[mz][1] = m1;
       }
       __syncthreads();
+      float d_i = 0.0f, d_g = 0.0f, d_o = 0.0f, gv = 0.0f;
       if (ep) {
         float du = 0.0f;
 #pragma unroll 16
@@ -522,109 +636,61 @@ __global__ __launch_bounds__(256) void ssd_loop_bwd_kernel(SsdBwdArgs p) {
         defer(3, p.du + (rt + b8) * GE + u, du);
         const float xh = (hx - mn) * rs;
         const float gd = du * gam_s[nl - 1][n16];
-        const float gv = rs * (gd - msum[m8][0] / (float)GE - xh * (msum[m8][1] / (float)GE));
+        gv = rs * (gd - msum[m8][0] / (float)GE - xh * (msum[m8][1] / (float)GE));
         defer(4, Ly.g + (rt + b8) * GE + u, gv);
-        float d_i, d_g, d_o;
         cell_bwd(Ly, rt + b8, gv, ig, gg, og, cc, 5, d_i, d_g, d_o);
-        const unsigned tag = (unsigned)(it * nl + 1);
-        unsigned long long* q = bdg + (long)b8 * SB_KD + u;
-        put_granule(q, tag, d_i, local);
-        put_granule(q + GE, tag, d_g, local);
-        put_granule(q + 2 * GE, tag, d_o, local);
-        gprev = gv;
       }
+      gprev = gv;
+      partial(it * nl, d_i, d_g, d_o, gv);
       SB_STAMP(2);
     }
     for (int l = nl - 1; l >= 1; --l) {
       const SsdBwdLayer& Ly = p.L[l];
       const SsdBwdLayer& Lb = p.L[l - 1];
-      const unsigned tag = (unsigned)(it * nl + (nl - 1 - l) + 1);
-      // ---- D: dX_l = dG W_ih + g (own columns), the partial row sums of LayerNorm l-1's backward
-      float gd = 0.0f, xh = 0.0f, rs = 0.0f, ig = 0.0f, gg = 0.0f, og = 0.0f, cc = 0.0f;
-      {
-        GlW<SB_KD> f;
-        const float* wr = Ly.w_t + (long)(16 * j + c16) * 4 * GE;
+      const int lv = it * nl + (nl - 1 - l);
+      // ---- B: dX_l (own columns), LayerNorm l-1 and cell backward; P of layer l-1, or the partial dyx
+      const long row = rt + bc;
+      const float hx = Lb.Hs[row * GE + u] + Lb.X[row * GE + u];
+      const float mn = Lb.mean[row], rs = Lb.rstd[row];
+      const float ig = Lb.G[row * 4 * GE + u], gg = Lb.G[row * 4 * GE + 2 * GE + u];
+      const float og = Lb.G[row * 4 * GE + 3 * GE + u], cc = Lb.C[row * GE + u];
+      gather_p(lv);
+      __syncthreads();
+      flush();
+      if (l - 1 > 0) load_p(l - 1, rt);
+      SB_STAMP(3 + 2 * (nl - 1 - l));
+      float d_i = 0.0f, d_g = 0.0f, d_o = 0.0f, gv = 0.0f;
+      if (ep) {
+        float dx = 0.0f, q0 = 0.0f, q1 = 0.0f;
 #pragma unroll
-        for (int i = 0; i < SB_KD / 64; ++i) {
-          const int kk = wave * (SB_KD / 4) + 16 * i + 4 * (lane >> 4);
-          f.v[i] = *reinterpret_cast<const float4*>(wr + (kk < GE ? kk : kk + GE));
+        for (int jm = 0; jm < GL_MEM; ++jm) {
+          dx += parts[m8][jm][n16];
+          q0 += sums[m8][2 * jm];
+          q1 += sums[m8][2 * jm + 1];
         }
-        const long row = rt + bc;
-        const float hx = Lb.Hs[row * GE + u] + Lb.X[row * GE + u];
-        const float mn = Lb.mean[row];
-        rs = Lb.rstd[row];
-        ig = Lb.G[row * 4 * GE + u]; gg = Lb.G[row * 4 * GE + 2 * GE + u];
-        og = Lb.G[row * 4 * GE + 3 * GE + u]; cc = Lb.C[row * GE + u];
-        gl_gather<SB_KD>(bdg, r0, B, tag, &A[0][0], KP, p.err, dead, &sdead);
-        __syncthreads();
-        flush();
-        SB_STAMP(3 + 4 * (nl - 1 - l));
-        {
-          const gv4 acc = gl_mma<SB_KD>(&A[0][0], KP, f, lane, wave);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) red[wave][4 * (lane >> 4) + i][lane & 15] = acc[i];
-        }
-        __syncthreads();
-        float s0 = 0.0f, s1 = 0.0f;
-        if (tid < GL_ROWS * 16) {
-          const float dx = ((red[0][m8][n16] + red[1][m8][n16]) + (red[2][m8][n16] + red[3][m8][n16])) + gprev;
-          if (ep) defer(0, Ly.dX + (rt + b8) * GE + u, dx);
-          xh = (hx - mn) * rs;
-          gd = ep ? dx * gam_s[l - 1][n16] : 0.0f;
-          s0 = gd;
-          s1 = gd * xh;
-        }
-        s0 = group_sum<16>(s0);
-        s1 = group_sum<16>(s1);
-        if (ep && n16 < 2) put_granule(bsum + (long)b8 * 32 + 2 * j + n16, tag, n16 ? s1 : s0, local);
-        SB_STAMP(4 + 4 * (nl - 1 - l));
+        dx += gprev;
+        defer(0, Ly.dX + (rt + b8) * GE + u, dx);
+        const float xh = (hx - mn) * rs;
+        const float gd = dx * gam_s[l - 1][n16];
+        gv = rs * (gd - q0 / (float)GE - xh * (q1 / (float)GE));
+        defer(1, Lb.g + (rt + b8) * GE + u, gv);
+        cell_bwd(Lb, rt + b8, gv, ig, gg, og, cc, 2, d_i, d_g, d_o);
       }
-      // ---- B: LayerNorm l-1 and cell backward (own columns); publish dG, or the partial dyx
-      {
-        const int row = tid >> 5, e = tid & 31;
-        int idx[1] = {min(r0 + row, B - 1) * 32 + e};
-        float v[1];
-        if (sdead) dead = true;
-        get_granules_idx<1>(bsum, idx, tag, v, p.err, dead);
-        part[row][e] = r0 + row < B ? v[0] : 0.0f;
-        if (dead) sdead = 1;
-        __syncthreads();
-        flush();
-        SB_STAMP(5 + 4 * (nl - 1 - l));
-        float d_i = 0.0f, d_g = 0.0f, d_o = 0.0f, gv = 0.0f;
-        if (ep) {
-          float q0 = 0.0f, q1 = 0.0f;
+      if (l - 1 > 0) {
+        gprev = gv;
+        partial(lv + 1, d_i, d_g, d_o, gv);
+      } else {
+        // partial dyx(t)[b][o] = sum over own units of dG . vt[o] + g . W_ms^T[o] (lane n16: output o = n16)
+        float mine = 0.0f;
 #pragma unroll
-          for (int jm = 0; jm < GL_MEM; ++jm) {
-            q0 += part[m8][2 * jm];
-            q1 += part[m8][2 * jm + 1];
-          }
-          gv = rs * (gd - q0 / (float)GE - xh * (q1 / (float)GE));
-          defer(1, Lb.g + (rt + b8) * GE + u, gv);
-          cell_bwd(Lb, rt + b8, gv, ig, gg, og, cc, 2, d_i, d_g, d_o);
+        for (int o = 0; o < 16; ++o) {
+          float q = fmaf(d_i, vts[0][o][n16], fmaf(d_g, vts[1][o][n16], fmaf(d_o, vts[2][o][n16], gv * wmc[o][n16])));
+          q = group_sum<16>(q);
+          mine = (n16 == o) ? q : mine;
         }
-        if (l - 1 > 0) {
-          if (ep) {
-            const unsigned tg = (unsigned)(it * nl + (nl - l) + 1);
-            unsigned long long* q = bdg + (long)b8 * SB_KD + u;
-            put_granule(q, tg, d_i, local);
-            put_granule(q + GE, tg, d_g, local);
-            put_granule(q + 2 * GE, tg, d_o, local);
-            gprev = gv;
-          }
-        } else {
-          // partial dyx(t)[b][o] = sum over own units of dG . vt[o] + g . W_ms^T[o] (lane n16: output o = n16)
-          float mine = 0.0f;
-#pragma unroll
-          for (int o = 0; o < 16; ++o) {
-            float q = fmaf(d_i, vts[0][o][n16], fmaf(d_g, vts[1][o][n16], fmaf(d_o, vts[2][o][n16], gv * wmc[o][n16])));
-            q = group_sum<16>(q);
-            mine = (n16 == o) ? q : mine;
-          }
-          if (ep) put_granule(bdyx + (long)b8 * 256 + 16 * j + n16, (unsigned)(it + 1), mine, local);
-        }
-        SB_STAMP(6 + 4 * (nl - 1 - l));
+        if (ep) put_granule(bdyx + (long)b8 * 256 + 16 * j + n16, (unsigned)(it + 1), mine, local);
       }
+      SB_STAMP(4 + 2 * (nl - 1 - l));
     }
   }
   flush();
@@ -709,7 +775,7 @@ MRG_API int mrg_ssd_loop_bwd_debug_stamps(void* buf) {
 // Bytes of the granule ring mrg_ssd_loop_bwd needs for B rows (zeroed by the caller before every launch).
 MRG_API long mrg_ssd_loop_bwd_ring_bytes(int B) {
   const int ng = (B + GL_ROWS - 1) / GL_ROWS;
-  return ((long)B * (SB_KD + 32 + 256) + (long)ng * GL_MEM) * 8;
+  return ((long)B * (2 * GL_MEM * (GE + 2) + 256) + (long)ng * GL_MEM) * 8;
 }
 
 MRG_API int mrg_ssd_loop_bwd_fits(int B, int cus) {
@@ -720,9 +786,9 @@ MRG_API int mrg_ssd_loop_bwd_fits(int B, int cus) {
 // The scheduled-sampling decode's backward frame loop (nl >= 2 layers) in one persistent launch
 // (ssd_loop_bwd_kernel; replaces decode.py's per-frame mrg_ssd_ffn_bwd / mrg_ssd_dx /
 // mrg_ssd_ln_cell_bwd sequence with the same outputs).  H = 256, HB = 64, FO <= 16, 2 <= nl <= 4.
-// lptrs (host array, 11 per layer): W_ih^T [H][4H] (null for layer 0), the gamma of the LayerNorm
-// after the layer, the forward's saved X, gates, c, h and that LayerNorm's mean / rstd, then the
-// outputs g = d(h + x) [T][B][H], dG [T][B][4H] and dX [T][B][H] (layers >= 1; null for layer 0).
+// lptrs (host array, 12 per layer): W_ih [4H][H] (null for layer 0), the gamma and beta of the
+// LayerNorm after the layer, the forward's saved X, gates, c, h and that LayerNorm's mean / rstd, then
+// the outputs g = d(h + x) [T][B][H], dG [T][B][4H] and dX [T][B][H] (layers >= 1; null for layer 0).
 // dy [B][T][FO]; mask [T] bytes; w1 [HB][H], w2 [FO][HB], b1, v = [W1 gamma | W1 beta] [HB][2] of the
 // last LayerNorm; z [T][B][HB]; vt = W_ms^T W_ih0 [FO][4H]; wms_t [FO][H]; outputs dyt [T][B][FO],
 // dz [T][B][HB], du [T][B][H]; ring: mrg_ssd_loop_bwd_ring_bytes of zeroed memory; err as the forward's.
@@ -734,24 +800,25 @@ MRG_API int mrg_ssd_loop_bwd(int B, int T, int H, int HB, int FO, int nl, const 
   MRG_REQUIRE(H == GE && HB == GHB && FO >= 1 && FO <= 16 && nl >= 2 && nl <= SL_MAXL,
               "mrg_ssd_loop_bwd: needs H = %d, HB = %d, 1 <= FO <= 16, 2 <= nl <= %d (H=%d HB=%d FO=%d nl=%d)", GE,
               GHB, SL_MAXL, H, HB, FO, nl);
-  MRG_REQUIRE(lptrs && nptrs == SL_PER_LAYER * nl && dy && mask && w1 && w2 && b1 && v && z && vt && wms_t && dyt &&
+  MRG_REQUIRE(lptrs && nptrs == SB_PER_LAYER * nl && dy && mask && w1 && w2 && b1 && v && z && vt && wms_t && dyt &&
                   dz && du && ring && err,
-              "mrg_ssd_loop_bwd: null argument or nptrs %d != %d", nptrs, SL_PER_LAYER * nl);
+              "mrg_ssd_loop_bwd: null argument or nptrs %d != %d", nptrs, SB_PER_LAYER * nl);
   MRG_REQUIRE(mrg_ssd_loop_bwd_fits(B, 0) == 1, "mrg_ssd_loop_bwd: %d workgroups cannot all be resident (B=%d)",
               GL_MEM * ((B + GL_ROWS - 1) / GL_ROWS), B);
   SsdBwdArgs a{};
   for (int i = 0; i < nl; ++i) {
-    const void* const* q = lptrs + SL_PER_LAYER * i;
-    for (int k = 0; k < SL_PER_LAYER; ++k) {
-      const bool optional = i == 0 && (k == 0 || k == 10);
+    const void* const* q = lptrs + SB_PER_LAYER * i;
+    for (int k = 0; k < SB_PER_LAYER; ++k) {
+      const bool optional = i == 0 && (k == 0 || k == 11);
       MRG_REQUIRE(optional || q[k] != nullptr, "mrg_ssd_loop_bwd: null pointer %d of layer %d", k, i);
     }
     SsdBwdLayer& L = a.L[i];
-    L.w_t = static_cast<const float*>(q[0]); L.ln_g = static_cast<const float*>(q[1]);
-    L.X = static_cast<const float*>(q[2]); L.G = static_cast<const float*>(q[3]);
-    L.C = static_cast<const float*>(q[4]); L.Hs = static_cast<const float*>(q[5]);
-    L.mean = static_cast<const float*>(q[6]); L.rstd = static_cast<const float*>(q[7]);
-    L.g = (float*)q[8]; L.dG = (float*)q[9]; L.dX = (float*)q[10];
+    L.w_ih = static_cast<const float*>(q[0]); L.ln_g = static_cast<const float*>(q[1]);
+    L.ln_b = static_cast<const float*>(q[2]);
+    L.X = static_cast<const float*>(q[3]); L.G = static_cast<const float*>(q[4]);
+    L.C = static_cast<const float*>(q[5]); L.Hs = static_cast<const float*>(q[6]);
+    L.mean = static_cast<const float*>(q[7]); L.rstd = static_cast<const float*>(q[8]);
+    L.g = (float*)q[9]; L.dG = (float*)q[10]; L.dX = (float*)q[11];
   }
   a.dy = dy; a.mask = mask; a.w1 = w1; a.w2 = w2; a.b1 = b1; a.v = v; a.z = z; a.vt = vt; a.wms = wms_t;
   a.dyt = dyt; a.dz = dz; a.du = du; a.ring = static_cast<unsigned long long*>(ring); a.err = err;

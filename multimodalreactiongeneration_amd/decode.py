@@ -175,8 +175,8 @@ class _SSDecodeFn(Function):
         if loop:
             lp = []
             for i, lay in enumerate(layers):
-                lp += [w_t[i], lay[4], X[i], G[i], C[i], Hs[i], stats[i][0], stats[i][1], gs[i], dG[i],
-                       dX[i] if i else None]
+                lp += [lay[0] if i else None, lay[4], lay[5], X[i], G[i], C[i], Hs[i], stats[i][0], stats[i][1],
+                       gs[i], dG[i], dX[i] if i else None]
             lpa = (ctypes.c_void_p * len(lp))(*[_ptr(q) for q in lp])
             ring = torch.zeros(max(1, lib.mrg_ssd_loop_bwd_ring_bytes(B) // 8), dtype=torch.int64, device=dev)
             # dX = dG W_ih over the 3 nonzero gate blocks per lower layer, FFN backward, the dyx products

@@ -68,10 +68,8 @@ for i in range(1, nl):
 fn[1 + 2 * nl] = "ffn gather"
 fn[2 + 2 * nl] = "ffn LN / Z / y / select"
 report("forward", fwd, lambda k: fn.get(k, k))
-bn = {1: "F gather dyx", 2: "F dy / dz / du / LN / cell / publish"}
+bn = {1: "F gather dyx", 2: "F dy / dz / du / LN / cell / P publish"}
 for q in range(nl - 1):
-    bn[3 + 4 * q] = f"D{nl - 1 - q} gather dG"
-    bn[4 + 4 * q] = f"D{nl - 1 - q} dX MFMA / row sums / publish"
-    bn[5 + 4 * q] = f"B{nl - 2 - q} gather row sums"
-    bn[6 + 4 * q] = f"B{nl - 2 - q} LN / cell / publish"
+    bn[3 + 2 * q] = f"B{nl - 2 - q} gather partials + sums"
+    bn[4 + 2 * q] = f"B{nl - 2 - q} dX / LN / cell / " + ("P publish" if nl - 2 - q > 0 else "dyx publish")
 report("backward", bwd, lambda k: bn.get(k, k))
