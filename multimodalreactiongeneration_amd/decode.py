@@ -156,8 +156,11 @@ class _SSDecodeFn(Function):
         dG = [torch.empty(T, B, 4 * H, device=dev, dtype=F32) for _ in range(nl)]
         dX = [torch.empty(T, B, H, device=dev, dtype=F32) for _ in range(nl)]  # dX[0] = dfeat
         slab, gslab, zslab = B * H, B * 4 * H, B * HB
+        ext = nl >= 2
+        loop = (ext and _LOOP_BWD[0] and H == 256 and HB == 64 and FO <= 16 and nl <= 4
+                and lib.mrg_ssd_loop_bwd_fits(B, 0) == 1)
         # W_ih^T copies: the per-frame dX = dG W_ih reads both operands k-contiguous (float4)
-        w_t = [None if (nl >= 2 and i == 0) else lay[0].t().contiguous() for i, lay in enumerate(layers)]
+        w_t = [None if (loop or (ext and i == 0)) else lay[0].t().contiguous() for i, lay in enumerate(layers)]
         # v = [W1 gamma | W1 beta] [HB, 2] of the last LayerNorm: its row sums through W1 (decode.hip)
         lw, lb = layers[-1][4], layers[-1][5]
         gb = torch.stack([lw.detach(), lb.detach()])
@@ -165,13 +168,10 @@ class _SSDecodeFn(Function):
         gemm(HB, 2, H, _ptr(w1), 0, H, _ptr(gb), 1, H, _ptr(v), 2, device=dev)
         # the bottom layer forms each frame's y gradient through the select itself (dyx = dfeat W_ms
         # with vt = W_ms^T W_ih0), so its dX (dfeat) is one GEMM over all frames after the loop
-        ext = nl >= 2
         if ext:
             vt = torch.empty(FM, 4 * H, device=dev, dtype=F32)
             gemm(FM, 4 * H, H, _ptr(wms_t), 0, H, _ptr(layers[0][0]), 1, H, _ptr(vt), 4 * H, device=dev)
-            dyx = torch.empty(T, B, FM, device=dev, dtype=F32)
-        loop = (ext and _LOOP_BWD[0] and H == 256 and HB == 64 and FO <= 16 and nl <= 4
-                and lib.mrg_ssd_loop_bwd_fits(B, 0) == 1)
+            dyx = None if loop else torch.empty(T, B, FM, device=dev, dtype=F32)
         if loop:
             lp = []
             for i, lay in enumerate(layers):
