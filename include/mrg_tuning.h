@@ -46,8 +46,9 @@ int mrg_debug_busy(int blocks, int threads, int lds, double usec, hipStream_t st
 /* Diagnostics: a 1-thread kernel writing the 100 MHz wall clock into ((uint64*)buf)[slot] in `stream`'s
  * order (tools/side_timing.py: when a replayed graph reaches a point). */
 int mrg_debug_stamp(void* buf, int slot, hipStream_t stream);
-/* Diagnostics: block 0's per-stage shader-clock stamps of later mrg_gen_loop launches ([T][32] u64;
- * slot 31 of frame 0: the group's local hand-off flag); null turns them off (tools/gen_stamps.py). */
+/* Diagnostics: per-stage 100 MHz real-time stamps of row group 0's 16 members in later mrg_gen_loop
+ * launches ([T][16 members][32] u64; slot 31 of frame 0: the local hand-off flag); null turns them off
+ * (tools/gen_stamps.py). */
 int mrg_gen_loop_debug_stamps(void* buf);
 /* Diagnostics: per-stage 100 MHz real-time stamps (s_memrealtime, one clock for all CUs) of the 16
  * members of row group 0 in later mrg_ssd_loop_fwd launches ([T][16 members][16] u64: frame start, then

@@ -382,11 +382,19 @@ struct GenLoopArgs {
   int* err;
   int B, T, fm, nb, ngroups;
   float eps;
-  unsigned long long* stamps;         // diagnostics (mrg_gen_loop_debug_stamps): [T][32] of block 0, or null
+  unsigned long long* stamps;         // diagnostics (mrg_gen_loop_debug_stamps): [T][16][32] of group 0, or null
 };
 
-// block 0 / thread 0: shader-clock stamp `slot` of frame t (slot 31: the group's local-hand-off flag)
-#define GL_STAMP(slot)                                                                     do {                                                                                       if (p.stamps && blockIdx.x == 0 && threadIdx.x == 0) {                                     unsigned long long _t;                                                                   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");             p.stamps[(long)t * 32 + (slot)] = _t;                                                  }                                                                                      } while (0)
+// thread 0 of each member of row group 0: 100 MHz real-time stamp (s_memrealtime, one clock for every
+// CU) `slot` of frame t into stamps[t][member][slot] (slot 31 of frame 0: the local-hand-off flag)
+#define GL_STAMP(slot)                                                                   \
+  do {                                                                                   \
+    if (p.stamps && g == 0 && threadIdx.x == 0) {                                        \
+      unsigned long long _t;                                                             \
+      asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");     \
+      p.stamps[((long)t * GL_MEM + j) * 32 + (slot)] = _t;                               \
+    }                                                                                    \
+  } while (0)
 
 enum { GL_WIH, GL_BIH, GL_BHH, GL_L1G, GL_L1B, GL_MW, GL_MB, GL_L2G, GL_L2B,
        GL_I0, GL_I1 = GL_I0 + 6, GL_CW = GL_I1 + 6, GL_CB, GL_FW1, GL_FB1, GL_FW2, GL_FB2, GL_FLG, GL_FLB,
@@ -431,7 +439,7 @@ __global__ __launch_bounds__(256) void gen_loop_kernel(GenLoopArgs p) {
   const int m8 = tid >> 4, n16 = tid & 15;   // epilogue thread -> (row, column of the tile), rows < 8 used
   const bool ep = tid < GL_ROWS * 16 && r0 + m8 < B;
   const int nl = lane & 15;                  // this lane's tile column (weight row) in the products
-  if (p.stamps && blockIdx.x == 0 && threadIdx.x == 0) p.stamps[31] = (unsigned long long)local;
+  if (p.stamps && g == 0 && threadIdx.x == 0) p.stamps[(long)j * 32 + 31] = (unsigned long long)local;
   for (int t = 0; t < T && !sdead; ++t) {
     GL_STAMP(0);
     for (int k = 0; k < p.nb; ++k) {
@@ -713,8 +721,9 @@ MRG_API int mrg_gen_ffn(int B, int N, const float* a, const float* r, const floa
 }
 
 static unsigned long long* g_gen_stamps = nullptr;
-// Diagnostics (tools/gen_stamps.py): later mrg_gen_loop launches write block 0's per-stage shader-clock
-// stamps into buf ([T][32] u64; slot 31 of frame 0: the group's local hand-off flag); null = off.
+// Diagnostics (tools/gen_stamps.py): later mrg_gen_loop launches write row group 0's members' per-stage
+// real-time (10 ns) stamps into buf ([T][16 members][32] u64; slot 31 of frame 0: the local hand-off
+// flag); null = off.
 MRG_API int mrg_gen_loop_debug_stamps(void* buf) {
   g_gen_stamps = static_cast<unsigned long long*>(buf);
   return 0;

@@ -62,7 +62,7 @@ def run(names):
         import multimodalreactiongeneration_amd.encoder_stack as ES
         import multimodalreactiongeneration_amd.integrate as IG
         side_saved = (Fn._on_side, ES._on_side, IG._on_side)
-        Fn._on_side = ES._on_side = IG._on_side = lambda device, rows, keep, fn: None
+        Fn._on_side = ES._on_side = IG._on_side = lambda device, rows, keep, fn, writes=None: None
     try:
         dev = torch.device("cuda", 0)
         mc, oc, me = C.lstmformer_config(ratio=1)
