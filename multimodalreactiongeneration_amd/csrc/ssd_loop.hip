@@ -144,11 +144,11 @@ __global__ __launch_bounds__(256) void ssd_loop_kernel(SsdLoopArgs p) {
       gs[0] = pg[0]; gs[GE] = pg[1]; gs[2 * GE] = pg[2]; gs[3 * GE] = pg[3];
       L.C[row * GE + u] = pc;
       L.Hs[row * GE + u] = ph;
-      L.X[row * GE + u] = px;
-      if (pl == 0 && j == 0 && n16 < FO) p.xf_ms[row * p.F + n16] = pms;
+      if (L.X) L.X[row * GE + u] = px;
+      if (pl == 0 && j == 0 && n16 < FO && p.xf_ms) p.xf_ms[row * p.F + n16] = pms;
     }
     pl = -1;
-    if (pst >= 0 && j == 0 && lane == 0) {
+    if (pst >= 0 && j == 0 && lane == 0 && p.L[pst].mean) {
 #pragma unroll
       for (int rr = 0; rr < 2; ++rr) {
         const int m = wave + 4 * rr;
@@ -161,13 +161,15 @@ __global__ __launch_bounds__(256) void ssd_loop_kernel(SsdLoopArgs p) {
     pst = -1;
     if (pft >= 0) {
       const long rt = (long)pft * B;
-      if (ep) p.U[(rt + b8) * GE + u] = pu;
-      if (j == 0) {
+      if (ep && p.U) p.U[(rt + b8) * GE + u] = pu;
+      if (j == 0 && p.Z) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int m = 4 * (lane >> 4) + i;
           if (m < GL_ROWS && r0 + m < B) p.Z[(rt + r0 + m) * GHB + 16 * wave + c16] = pz[i];
         }
+      }
+      if (j == 0 && p.y) {
         if (ep && n16 < FO) p.y[((long)b8 * T + pft) * FO + n16] = py;
       }
     }
@@ -730,6 +732,9 @@ MRG_API int mrg_ssd_loop_fits(int B, int cus) {
 // [T][B].  P [T][B][H]; wms = W_ms^T [FO][H]; FFN w1 [HB][H], b1, w2 [FO][HB], b2; ms, mask as in
 // mrg_ssd_feat_gate_cell_fwd; xf_ms: X_f's ms columns (row stride F); U [T][B][H], Z [T][B][HB],
 // y [B][T][FO]; ring: mrg_ssd_loop_ring_bytes of zeroed memory; err: the recurrences' error flag.
+// Outputs that can be formed after the loop may be null and are then not stored (a store ahead of a
+// hand-off poll delays it; the row-wide ones fell on one member): X of layers > 0, the LayerNorm
+// statistics (both of a layer), U, Z, y and xf_ms (decode.py forms them from h, X_0 and P).
 MRG_API int mrg_ssd_loop_fwd(int B, int T, int H, int HB, int FO, int F, int nl, float eps, const void* const* lptrs,
                              int nptrs, const float* P, const float* wms, const float* w1, const float* b1,
                              const float* w2, const float* b2, const float* ms, long ms_bs, long ms_ts,
@@ -739,15 +744,17 @@ MRG_API int mrg_ssd_loop_fwd(int B, int T, int H, int HB, int FO, int F, int nl,
   MRG_REQUIRE(H == GE && HB == GHB && FO >= 1 && FO <= 16 && nl >= 1 && nl <= SL_MAXL && F >= FO,
               "mrg_ssd_loop_fwd: needs H = %d, HB = %d, 1 <= FO <= 16, 1 <= nl <= %d (H=%d HB=%d FO=%d nl=%d)", GE,
               GHB, SL_MAXL, H, HB, FO, nl);
-  MRG_REQUIRE(lptrs && nptrs == SL_PER_LAYER * nl && P && wms && w1 && b1 && w2 && b2 && ms && mask && xf_ms && U &&
-                  Z && y && ring && err,
+  MRG_REQUIRE(lptrs && nptrs == SL_PER_LAYER * nl && P && wms && w1 && b1 && w2 && b2 && ms && mask && ring && err,
               "mrg_ssd_loop_fwd: null argument or nptrs %d != %d", nptrs, SL_PER_LAYER * nl);
   MRG_REQUIRE(mrg_ssd_loop_fits(B, 0) == 1, "mrg_ssd_loop_fwd: %d workgroups cannot all be resident (B=%d)",
               GL_MEM * ((B + GL_ROWS - 1) / GL_ROWS), B);
   SsdLoopArgs a{};
   for (int i = 0; i < nl; ++i) {
     const void* const* q = lptrs + SL_PER_LAYER * i;
-    for (int k = 0; k < SL_PER_LAYER; ++k) MRG_REQUIRE(q[k] != nullptr, "mrg_ssd_loop_fwd: null pointer %d of layer %d", k, i);
+    for (int k = 0; k < SL_PER_LAYER; ++k)   // X (i > 0), mean and rstd may be null: not stored
+      MRG_REQUIRE(q[k] != nullptr || (k == 5 && i > 0) || k == 9 || k == 10, "mrg_ssd_loop_fwd: null pointer %d of layer %d",
+                  k, i);
+    MRG_REQUIRE((q[9] == nullptr) == (q[10] == nullptr), "mrg_ssd_loop_fwd: mean and rstd of layer %d: both or neither", i);
     SsdLoopLayer& L = a.L[i];
     L.w_ih = static_cast<const float*>(q[0]); L.b_ih = static_cast<const float*>(q[1]);
     L.b_hh = static_cast<const float*>(q[2]); L.ln_g = static_cast<const float*>(q[3]);

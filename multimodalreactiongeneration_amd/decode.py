@@ -87,9 +87,12 @@ class _SSDecodeFn(Function):
         slab, gslab, zslab = B * H, B * 4 * H, B * HB
         lw, lb = layers[-1][4], layers[-1][5]
         if _LOOP[0] and H == 256 and HB == 64 and FO <= 16 and nl <= 4 and lib.mrg_ssd_loop_fits(B, 0) == 1:
+            # the loop stores the gates, c, h and X_0; the LayerNorm outputs (X_i, U) and statistics,
+            # Z, y and X_f's ms columns are formed after it (below): a store ahead of a hand-off poll
+            # delays that poll, and the row-wide ones fell on one member (ssd_loop.hip)
             lp = []
             for i, (w_ih, _w_hh, b_ih, b_hh, g_, b_) in enumerate(layers):
-                lp += [w_ih, b_ih, b_hh, g_, b_, X[i], G[i], C[i], Hs[i], stats[i][0], stats[i][1]]
+                lp += [w_ih, b_ih, b_hh, g_, b_, X[i] if i == 0 else None, G[i], C[i], Hs[i], None, None]
             lpa = (ctypes.c_void_p * len(lp))(*[_ptr(q) for q in lp])
             ring = torch.zeros(max(1, lib.mrg_ssd_loop_ring_bytes(B, nl) // 8), dtype=torch.int64, device=dev)
             # algorithmic FLOPs (bench's "ssd" family): gates 8H^2 per row and layer, FFN, the ms columns
@@ -97,8 +100,24 @@ class _SSDecodeFn(Function):
             with _probe("ssd", flop):
                 _lib.check(lib.mrg_ssd_loop_fwd(
                     B, T, H, HB, FO, F, nl, eps, lpa, len(lp), _ptr(P), _ptr(wms_t), _ptr(w1), _ptr(b1), _ptr(w2),
-                    _ptr(b2), _ptr(msc), msc.stride(0), msc.stride(1), _ptr(mask), _ptr(xf, SA + FMp), _ptr(U),
-                    _ptr(Z), _ptr(y), _ptr(ring), _ptr(_err_flag(dev)), _stream()), "ssd loop fwd")
+                    _ptr(b2), _ptr(msc), msc.stride(0), msc.stride(1), _ptr(mask), None, None, None, None,
+                    _ptr(ring), _ptr(_err_flag(dev)), _stream()), "ssd loop fwd")
+            rows = T * B
+            for i, (_w_ih, _w_hh, _b_ih, _b_hh, g_, b_) in enumerate(layers):
+                # X_{i+1} (U after the last layer) = LN(h_i + X_i) with its statistics
+                out = X[i + 1] if i + 1 < nl else U
+                _lib.check(lib.mrg_residual_layernorm_fwd(rows, H, _ptr(Hs[i]), _ptr(X[i]), _ptr(g_), _ptr(b_), eps,
+                                                          _ptr(out), _ptr(stats[i][0]), _ptr(stats[i][1]),
+                                                          _stream()), "ssd layernorm")
+            gemm(rows, HB, H, _ptr(U), 0, H, _ptr(w1), 1, H, _ptr(Z), HB, bias=_ptr(b1), epi=1, device=dev)
+            y_tb = torch.empty(T, B, FO, device=dev, dtype=F32)
+            gemm(rows, FO, HB, _ptr(Z), 0, HB, _ptr(w2), 1, HB, _ptr(y_tb), FO, bias=_ptr(b2), device=dev)
+            y.copy_(y_tb.transpose(0, 1))
+            # X_f's ms columns: ms_in(0) = ms[:, 0], ms_in(t + 1) = mask[t] ? y(t) : ms[:, t]
+            xms = xf[:, :, SA + FMp:]
+            xms[0].copy_(msc[:, 0])
+            if T > 1:
+                xms[1:].copy_(torch.where(mask[:-1].bool()[:, None, None], y_tb[:-1], msc[:, :-1].transpose(0, 1)))
             T_launch = 0
         else:
             T_launch = T
