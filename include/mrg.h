@@ -254,20 +254,19 @@ int mrg_ssd_y_fwd(int B, int HB, int FO, const float* z, const float* w2, const 
 /* The forward frame loop above (every frame's gate / cell / FFN kernels) in ONE persistent launch
  * (ssd_loop.hip ssd_loop_kernel; decode.py uses it when H = 256, HB = 64, FO <= 16, nl <= 4 and the
  * grid fits): groups of 8 batch rows x 16 workgroups, each layer's h handed to the group's members
- * as {tag, value} granules.  lptrs: 11 device pointers per layer (w_ih, b_ih, b_hh, the LayerNorm
- * after the layer gamma / beta, then its saved X [T][B][H], gates [T][B][4H], c, h [T][B][H] and that
- * LayerNorm's mean / rstd [T][B]); P [T][B][H] = the sampler / partner projection + b_f; wms_t;
- * w1 / b1 / w2 / b2; ms, mask as above; xf_ms the ms columns of X_f [T][B][F]; U [T][B][H], Z
- * [T][B][HB], y [B][T][FO].  ring: mrg_ssd_loop_ring_bytes(B, nl) of zeroed device memory per
- * launch; err: set when a hand-off poll times out.  Replaces the per-frame launches of
- * lstm_with_sample.py:379-433's loop (same outputs up to fp32 reassociation).                   */
+ * as {tag, value} granules.  lptrs: 9 device pointers per layer (w_ih, b_ih, b_hh, the LayerNorm
+ * after the layer gamma / beta, then the saved X [T][B][H] (layer 0's; null for the others), gates
+ * [T][B][4H], c and h [T][B][H]); P [T][B][H] = the sampler / partner projection + b_f; wms_t;
+ * w1 / b1 / w2 / b2; ms, mask as above.  The LayerNorm outputs / statistics, z, y and the sampled
+ * self-motion inputs are not written (they follow from h, X_0 and ms: decode.py forms them after the
+ * launch).  ring: mrg_ssd_loop_ring_bytes(B, nl) of zeroed device memory per launch; err: set when a
+ * hand-off poll times out.  Replaces the per-frame launches of lstm_with_sample.py:379-433's loop.   */
 long mrg_ssd_loop_ring_bytes(int B, int nl);
 int mrg_ssd_loop_fits(int B, int cus);
-int mrg_ssd_loop_fwd(int B, int T, int H, int HB, int FO, int F, int nl, float eps, const void* const* lptrs,
+int mrg_ssd_loop_fwd(int B, int T, int H, int HB, int FO, int nl, float eps, const void* const* lptrs,
                      int nptrs, const float* P, const float* wms_t, const float* w1, const float* b1,
                      const float* w2, const float* b2, const float* ms, long ms_bs, long ms_ts,
-                     const unsigned char* mask, float* xf_ms, float* U, float* Z, float* y, void* ring, int* err,
-                     hipStream_t stream);
+                     const unsigned char* mask, void* ring, int* err, hipStream_t stream);
 /* The backward frame loop (mrg_ssd_ffn_bwd / mrg_ssd_dx / mrg_ssd_ln_cell_bwd of every frame, nl >= 2)
  * in ONE persistent launch (ssd_loop.hip ssd_loop_bwd_kernel; decode.py uses it under the same
  * conditions as the forward loop): per frame the last layer's FFN / LayerNorm / cell backward needs no

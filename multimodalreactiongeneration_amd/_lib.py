@@ -160,8 +160,8 @@ SIGNATURES = {
     "mrg_gen_loop": (c_int, [c_int, c_int, c_int, c_int, c_float, PP, c_int, P, P, P, P, P, P]),
     "mrg_ssd_loop_ring_bytes": (c_long, [c_int, c_int]),
     "mrg_ssd_loop_fits": (c_int, [c_int, c_int]),
-    "mrg_ssd_loop_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, PP, c_int, P, P, P, P, P, P,
-                                 P, c_long, c_long, P, P, P, P, P, P, P, P]),
+    "mrg_ssd_loop_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_float, PP, c_int, P, P, P, P, P, P,
+                                 P, c_long, c_long, P, P, P, P]),
     "mrg_ssd_loop_bwd_ring_bytes": (c_long, [c_int]),
     "mrg_ssd_loop_bwd_fits": (c_int, [c_int, c_int]),
     "mrg_ssd_loop_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, PP, c_int, P, P, P, P, P, P, P, P, P, P, P, P,

@@ -13,22 +13,23 @@
 //   F   gather h_{L-1} -> U = LN(h_{L-1} + X_{L-1}) -> Z = relu(U W1^T + b1) (all 64 hidden columns,
 //       per member) -> y = Z W2^T + b2 -> ms_in(t + 1) = mask[t] ? y : ms[t]  (no exchange: every
 //       member holds its rows' next input)
-// so a frame is L hand-offs instead of L + 1 kernel boundaries.  Every tensor the backward reads
-// (decode.py: X_f's ms columns, X_i, post-activation gates, c, h, the LayerNorm statistics, U, Z, y)
-// is written with the per-frame kernels' layout; member j writes its 16 columns, member 0 the
-// row-wide values.  Hand-off buffers alternate by frame parity: a slot is rewritten two frames
-// later, after every reader of it has passed the next frame's last gather.
+// so a frame is L hand-offs instead of L + 1 kernel boundaries.  The loop stores the post-activation
+// gates, c and h of every layer and X_0 (member j its 16 units, the per-frame kernels' layout);
+// everything else the backward reads is formed from those after the loop by decode.py (the
+// LayerNorms X_i / U with their statistics, Z, y, X_f's ms columns: two LayerNorm launches, two
+// products).  Storing the row-wide values inside the loop fell on one member, whose extra code held it
+// ~1.2 us behind its group at every stage.  Hand-off buffers alternate by frame parity: a slot is
+// rewritten two frames later, after every reader of it has passed the next frame's last gather.
 #include "gen_loop.h"
 
 namespace mrg {
 
 static constexpr int SL_MAXL = 4;        // layered LSTM depth
-static constexpr int SL_PER_LAYER = 11;  // see mrg_ssd_loop_fwd
+static constexpr int SL_PER_LAYER = 9;   // see mrg_ssd_loop_fwd
 
 struct SsdLoopLayer {
   const float *w_ih, *b_ih, *b_hh, *ln_g, *ln_b;   // ln: the LayerNorm after this layer
-  float *X, *G, *C, *Hs;                          // [T][B][H], [T][B][4H], [T][B][H], [T][B][H]
-  float *mean, *rstd;                             // that LayerNorm's statistics [T][B]
+  float *X, *G, *C, *Hs;                          // [T][B][H] (layer 0 only), [T][B][4H], [T][B][H], [T][B][H]
 };
 struct SsdLoopArgs {
   SsdLoopLayer L[SL_MAXL];
@@ -38,11 +39,9 @@ struct SsdLoopArgs {
   const float* ms;                // ms[b * ms_bs + t * ms_ts + o]
   long ms_bs, ms_ts;
   const unsigned char* mask;      // [T]
-  float* xf_ms;                   // ms_in(t) -> xf_ms[(t * B + b) * F + o]
-  float *U, *Z, *y;               // [T][B][H], [T][B][HB], [B][T][FO]
   unsigned long long* ring;       // 2 x L x [B][H] granules, then the XCC slots
   int* err;
-  int B, T, FO, F, nl, ngroups;
+  int B, T, FO, nl, ngroups;
   float eps;
   unsigned long long* stamps;     // diagnostics (mrg_ssd_loop_debug_stamps): [T][16] of block 0, or null
 };
@@ -67,19 +66,6 @@ struct SsdLoopArgs {
       p.stamps[(long)j * 16 + 14] = (unsigned long long)_id;                             \
     }                                                                                    \
   } while (0)
-
-// LN(a + r) of one 256-wide row (4 values per lane) into out (and out2); the statistics returned
-__device__ __forceinline__ void sl_ln_row(const float* a, const float* r, const GlLn& p, float eps, float* out,
-                                          float* out2, int lane, float& mean, float& rs) {
-  const float4 v = gen_add4(*reinterpret_cast<const float4*>(a + 4 * lane), *reinterpret_cast<const float4*>(r + 4 * lane));
-  mean = gen_wave_sum((v.x + v.y) + (v.z + v.w)) * (1.0f / GE);
-  const float dx = v.x - mean, dy = v.y - mean, dz = v.z - mean, dw = v.w - mean;
-  rs = rsqrtf(gen_wave_sum((dx * dx + dy * dy) + (dz * dz + dw * dw)) * (1.0f / GE) + eps);
-  const float4 o = make_float4(fmaf(dx * rs, p.g.x, p.b.x), fmaf(dy * rs, p.g.y, p.b.y), fmaf(dz * rs, p.g.z, p.b.z),
-                               fmaf(dw * rs, p.g.w, p.b.w));
-  *reinterpret_cast<float4*>(out + 4 * lane) = o;
-  if (out2) *reinterpret_cast<float4*>(out2 + 4 * lane) = o;
-}
 
 __global__ __launch_bounds__(256) void ssd_loop_kernel(SsdLoopArgs p) {
   constexpr int AP = GE + 4, HP = GHB + 4;
@@ -126,16 +112,12 @@ __global__ __launch_bounds__(256) void ssd_loop_kernel(SsdLoopArgs p) {
   const int c16 = lane & 15;                 // this lane's tile column (weight row) in the products
   const int u = 16 * j + n16;                // the epilogue thread's hidden unit
   SL_STAMP_ID();
-  // Saved-tensor stores are deferred to just after the NEXT hand-off poll: on gfx9 a store holds a
-  // vmcnt slot until the memory acknowledges it, and the counter retires in order, so stores issued
-  // before a poll would sit in front of the poll's loads.  Pending: one layer's gate / cell / input
-  // values (epilogue threads), one LayerNorm's statistics (member 0, lane 0 of each wave: rows wave
-  // and wave + 4) and the FFN stage's U / Z / y.
-  int pl = -1, pst = -1, pft = -1;     // pending layer, statistics layer, FFN frame (-1: none)
-  long prt = 0, pstrt = 0;             // their frames' first rows
-  float pg[4] = {0.f, 0.f, 0.f, 0.f}, pc = 0.f, ph = 0.f, px = 0.f, pms = 0.f;
-  float pmean[2] = {0.f, 0.f}, prs[2] = {0.f, 0.f};
-  float pu = 0.f, py = 0.f, pz[4] = {0.f, 0.f, 0.f, 0.f};
+  // The stores of a layer's gates, c and h (and X_0) are deferred to just after the NEXT hand-off poll:
+  // on gfx9 a store holds a vmcnt slot until the memory acknowledges it, and the counter retires in
+  // order, so stores issued before a poll would sit in front of the poll's loads.
+  int pl = -1;                         // pending layer (-1: none)
+  long prt = 0;                        // its frame's first row
+  float pg[4] = {0.f, 0.f, 0.f, 0.f}, pc = 0.f, ph = 0.f, px = 0.f;
   auto flush = [&]() {
     if (pl >= 0 && ep) {
       const SsdLoopLayer& L = p.L[pl];
@@ -144,36 +126,9 @@ __global__ __launch_bounds__(256) void ssd_loop_kernel(SsdLoopArgs p) {
       gs[0] = pg[0]; gs[GE] = pg[1]; gs[2 * GE] = pg[2]; gs[3 * GE] = pg[3];
       L.C[row * GE + u] = pc;
       L.Hs[row * GE + u] = ph;
-      if (L.X) L.X[row * GE + u] = px;
-      if (pl == 0 && j == 0 && n16 < FO && p.xf_ms) p.xf_ms[row * p.F + n16] = pms;
+      if (pl == 0) L.X[row * GE + u] = px;
     }
     pl = -1;
-    if (pst >= 0 && j == 0 && lane == 0 && p.L[pst].mean) {
-#pragma unroll
-      for (int rr = 0; rr < 2; ++rr) {
-        const int m = wave + 4 * rr;
-        if (r0 + m < B) {
-          p.L[pst].mean[pstrt + r0 + m] = pmean[rr];
-          p.L[pst].rstd[pstrt + r0 + m] = prs[rr];
-        }
-      }
-    }
-    pst = -1;
-    if (pft >= 0) {
-      const long rt = (long)pft * B;
-      if (ep && p.U) p.U[(rt + b8) * GE + u] = pu;
-      if (j == 0 && p.Z) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int m = 4 * (lane >> 4) + i;
-          if (m < GL_ROWS && r0 + m < B) p.Z[(rt + r0 + m) * GHB + 16 * wave + c16] = pz[i];
-        }
-      }
-      if (j == 0 && p.y) {
-        if (ep && n16 < FO) p.y[((long)b8 * T + pft) * FO + n16] = py;
-      }
-    }
-    pft = -1;
   };
   // the gate tiles of layer i from A (4 tiles q: units 16 j + 4 q + (n & 3), gate n >> 2), the
   // zero-state cell, h published; the values saved for the backward become the pending set
@@ -239,7 +194,6 @@ __global__ __launch_bounds__(256) void ssd_loop_kernel(SsdLoopArgs p) {
         A[m][tid] = v;
       }
       SL_STAMP(1);
-      if (tid < GL_ROWS * 16) pms = msin[m8][n16];
       // the weight fragments after the build (a barrier keeps the compiler from hoisting them: held
       // through it they leave too few registers and the build's LDS reads serialise)
       __syncthreads();
@@ -265,10 +219,8 @@ __global__ __launch_bounds__(256) void ssd_loop_kernel(SsdLoopArgs p) {
 #pragma unroll
       for (int rr = 0; rr < 2; ++rr) {
         const int m = wave + 4 * rr;
-        sl_ln_row(A[m], Xs[m], ln, eps, Xs[m], A[m], lane, pmean[rr], prs[rr]);
+        gl_ln_row(A[m], Xs[m], ln, eps, Xs[m], A[m], lane);
       }
-      pst = i - 1;
-      pstrt = row_t;
       gates(i, f, hb + (long)i * BH, tag, row_t);
       SL_STAMP(2 + 2 * i);
     }
@@ -298,18 +250,14 @@ __global__ __launch_bounds__(256) void ssd_loop_kernel(SsdLoopArgs p) {
 #pragma unroll
       for (int rr = 0; rr < 2; ++rr) {
         const int m = wave + 4 * rr;
-        sl_ln_row(A[m], Xs[m], ln, eps, A[m], nullptr, lane, pmean[rr], prs[rr]);
+        gl_ln_row(A[m], Xs[m], ln, eps, A[m], nullptr, lane);
       }
-      pst = nl - 1;
-      pstrt = row_t;
       __syncthreads();
-      if (tid < GL_ROWS * 16) pu = A[m8][u];
       {
         const gv4 acc = gl_mma<4 * GE>(&A[0][0], AP, f1, lane, 0);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          pz[i] = fmaxf(acc[i] + b1, 0.0f);
-          hs[4 * (lane >> 4) + i][hc] = pz[i];
+          hs[4 * (lane >> 4) + i][hc] = fmaxf(acc[i] + b1, 0.0f);
         }
       }
       __syncthreads();
@@ -318,13 +266,11 @@ __global__ __launch_bounds__(256) void ssd_loop_kernel(SsdLoopArgs p) {
       if (tid < GL_ROWS * 16) {
         float nxt = 0.0f;
         if (yv_ok) {
-          py = gl_sum(red, 0, m8, n16) + b2;
-          nxt = sel ? py : msv;
+          nxt = sel ? gl_sum(red, 0, m8, n16) + b2 : msv;
         }
         msin[m8][n16] = nxt;
       }
       if (nl == 1 && t + 1 < T) park_p();
-      pft = t;
       if (dead) sdead = 1;
       __syncthreads();
       SL_STAMP(2 + 2 * nl);
@@ -726,22 +672,19 @@ MRG_API int mrg_ssd_loop_fits(int B, int cus) {
 
 // The scheduled-sampling decode's forward frame loop in one persistent launch (ssd_loop_kernel;
 // replaces the per-frame mrg_ssd_feat_gate_cell_fwd / mrg_ssd_gate_cell_fwd / mrg_ssd_ffn_z_fwd /
-// mrg_ssd_y_fwd sequence of decode.py with the same outputs).  H = 256, HB = 64, FO <= 16, nl <= 4.
-// lptrs (host array, 11 per layer): w_ih [4H][H], b_ih, b_hh, the LayerNorm after the layer (gamma,
-// beta), then the saved X [T][B][H], gates [T][B][4H], c, h [T][B][H] and that LayerNorm's mean / rstd
-// [T][B].  P [T][B][H]; wms = W_ms^T [FO][H]; FFN w1 [HB][H], b1, w2 [FO][HB], b2; ms, mask as in
-// mrg_ssd_feat_gate_cell_fwd; xf_ms: X_f's ms columns (row stride F); U [T][B][H], Z [T][B][HB],
-// y [B][T][FO]; ring: mrg_ssd_loop_ring_bytes of zeroed memory; err: the recurrences' error flag.
-// Outputs that can be formed after the loop may be null and are then not stored (a store ahead of a
-// hand-off poll delays it; the row-wide ones fell on one member): X of layers > 0, the LayerNorm
-// statistics (both of a layer), U, Z, y and xf_ms (decode.py forms them from h, X_0 and P).
-MRG_API int mrg_ssd_loop_fwd(int B, int T, int H, int HB, int FO, int F, int nl, float eps, const void* const* lptrs,
+// mrg_ssd_y_fwd sequence of decode.py).  H = 256, HB = 64, FO <= 16, nl <= 4.  lptrs (host array, 9 per
+// layer): w_ih [4H][H], b_ih, b_hh, the LayerNorm after the layer (gamma, beta), then the saved X
+// [T][B][H] (layer 0's; ignored, may be null, for the others), gates [T][B][4H], c and h [T][B][H].
+// P [T][B][H]; wms = W_ms^T [FO][H]; FFN w1 [HB][H], b1, w2 [FO][HB], b2; ms, mask as in
+// mrg_ssd_feat_gate_cell_fwd; ring: mrg_ssd_loop_ring_bytes of zeroed memory; err: the recurrences'
+// error flag.  The LayerNorm outputs and statistics, Z, y and the sampled self-motion inputs are not
+// written: they follow from h, X_0 and ms after the loop (decode.py).
+MRG_API int mrg_ssd_loop_fwd(int B, int T, int H, int HB, int FO, int nl, float eps, const void* const* lptrs,
                              int nptrs, const float* P, const float* wms, const float* w1, const float* b1,
                              const float* w2, const float* b2, const float* ms, long ms_bs, long ms_ts,
-                             const unsigned char* mask, float* xf_ms, float* U, float* Z, float* y, void* ring,
-                             int* err, hipStream_t stream) {
+                             const unsigned char* mask, void* ring, int* err, hipStream_t stream) {
   if (B == 0 || T == 0) return 0;
-  MRG_REQUIRE(H == GE && HB == GHB && FO >= 1 && FO <= 16 && nl >= 1 && nl <= SL_MAXL && F >= FO,
+  MRG_REQUIRE(H == GE && HB == GHB && FO >= 1 && FO <= 16 && nl >= 1 && nl <= SL_MAXL,
               "mrg_ssd_loop_fwd: needs H = %d, HB = %d, 1 <= FO <= 16, 1 <= nl <= %d (H=%d HB=%d FO=%d nl=%d)", GE,
               GHB, SL_MAXL, H, HB, FO, nl);
   MRG_REQUIRE(lptrs && nptrs == SL_PER_LAYER * nl && P && wms && w1 && b1 && w2 && b2 && ms && mask && ring && err,
@@ -751,21 +694,18 @@ MRG_API int mrg_ssd_loop_fwd(int B, int T, int H, int HB, int FO, int F, int nl,
   SsdLoopArgs a{};
   for (int i = 0; i < nl; ++i) {
     const void* const* q = lptrs + SL_PER_LAYER * i;
-    for (int k = 0; k < SL_PER_LAYER; ++k)   // X (i > 0), mean and rstd may be null: not stored
-      MRG_REQUIRE(q[k] != nullptr || (k == 5 && i > 0) || k == 9 || k == 10, "mrg_ssd_loop_fwd: null pointer %d of layer %d",
-                  k, i);
-    MRG_REQUIRE((q[9] == nullptr) == (q[10] == nullptr), "mrg_ssd_loop_fwd: mean and rstd of layer %d: both or neither", i);
+    for (int k = 0; k < SL_PER_LAYER; ++k)
+      MRG_REQUIRE(q[k] != nullptr || (k == 5 && i > 0), "mrg_ssd_loop_fwd: null pointer %d of layer %d", k, i);
     SsdLoopLayer& L = a.L[i];
     L.w_ih = static_cast<const float*>(q[0]); L.b_ih = static_cast<const float*>(q[1]);
     L.b_hh = static_cast<const float*>(q[2]); L.ln_g = static_cast<const float*>(q[3]);
     L.ln_b = static_cast<const float*>(q[4]);
     L.X = (float*)q[5]; L.G = (float*)q[6]; L.C = (float*)q[7]; L.Hs = (float*)q[8];
-    L.mean = (float*)q[9]; L.rstd = (float*)q[10];
   }
   a.P = P; a.wms = wms; a.w1 = w1; a.b1 = b1; a.w2 = w2; a.b2 = b2;
-  a.ms = ms; a.ms_bs = ms_bs; a.ms_ts = ms_ts; a.mask = mask; a.xf_ms = xf_ms;
-  a.U = U; a.Z = Z; a.y = y; a.ring = static_cast<unsigned long long*>(ring); a.err = err;
-  a.B = B; a.T = T; a.FO = FO; a.F = F; a.nl = nl; a.ngroups = (B + GL_ROWS - 1) / GL_ROWS; a.eps = eps;
+  a.ms = ms; a.ms_bs = ms_bs; a.ms_ts = ms_ts; a.mask = mask;
+  a.ring = static_cast<unsigned long long*>(ring); a.err = err;
+  a.B = B; a.T = T; a.FO = FO; a.nl = nl; a.ngroups = (B + GL_ROWS - 1) / GL_ROWS; a.eps = eps;
   a.stamps = g_ssd_stamps;
   klaunch(ssd_loop_kernel, dim3(GL_MEM * a.ngroups), 256, 0, stream, a);
   return check_launch("ssd_loop_kernel");

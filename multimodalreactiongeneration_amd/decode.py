@@ -88,20 +88,20 @@ class _SSDecodeFn(Function):
         lw, lb = layers[-1][4], layers[-1][5]
         if _LOOP[0] and H == 256 and HB == 64 and FO <= 16 and nl <= 4 and lib.mrg_ssd_loop_fits(B, 0) == 1:
             # the loop stores the gates, c, h and X_0; the LayerNorm outputs (X_i, U) and statistics,
-            # Z, y and X_f's ms columns are formed after it (below): a store ahead of a hand-off poll
-            # delays that poll, and the row-wide ones fell on one member (ssd_loop.hip)
+            # Z, y and X_f's ms columns are formed after it (below): stored inside the loop they fell on
+            # one member, which then ran ~1.2 us behind its group at every stage (ssd_loop.hip)
             lp = []
             for i, (w_ih, _w_hh, b_ih, b_hh, g_, b_) in enumerate(layers):
-                lp += [w_ih, b_ih, b_hh, g_, b_, X[i] if i == 0 else None, G[i], C[i], Hs[i], None, None]
+                lp += [w_ih, b_ih, b_hh, g_, b_, X[i] if i == 0 else None, G[i], C[i], Hs[i]]
             lpa = (ctypes.c_void_p * len(lp))(*[_ptr(q) for q in lp])
             ring = torch.zeros(max(1, lib.mrg_ssd_loop_ring_bytes(B, nl) // 8), dtype=torch.int64, device=dev)
             # algorithmic FLOPs (bench's "ssd" family): gates 8H^2 per row and layer, FFN, the ms columns
             flop = 2.0 * T * B * (4 * H * H * nl + H * HB + HB * FO + FO * H)
             with _probe("ssd", flop):
                 _lib.check(lib.mrg_ssd_loop_fwd(
-                    B, T, H, HB, FO, F, nl, eps, lpa, len(lp), _ptr(P), _ptr(wms_t), _ptr(w1), _ptr(b1), _ptr(w2),
-                    _ptr(b2), _ptr(msc), msc.stride(0), msc.stride(1), _ptr(mask), None, None, None, None,
-                    _ptr(ring), _ptr(_err_flag(dev)), _stream()), "ssd loop fwd")
+                    B, T, H, HB, FO, nl, eps, lpa, len(lp), _ptr(P), _ptr(wms_t), _ptr(w1), _ptr(b1), _ptr(w2),
+                    _ptr(b2), _ptr(msc), msc.stride(0), msc.stride(1), _ptr(mask), _ptr(ring),
+                    _ptr(_err_flag(dev)), _stream()), "ssd loop fwd")
             rows = T * B
             for i, (_w_ih, _w_hh, _b_ih, _b_hh, g_, b_) in enumerate(layers):
                 # X_{i+1} (U after the last layer) = LN(h_i + X_i) with its statistics
