@@ -274,14 +274,15 @@ int mrg_ssd_loop_fwd(int B, int T, int H, int HB, int FO, int nl, float eps, con
  * on MFMA) and one of partial LayerNorm row sums, and the bottom layer's partial dyx feeds the
  * previous frame.  lptrs: 12 per layer (W_ih [4H][H] or null for layer 0, the LayerNorm gamma and
  * beta, the forward's X, gates, c, h, mean, rstd, then g, dG and dX (null for layer 0)); dy [B][T][FO]; v =
- * [W1 gamma | W1 beta] [HB][2]; z [T][B][HB]; vt = W_ms^T W_ih0 [FO][4H]; outputs dyt [T][B][FO], dz
- * [T][B][HB], du [T][B][H]; ring: mrg_ssd_loop_bwd_ring_bytes(B) of zeroed memory per launch.       */
+ * [W1 gamma | W1 beta] [HB][2]; z [T][B][HB]; vt = W_ms^T W_ih0 [FO][4H]; output du [T][B][H] (dy_total
+ * and dz follow from dy, dX_0 and z after the launch); ring: mrg_ssd_loop_bwd_ring_bytes(B) of zeroed
+ * memory per launch.                                                                                  */
 long mrg_ssd_loop_bwd_ring_bytes(int B);
 int mrg_ssd_loop_bwd_fits(int B, int cus);
 int mrg_ssd_loop_bwd(int B, int T, int H, int HB, int FO, int nl, const void* const* lptrs, int nptrs,
                      const float* dy, const unsigned char* mask, const float* w1, const float* w2, const float* b1,
-                     const float* v, const float* z, const float* vt, const float* wms_t, float* dyt, float* dz,
-                     float* du, void* ring, int* err, hipStream_t stream);
+                     const float* v, const float* z, const float* vt, const float* wms_t, float* du, void* ring,
+                     int* err, hipStream_t stream);
 int mrg_ssd_ffn_bwd(int B, int H, int HB, int FO, int t, const float* dy, long dy_bs, const float* dfeat_next,
                     const float* dyx_next, const float* wms_t, const unsigned char* mask, const float* w1,
                     const float* w2,

@@ -164,8 +164,8 @@ SIGNATURES = {
                                  P, c_long, c_long, P, P, P, P]),
     "mrg_ssd_loop_bwd_ring_bytes": (c_long, [c_int]),
     "mrg_ssd_loop_bwd_fits": (c_int, [c_int, c_int]),
-    "mrg_ssd_loop_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, PP, c_int, P, P, P, P, P, P, P, P, P, P, P, P,
-                                 P, P, P]),
+    "mrg_ssd_loop_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, PP, c_int, P, P, P, P, P, P, P, P, P, P, P,
+                                 P, P]),
     "mrg_ssd_ffn_z_fwd": (c_int, [c_int, c_int, c_int, P, P, P, P, c_float, P, P, P, P, P, P, P]),
     "mrg_ssd_y_fwd": (c_int, [c_int, c_int, c_int, P, P, P, P, c_long, P]),
     "mrg_ssd_ffn_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_long, P, P, P, P, P, P, P, P, P, P, P,

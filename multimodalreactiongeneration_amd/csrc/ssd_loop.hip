@@ -314,7 +314,7 @@ struct SsdBwdArgs {
   const float *w1, *w2, *b1, *v;       // FFN W1 [HB][H], W2 [FO][HB], b1, v = [W1 gamma | W1 beta] [HB][2]
   const float* z;                      // Z [T][B][HB]
   const float *vt, *wms;               // vt = W_ms^T W_ih0 [FO][4H], W_ms^T [FO][H]
-  float *dyt, *dz, *du;                // [T][B][FO], [T][B][HB], [T][B][H]
+  float* du;                           // [T][B][H]
   unsigned long long* ring;            // 2 x (partials [B][16][256] | sums [B][16][2]) | dyx [B][256] granules, XCC slots
   int* err;
   int B, T, FO, nl, ngroups;
@@ -549,7 +549,6 @@ __global__ __launch_bounds__(256) void ssd_loop_bwd_kernel(SsdBwdArgs p) {
         for (int jm = 0; jm < GL_MEM; ++jm) dyx += A[m8][16 * jm + n16];
         const float v = dyv ? dyin + (fed ? dyx : 0.0f) : 0.0f;
         dys[m8][n16] = v;
-        if (j == 0 && dyv) defer(0, p.dyt + (rt + b8) * FO + n16, v);
       }
       __syncthreads();
       float m0 = 0.0f, m1 = 0.0f;
@@ -562,7 +561,6 @@ __global__ __launch_bounds__(256) void ssd_loop_bwd_kernel(SsdBwdArgs p) {
         for (int o = 0; o < 16; ++o) acc = fmaf(dys[mz][o], w2s[o][jh], acc);
         const float d = zv > 0.0f ? acc : 0.0f;
         dzs[mz][jh] = d;
-        if (j == 0 && r0 + mz < B) defer(1 + i, p.dz + (rt + r0 + mz) * GHB + jh, d);
         m0 = fmaf(d, hv1[jh], m0);
         m1 = fmaf(d, (zv - hb1[jh]) - hv2[jh], m1);
       }
@@ -737,18 +735,20 @@ MRG_API int mrg_ssd_loop_bwd_fits(int B, int cus) {
 // LayerNorm after the layer, the forward's saved X, gates, c, h and that LayerNorm's mean / rstd, then
 // the outputs g = d(h + x) [T][B][H], dG [T][B][4H] and dX [T][B][H] (layers >= 1; null for layer 0).
 // dy [B][T][FO]; mask [T] bytes; w1 [HB][H], w2 [FO][HB], b1, v = [W1 gamma | W1 beta] [HB][2] of the
-// last LayerNorm; z [T][B][HB]; vt = W_ms^T W_ih0 [FO][4H]; wms_t [FO][H]; outputs dyt [T][B][FO],
-// dz [T][B][HB], du [T][B][H]; ring: mrg_ssd_loop_bwd_ring_bytes of zeroed memory; err as the forward's.
+// last LayerNorm; z [T][B][HB]; vt = W_ms^T W_ih0 [FO][4H]; wms_t [FO][H]; output du [T][B][H] (the
+// last LayerNorm's upstream gradient, for its parameters); ring: mrg_ssd_loop_bwd_ring_bytes of zeroed
+// memory; err as the forward's.  The prediction gradient through the select (dy_total) and dz are
+// not written: they follow from dy, dfeat = dX_0 and z after the loop (decode.py).
 MRG_API int mrg_ssd_loop_bwd(int B, int T, int H, int HB, int FO, int nl, const void* const* lptrs, int nptrs,
                              const float* dy, const unsigned char* mask, const float* w1, const float* w2,
                              const float* b1, const float* v, const float* z, const float* vt, const float* wms_t,
-                             float* dyt, float* dz, float* du, void* ring, int* err, hipStream_t stream) {
+                             float* du, void* ring, int* err, hipStream_t stream) {
   if (B == 0 || T == 0) return 0;
   MRG_REQUIRE(H == GE && HB == GHB && FO >= 1 && FO <= 16 && nl >= 2 && nl <= SL_MAXL,
               "mrg_ssd_loop_bwd: needs H = %d, HB = %d, 1 <= FO <= 16, 2 <= nl <= %d (H=%d HB=%d FO=%d nl=%d)", GE,
               GHB, SL_MAXL, H, HB, FO, nl);
-  MRG_REQUIRE(lptrs && nptrs == SB_PER_LAYER * nl && dy && mask && w1 && w2 && b1 && v && z && vt && wms_t && dyt &&
-                  dz && du && ring && err,
+  MRG_REQUIRE(lptrs && nptrs == SB_PER_LAYER * nl && dy && mask && w1 && w2 && b1 && v && z && vt && wms_t && du &&
+                  ring && err,
               "mrg_ssd_loop_bwd: null argument or nptrs %d != %d", nptrs, SB_PER_LAYER * nl);
   MRG_REQUIRE(mrg_ssd_loop_bwd_fits(B, 0) == 1, "mrg_ssd_loop_bwd: %d workgroups cannot all be resident (B=%d)",
               GL_MEM * ((B + GL_ROWS - 1) / GL_ROWS), B);
@@ -768,7 +768,7 @@ MRG_API int mrg_ssd_loop_bwd(int B, int T, int H, int HB, int FO, int nl, const 
     L.g = (float*)q[9]; L.dG = (float*)q[10]; L.dX = (float*)q[11];
   }
   a.dy = dy; a.mask = mask; a.w1 = w1; a.w2 = w2; a.b1 = b1; a.v = v; a.z = z; a.vt = vt; a.wms = wms_t;
-  a.dyt = dyt; a.dz = dz; a.du = du; a.ring = static_cast<unsigned long long*>(ring); a.err = err;
+  a.du = du; a.ring = static_cast<unsigned long long*>(ring); a.err = err;
   a.B = B; a.T = T; a.FO = FO; a.nl = nl; a.ngroups = (B + GL_ROWS - 1) / GL_ROWS;
   a.stamps = g_ssd_bwd_stamps;
   klaunch(ssd_loop_bwd_kernel, dim3(GL_MEM * a.ngroups), 256, 0, stream, a);

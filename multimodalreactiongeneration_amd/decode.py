@@ -203,8 +203,8 @@ class _SSDecodeFn(Function):
             with _probe("ssd", flop):
                 _lib.check(lib.mrg_ssd_loop_bwd(
                     B, T, H, HB, FO, nl, lpa, len(lp), _ptr(dy), _ptr(mask), _ptr(w1), _ptr(w2), _ptr(b1), _ptr(v),
-                    _ptr(Z), _ptr(vt), _ptr(wms_t), _ptr(dyt), _ptr(dz), _ptr(duL), _ptr(ring),
-                    _ptr(_err_flag(dev)), _stream()), "ssd loop bwd")
+                    _ptr(Z), _ptr(vt), _ptr(wms_t), _ptr(duL), _ptr(ring), _ptr(_err_flag(dev)), _stream()),
+                    "ssd loop bwd")
         for t in (range(T - 1, -1, -1) if not loop else ()):
             for i in range(nl - 1, -1, -1):
                 cell = (_ptr(gs[i], t * slab), _ptr(G[i], t * gslab), _ptr(C[i], t * slab), _ptr(dG[i], t * gslab))
@@ -233,6 +233,16 @@ class _SSDecodeFn(Function):
         if ext:  # every frame's dfeat = dG0 W_ih0 + g0 in one GEMM
             gemm(T * B, H, 4 * H, _ptr(dG[0]), 0, 4 * H, _ptr(layers[0][0]), 0, H, _ptr(dX[0]), H, epi=3,
                  aux=_ptr(gs[0]), ldaux=H, device=dev)
+        if loop:
+            # dy_total(t) = dy(t) + mask[t] dfeat(t+1) W_ms and dz = relu'(z) (dy_total W2), formed here
+            # from dX_0 (the loop keeps them in registers: stored by one member they held it back)
+            dyx = torch.empty(T, B, FM, device=dev, dtype=F32)
+            gemm(rows, FM, H, _ptr(dX[0]), 0, H, _ptr(wms_t), 1, H, _ptr(dyx), FM, device=dev)
+            dyt.copy_(dy.transpose(0, 1))
+            if T > 1:
+                dyt[:-1].add_(dyx[1:] * mask[:-1].to(F32)[:, None, None])
+            gemm(rows, HB, FO, _ptr(dyt), 0, FO, _ptr(w2), 0, HB, _ptr(dz), HB, device=dev)
+            dz.mul_(Z > 0)
         # weight gradients over all T * B rows
         for i, (w_ih, w_hh, b_ih, b_hh, lw, lb) in enumerate(layers):
             _wgrad(_ptr(dG[i]), 4 * H, _ptr(X[i]), H, rows, 4 * H, H, _gbuf(w_ih), dev, gb=_gbuf(b_ih),
