@@ -43,7 +43,7 @@ struct SsdLoopArgs {
   int* err;
   int B, T, FO, nl, ngroups;
   float eps;
-  unsigned long long* stamps;     // diagnostics (mrg_ssd_loop_debug_stamps): [T][16] of block 0, or null
+  unsigned long long* stamps;     // diagnostics (mrg_ssd_loop_debug_stamps): [T][16][16] of row group 0, or null
 };
 
 // thread 0 of each member of group 0: 100 MHz real-time stamp (s_memrealtime: one clock for every CU)
@@ -318,7 +318,7 @@ struct SsdBwdArgs {
   unsigned long long* ring;            // 2 x (partials [B][16][256] | sums [B][16][2]) | dyx [B][256] granules, XCC slots
   int* err;
   int B, T, FO, nl, ngroups;
-  unsigned long long* stamps;          // diagnostics (mrg_ssd_loop_bwd_debug_stamps), or null
+  unsigned long long* stamps;          // diagnostics (mrg_ssd_loop_bwd_debug_stamps): [T][16][16] of row group 0, or null
 };
 
 #define SB_STAMP(slot)                                                                   \
