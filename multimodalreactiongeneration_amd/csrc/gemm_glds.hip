@@ -43,6 +43,25 @@ __device__ __forceinline__ float lds_read4(unsigned addr) {
   return v;
 }
 
+// 8 ds_read_b32 at addr + (K0 + j) * ROWB, j = 0..7 (immediate offsets: one address register for the
+// eight k-rows of a weight-gradient fragment); the caller waits lgkmcnt
+template <int ROWB, int K0>
+__device__ __forceinline__ void lds_read8k(unsigned addr, float (&v)[8]) {
+  asm volatile(
+      "ds_read_b32 %0, %8 offset:%9\n\t"
+      "ds_read_b32 %1, %8 offset:%10\n\t"
+      "ds_read_b32 %2, %8 offset:%11\n\t"
+      "ds_read_b32 %3, %8 offset:%12\n\t"
+      "ds_read_b32 %4, %8 offset:%13\n\t"
+      "ds_read_b32 %5, %8 offset:%14\n\t"
+      "ds_read_b32 %6, %8 offset:%15\n\t"
+      "ds_read_b32 %7, %8 offset:%16"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7])
+      : "v"(addr), "n"(K0 * ROWB), "n"((K0 + 1) * ROWB), "n"((K0 + 2) * ROWB), "n"((K0 + 3) * ROWB),
+        "n"((K0 + 4) * ROWB), "n"((K0 + 5) * ROWB), "n"((K0 + 6) * ROWB), "n"((K0 + 7) * ROWB)
+      : "memory");
+}
+
 // 8 consecutive-k fp32 -> three bf16x8 planes (v = p0 + p1 + p2 + r, |r| <= 2^-24 |v|)
 __device__ __forceinline__ void split8(f32x4v_ v0, f32x4v_ v1, bf16x8 (&f)[3]) {
   unsigned a0, a1, a2, b0, b1, b2, c0, c1, c2, d0, d1, d2;
@@ -375,6 +394,19 @@ __device__ __forceinline__ void wgrad_tile(const GemmArgs& a, int t, unsigned ch
   const bool do_asum = a.asum && n0 == 0 && (wave & 1) == 0;
   float cs[TM] = {};
   const unsigned lds_base = (unsigned)(uintptr_t)((__attribute__((address_space(3))) unsigned char*)lds);
+  // a fragment's k-rows 16 s + 8 lh + j share the chunk swizzle of row 8 lh ((k >> 3) & 1 = lh), so
+  // each fragment is one lane address (k-row 8 lh) plus immediate row offsets
+  unsigned oa[TM], ob[TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = wm + 32 * i + lr;
+    oa[i] = wg_off<BM>(8 * lh, m >> 2) + 4 * (m & 3);
+  }
+#pragma unroll
+  for (int jj = 0; jj < TN; ++jj) {
+    const int n = wn + 32 * jj + lr;
+    ob[jj] = SA + wg_off<BN>(8 * lh, n >> 2) + 4 * (n & 3);
+  }
 
 #pragma unroll
   for (int st = 0; st < NS - 1; ++st)
@@ -387,21 +419,18 @@ __device__ __forceinline__ void wgrad_tile(const GemmArgs& a, int t, unsigned ch
     __builtin_amdgcn_s_barrier();
     if (kt + NS - 1 < nk) issue(kt + NS - 1, (kt + NS - 1) % NS);
     const unsigned sa = lds_base + (kt % NS) * SS;
-    const unsigned sb = sa + SA;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       float va[TM][8], vb[TN][8];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const int m = wm + 32 * i + lr;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) va[i][j] = lds_read4(sa + wg_off<BM>(16 * s + 8 * lh + j, m >> 2) + 4 * (m & 3));
+        if (s == 0) lds_read8k<BM * 4, 0>(sa + oa[i], va[i]);
+        else lds_read8k<BM * 4, 16>(sa + oa[i], va[i]);
       }
 #pragma unroll
       for (int jj = 0; jj < TN; ++jj) {
-        const int n = wn + 32 * jj + lr;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) vb[jj][j] = lds_read4(sb + wg_off<BN>(16 * s + 8 * lh + j, n >> 2) + 4 * (n & 3));
+        if (s == 0) lds_read8k<BN * 4, 0>(sa + ob[jj], vb[jj]);
+        else lds_read8k<BN * 4, 16>(sa + ob[jj], vb[jj]);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);

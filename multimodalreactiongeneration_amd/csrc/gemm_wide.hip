@@ -23,6 +23,7 @@
 //   kt + NS - 1 into the slot read in the previous k-tile -> A fragment, split -> per block: its three
 //   B plane fragments (issued one block ahead) and six MFMAs.
 #include "gemm_common.h"
+#include <utility>
 
 namespace mrg {
 
@@ -40,6 +41,26 @@ __device__ __forceinline__ f32x4w wlds16(unsigned addr) {
   f32x4w v;
   asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr) : "memory");
   return v;
+}
+
+// the same read at addr + OFF (immediate offset: the fragment reads of one k-tile share one address)
+template <int OFF>
+__device__ __forceinline__ f32x4w wlds16o(unsigned addr) {
+  f32x4w v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "n"(OFF) : "memory");
+  return v;
+}
+
+// B plane P of block j (a constant once the block loop is unrolled): offset P SBP + 1024 j
+template <int P, int SBP, int... J>
+__device__ __forceinline__ f32x4w wlds16o_sel(unsigned addr, int j, std::integer_sequence<int, J...>) {
+  f32x4w v{};
+  ((j == J ? (void)(v = wlds16o<P * SBP + 1024 * J>(addr)) : (void)0), ...);
+  return v;
+}
+template <int P, int SBP, int NB>
+__device__ __forceinline__ f32x4w wlds16o_j(unsigned addr, int j) {
+  return wlds16o_sel<P, SBP>(addr, j, std::make_integer_sequence<int, NB>{});
 }
 
 // 8 fp32 -> three bf16x8 planes (the x6 split of gemm_common.h, RNE)
@@ -122,6 +143,9 @@ __global__ __launch_bounds__(256, 2) void gemm_x6w_kernel(GemmArgs a_in, long bp
   const unsigned lds_base = (unsigned)(uintptr_t)((__attribute__((address_space(3))) unsigned char*)lds);
   const int ar = 16 * wave + (lane & 15), ac = 2 * (lane >> 4);   // A fragment row, first chunk
   const int bc = lane >> 4;                                        // B fragment chunk
+  // fragment offsets in a slot: A's two chunks; B block j plane p at ob + p SBP + 1024 j (wb_off's
+  // swizzle bit (n >> 3) & 1 is the same for rows 16 j + (lane & 15) of every block)
+  const unsigned oa0 = wa_off(ar, ac), oa1 = wa_off(ar, ac + 1), ob = SA + wb_off(lane & 15, bc);
 
   f32x4w acc[NB];
 #pragma unroll
@@ -138,11 +162,12 @@ __global__ __launch_bounds__(256, 2) void gemm_x6w_kernel(GemmArgs a_in, long bp
     __builtin_amdgcn_s_barrier();
     if (kt + NS - 1 < nk) issue(kt + NS - 1, (kt + NS - 1) % NS);
     const unsigned sa = lds_base + (kt % NS) * SS;
-    const unsigned sb = sa + SA;
-    f32x4w va0 = wlds16(sa + wa_off(ar, ac)), va1 = wlds16(sa + wa_off(ar, ac + 1));
+    const unsigned sb = sa + ob;
+    f32x4w va0 = wlds16(sa + oa0), va1 = wlds16(sa + oa1);
     f32x4w vb[2][3];
-#pragma unroll
-    for (int p = 0; p < 3; ++p) vb[0][p] = wlds16(sb + p * SBP + wb_off(lane & 15, bc));
+    vb[0][0] = wlds16o<0>(sb);
+    vb[0][1] = wlds16o<SBP>(sb);
+    vb[0][2] = wlds16o<2 * SBP>(sb);
     asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(va0), "+v"(va1)::"memory");
     bf16x8 fa[3];
     wsplit8(va0, va1, fa);
@@ -150,8 +175,9 @@ __global__ __launch_bounds__(256, 2) void gemm_x6w_kernel(GemmArgs a_in, long bp
     for (int j = 0; j < NB; ++j) {
       const int cur = j & 1, nxt = cur ^ 1;
       if (j + 1 < NB) {
-#pragma unroll
-        for (int p = 0; p < 3; ++p) vb[nxt][p] = wlds16(sb + p * SBP + wb_off(16 * (j + 1) + (lane & 15), bc));
+        vb[nxt][0] = wlds16o_j<0, SBP, NB>(sb, j + 1);
+        vb[nxt][1] = wlds16o_j<1, SBP, NB>(sb, j + 1);
+        vb[nxt][2] = wlds16o_j<2, SBP, NB>(sb, j + 1);
         asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(vb[cur][0]), "+v"(vb[cur][1]), "+v"(vb[cur][2])::"memory");
       } else {
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vb[cur][0]), "+v"(vb[cur][1]), "+v"(vb[cur][2])::"memory");
