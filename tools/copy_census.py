@@ -33,10 +33,12 @@ class Census(TorchDispatchMode):
     def __init__(self):
         super().__init__()
         self.count = Counter()
+        self.every = Counter()   # every op seen, by name (skipped ones included)
 
     def __torch_dispatch__(self, func, types, args=(), kwargs=None):
         out = func(*args, **(kwargs or {}))
         name = func.overloadpacket.__name__
+        self.every[name] += 1
         if name in SKIP:
             return out
         outs = out if isinstance(out, (tuple, list)) else (out,)
@@ -72,7 +74,7 @@ def main():
         step()
     torch.cuda.synchronize()
     total = sum(cen.count.values())
-    print(f"{total} torch-launched ATen ops in one step", flush=True)
+    print(f"{total} torch-launched ATen ops in one step; every op seen: {dict(cen.every)}", flush=True)
     for (name, where), n in sorted(cen.count.items(), key=lambda kv: -kv[1]):
         print(f"{n:5d}  {name:28s} {where}", flush=True)
 
