@@ -4,7 +4,8 @@
 # workload (graph replayed) -> trace roofline summary, FETCH_SIZE / WRITE_SIZE passes over one eager
 # step -> PMC summary.  Every GPU step has its own limit; the script stops at the first failure.
 # PART=1: GPU tests + smoke; PART=2: bench, trace, PMC, stamps; PART=3: kernel census of the C3 step
-# and of generation (tools/c3_census.py under rocprofv3).
+# and of generation (tools/c3_census.py under rocprofv3); PART=4: the final set (tests, smoke, trace
+# installed as the committed trace summary, then the bench line that checks against it).
 set -o pipefail
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
@@ -12,6 +13,30 @@ TAG=${1:-v1}
 O=$R/gpurun_out/r06_$TAG
 mkdir -p $O
 cd $R
+if [ "${PART:-1}" = "4" ]; then
+# final set: GPU tests + smoke, then the kernel trace FIRST, its summary installed as the committed
+# profiles/r06_trace_roofline.json that the bench line's trace_check reads, then the default bench line
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread \
+  > $O/gpu_tests.log 2>&1 || { tail -30 $O/gpu_tests.log; exit 1; }
+tail -1 $O/gpu_tests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+cd /tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- \
+  python3 $R/bench.py --steps 5 --warmup 2 --cpu-baseline 0 --secondary 0 > $O/trace.log 2>&1 \
+  || { echo "trace failed"; tail -20 $O/trace.log; exit 1; }
+cd $R
+T=$(ls $O/trace/*/run_kernel_trace.csv $O/trace/run_kernel_trace.csv 2>/dev/null | head -1)
+python3 tools/tools_trace_roofline.py $T $O/trace_roofline.json > /dev/null
+cp $O/trace_roofline.json profiles/r06_trace_roofline.json
+python3 tools/tools_timeline.py $T 2 > $O/timeline.txt
+S=$(ls $O/trace/*/run_kernel_stats.csv $O/trace/run_kernel_stats.csv 2>/dev/null | head -1)
+python3 tools/tools_prof_summary.py $S > $O/kernel_summary.txt 2>/dev/null || cp $S $O/kernel_stats.csv
+echo "trace ok"
+timeout -k 10 600 python bench.py > $O/bench.json.log 2>&1 || { tail -20 $O/bench.json.log; exit 1; }
+grep -o '"ms_per_step": [0-9.]*' $O/bench.json.log | tail -1
+exit 0
+fi
 if [ "${PART:-1}" = "3" ]; then
 cd /tmp
 for w in c3 gen; do
