@@ -21,9 +21,9 @@ int mrg_gemm_set_glds(int depth, int bn);
 /* Weight-gradient products (transA 1, transB 0) on the LDS-DMA kernel (1, default) or the
  * register-staged one (0); returns the previous setting.                                        */
 int mrg_gemm_set_glds_wg(int on);
-/* Kernel of mrg_gemm_x6_planes: 0 = gemm_x6g_kernel (pre-split B, 32 x 32 blocks), 10 * (bn / 64) + ns =
- * gemm_x6w_kernel (gemm_wide.hip: row-owning waves, bn columns per tile, ring depth ns); env
- * MRG_GEMM_WIDE; returns the previous setting.                                                      */
+/* Kernel of mrg_gemm_x6_planes: 0 = gemm_x6g_kernel (pre-split B, 32 x 32 blocks), 12 / 22 =
+ * gemm_x6w_kernel (gemm_wide.hip: row-owning waves, 64 / 128 columns per tile, ring depth 2); env
+ * MRG_GEMM_WIDE; other values are ignored; returns the previous setting.                            */
 int mrg_gemm_set_wide(int cfg);
 /* Attention backward form: 1 (default, MRG_ATTN_FUSED) = the single-pass kernel (one workgroup per
  * (sample, head); D = 64, Tq <= 320, 16-B rows) where it applies, 0 = always the two-pass dQ, dK / dV

@@ -620,7 +620,8 @@ using namespace mrg;
 
 static int g_wide_cfg = [] {
   const char* e = getenv("MRG_GEMM_WIDE");
-  return e ? atoi(e) : 12;
+  const int v = e ? atoi(e) : 12;
+  return (v == 0 || v == 22) ? v : 12;
 }();
 
 // planes of n weights (see split_planes_kernel): dst_i holds 3 x rows_i x cols_i bf16
@@ -722,11 +723,11 @@ MRG_API int mrg_gemm_x6_planes_batched(int n, int M, int N, int K, float alpha, 
   return check_launch("gemm_x6w_kernel (batched)");
 }
 
-// Tuning: which kernel mrg_gemm_x6_planes runs (0 = gemm_x6g_kernel with pre-split B; 10 * (bn / 64) + ns =
-// gemm_x6w_kernel with bn columns and ring depth ns); returns the previous setting.
+// Tuning: which kernel mrg_gemm_x6_planes runs (0 = gemm_x6g_kernel with pre-split B; 12 / 22 =
+// gemm_x6w_kernel with 64 / 128 columns); returns the previous setting.
 MRG_API int mrg_gemm_set_wide(int cfg) {
   const int prev = g_wide_cfg;
-  if (cfg == 0 || cfg == 12 || cfg == 13 || cfg == 22 || cfg == 23 || cfg == 42)
+  if (cfg == 0 || cfg == 12 || cfg == 22)
     g_wide_cfg = cfg;
   return prev;
 }

@@ -218,20 +218,15 @@ static void launch_w(GemmArgs a, long bplane, hipStream_t s, const GemmBatch& gb
   klaunch(gemm_x6w_kernel<BN, NS>, grid, NT, 0, s, a, bplane, gb);
 }
 
-// config: bn in {64, 128, 256}, ns in {2, 3}
+// config: bn in {64, 128}, ring depth 2 (depth 3 and 256-wide tiles measured slower in the step and
+// were removed: profiles/r06_knobs_ab.txt)
 void launch_x6w(GemmArgs a, int bn, int ns, long bplane, hipStream_t s, const GemmBatch* gbp) {
+  (void)ns;
   GemmBatch none;
   none.n = 0;
   const GemmBatch& gb = gbp ? *gbp : none;
-  if (bn == 64) {
-    if (ns == 3) launch_w<64, 3>(a, bplane, s, gb);
-    else launch_w<64, 2>(a, bplane, s, gb);
-  } else if (bn == 256) {
-    launch_w<256, 2>(a, bplane, s, gb);
-  } else {
-    if (ns == 3) launch_w<128, 3>(a, bplane, s, gb);
-    else launch_w<128, 2>(a, bplane, s, gb);
-  }
+  if (bn == 64) launch_w<64, 2>(a, bplane, s, gb);
+  else launch_w<128, 2>(a, bplane, s, gb);
 }
 
 }  // namespace mrg

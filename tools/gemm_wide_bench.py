@@ -77,4 +77,4 @@ def main(cfgs):
 
 
 if __name__ == "__main__":
-    main([int(c) for c in sys.argv[1:]] or [12, 13, 22, 23, 42])
+    main([int(c) for c in sys.argv[1:]] or [12, 22])
