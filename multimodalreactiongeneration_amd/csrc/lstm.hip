@@ -43,8 +43,6 @@
 
 namespace mrg {
 
-typedef float lf2 __attribute__((ext_vector_type(2)));  // output pairs of the backward GEMV (v_pk_fma_f32)
-
 // Threads per workgroup and resident workgroups per CU for a (hidden size, group size):
 //   H = 256, G = 8  : 512 threads (64 W_hh values per lane), 2 workgroups per CU
 //   H = 256, G = 16 : 256 threads (64 W_hh values per lane), 4 workgroups per CU
@@ -265,19 +263,15 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
   const int b0 = grp * BS;
   bool dead = false;
 
-  // dot role: w[o][i] = W_hh[grow(rc*RL + i)][ogr*OT + o], held as output pairs (o, o + 1) so the
-  // GEMV runs on v_pk_fma_f32 (two outputs per instruction, each output's sum in the same order)
+  // dot role: w[o][i] = W_hh[grow(rc*RL + i)][ogr*OT + o]
   const int ogr = tid / RC, rc = tid % RC;
-  constexpr int OP = (OT + 1) / 2;   // pairs (an odd OT's last pair carries a zero second output)
-  lf2 w[OP][RL];
+  float w[OT][RL];
 #pragma unroll
   for (int i = 0; i < RL; ++i) {
     const int rr = rc * RL + i;
     const int grow = (rr / U) * H + j * U + (rr % U);
 #pragma unroll
-    for (int o = 0; o < OT; o += 2)
-      w[o / 2][i] = lf2{P.w_hh[(long)grow * H + ogr * OT + o],
-                        o + 1 < OT ? P.w_hh[(long)grow * H + ogr * OT + o + 1] : 0.0f};
+    for (int o = 0; o < OT; ++o) w[o][i] = P.w_hh[(long)grow * H + ogr * OT + o];
   }
 
   const bool cell = tid < BS * U;
@@ -381,24 +375,21 @@ __global__ __launch_bounds__((LstmNT<H, G>::value), (LstmNT<H, G>::waves_per_sim
       const int par = tt & 1;
 #pragma unroll
       for (int b = 0; b < BS; ++b) {  // one batch row at a time: short live ranges
-        lf2 acc2[OP];
+        float acc[OT];
 #pragma unroll
-        for (int o = 0; o < OP; ++o) acc2[o] = lf2{0.0f, 0.0f};
+        for (int o = 0; o < OT; ++o) acc[o] = 0.0f;
         const float* dp = &dgl[b][rc][0];
 #pragma unroll
         for (int i = 0; i < RL; i += 4) {
           float4 dv = *reinterpret_cast<const float4*>(dp + i);
 #pragma unroll
-          for (int o = 0; o < OP; ++o) {
-            acc2[o] = __builtin_elementwise_fma(lf2{dv.x, dv.x}, w[o][i], acc2[o]);
-            acc2[o] = __builtin_elementwise_fma(lf2{dv.y, dv.y}, w[o][i + 1], acc2[o]);
-            acc2[o] = __builtin_elementwise_fma(lf2{dv.z, dv.z}, w[o][i + 2], acc2[o]);
-            acc2[o] = __builtin_elementwise_fma(lf2{dv.w, dv.w}, w[o][i + 3], acc2[o]);
+          for (int o = 0; o < OT; ++o) {
+            acc[o] = fmaf(dv.x, w[o][i], acc[o]);
+            acc[o] = fmaf(dv.y, w[o][i + 1], acc[o]);
+            acc[o] = fmaf(dv.z, w[o][i + 2], acc[o]);
+            acc[o] = fmaf(dv.w, w[o][i + 3], acc[o]);
           }
         }
-        float acc[OT];
-#pragma unroll
-        for (int o = 0; o < OT; ++o) acc[o] = acc2[o / 2][o & 1];
         if (b == 0) MRG_STAMP(4);
 #pragma unroll
         for (int o = 0; o < OT; ++o) acc[o] = group_sum<RC>(acc[o]);
